@@ -1,0 +1,153 @@
+"""ctypes binding of libdsx.so (the C-ABI declared in include/dsx.h).
+
+The library is built in-tree (``depthestimation_amd/libdsx.so``, see ``__graft_entry__.build``).
+There is no CPU fallback: if the library cannot be loaded, or no HIP device is present when a
+matcher is first used, the product raises ``RuntimeError`` (the reference equally fails hard
+when cv2's native matcher is unavailable: ``import cv2`` at depthlib/stereo_core.py:1).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("DSX_LIB", os.path.join(_HERE, "libdsx.so"))
+
+DSX_OK = 0
+DSX_EINVAL = -1
+DSX_EHIP = -2
+DSX_ECOMM = -3
+DSX_ENOMEM = -4
+
+COST = {"sad": 0, "ssd": 1}
+FLOAT_MODE = {"fixed": 0, "parabola": 1}
+PATH = {"fused": 0, "volume": 1}
+
+# Every symbol include/dsx.h declares (checked by tests/test_abi.py against the header).
+EXPORTS = (
+    "dsx_version", "dsx_device_count", "dsx_default_params", "dsx_check_params", "dsx_create",
+    "dsx_set_params", "dsx_compute_host", "dsx_compute_device", "dsx_right_map_device",
+    "dsx_kernel_times", "dsx_reset_times", "dsx_workspace_bytes", "dsx_destroy", "dsx_last_error",
+)
+
+
+class DsxParams(ctypes.Structure):
+    _fields_ = [
+        ("min_disp", ctypes.c_int32),
+        ("num_disp", ctypes.c_int32),
+        ("block_size", ctypes.c_int32),
+        ("cost", ctypes.c_int32),
+        ("uniqueness_ratio", ctypes.c_int32),
+        ("disp12_max_diff", ctypes.c_int32),
+        ("subpixel", ctypes.c_int32),
+        ("float_mode", ctypes.c_int32),
+        ("path", ctypes.c_int32),
+        ("timing", ctypes.c_int32),
+        ("reserved", ctypes.c_int32 * 6),
+    ]
+
+
+_lib = None
+_lock = threading.Lock()
+
+
+def _bind(lib):
+    vp, i32, i64 = ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64
+    P = ctypes.POINTER(DsxParams)
+    sig = {
+        "dsx_version": (ctypes.c_int, []),
+        "dsx_device_count": (ctypes.c_int, [ctypes.POINTER(ctypes.c_int)]),
+        "dsx_default_params": (None, [P]),
+        "dsx_check_params": (ctypes.c_int, [P]),
+        "dsx_create": (ctypes.c_int, [ctypes.c_int, P, ctypes.POINTER(vp)]),
+        "dsx_set_params": (ctypes.c_int, [vp, P]),
+        "dsx_compute_host": (ctypes.c_int, [vp, vp, vp, i32, i32, i64, vp, vp]),
+        "dsx_compute_device": (ctypes.c_int, [vp, vp, vp, i32, i32, i64, vp, vp, vp]),
+        "dsx_right_map_device": (ctypes.c_int, [vp, vp, vp, i32, i32, i64, vp, vp]),
+        "dsx_kernel_times": (ctypes.c_int, [vp, ctypes.c_char_p, ctypes.c_int, ctypes.POINTER(ctypes.c_float),
+                                             ctypes.POINTER(ctypes.c_int), ctypes.c_int, ctypes.POINTER(ctypes.c_int)]),
+        "dsx_reset_times": (ctypes.c_int, [vp]),
+        "dsx_workspace_bytes": (ctypes.c_int, [vp, ctypes.POINTER(ctypes.c_int64)]),
+        "dsx_destroy": (ctypes.c_int, [vp]),
+        "dsx_last_error": (ctypes.c_char_p, []),
+    }
+    for name, (res, args) in sig.items():
+        f = getattr(lib, name)
+        f.restype = res
+        f.argtypes = args
+    return lib
+
+
+def lib():
+    """Load (once) and return the ctypes handle of libdsx.so; RuntimeError if unavailable."""
+    global _lib
+    if _lib is None:
+        with _lock:
+            if _lib is None:
+                if not os.path.exists(LIB_PATH):
+                    raise RuntimeError(
+                        f"libdsx.so not found at {LIB_PATH}: build it with "
+                        "`python -c 'import __graft_entry__ as g; g.build()'` (no CPU fallback)")
+                try:
+                    _lib = _bind(ctypes.CDLL(LIB_PATH))
+                except OSError as e:  # pragma: no cover - depends on the image
+                    raise RuntimeError(f"cannot load {LIB_PATH}: {e}") from e
+    return _lib
+
+
+def last_error() -> str:
+    msg = lib().dsx_last_error()
+    return msg.decode() if msg else ""
+
+
+def check(rc: int, what: str = "dsx") -> None:
+    """Map a DSX_E* code onto the reference's error behaviour: ValueError for bad arguments
+    (stereo_core.py:106-109 raises ValueError for bad params), RuntimeError otherwise."""
+    if rc == DSX_OK:
+        return
+    msg = f"{what}: {last_error() or 'error ' + str(rc)}"
+    if rc == DSX_EINVAL:
+        raise ValueError(msg)
+    if rc == DSX_ENOMEM:
+        raise MemoryError(msg)
+    raise RuntimeError(msg)
+
+
+def default_params() -> DsxParams:
+    p = DsxParams()
+    lib().dsx_default_params(ctypes.byref(p))
+    return p
+
+
+def make_params(min_disp=0, num_disp=128, block_size=5, cost="sad", uniqueness_ratio=10,
+                disp12_max_diff=1, subpixel=True, float_mode="fixed", path="fused",
+                timing=False) -> DsxParams:
+    p = default_params()
+    p.min_disp = int(min_disp)
+    p.num_disp = int(num_disp)
+    p.block_size = int(block_size)
+    if cost not in COST:
+        raise ValueError(f"cost must be one of {list(COST)}")
+    p.cost = COST[cost]
+    p.uniqueness_ratio = int(uniqueness_ratio)
+    p.disp12_max_diff = int(disp12_max_diff)
+    p.subpixel = int(bool(subpixel))
+    if float_mode not in FLOAT_MODE:
+        raise ValueError(f"float_mode must be one of {list(FLOAT_MODE)}")
+    p.float_mode = FLOAT_MODE[float_mode]
+    if path not in PATH:
+        raise ValueError(f"path must be one of {list(PATH)}")
+    p.path = PATH[path]
+    p.timing = int(bool(timing))
+    return p
+
+
+def check_params(p: DsxParams) -> None:
+    check(lib().dsx_check_params(ctypes.byref(p)), "dsx_check_params")
+
+
+def device_count() -> int:
+    n = ctypes.c_int(0)
+    check(lib().dsx_device_count(ctypes.byref(n)), "dsx_device_count")
+    return n.value

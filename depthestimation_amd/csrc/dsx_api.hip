@@ -1,0 +1,468 @@
+// C-ABI implementation of include/dsx.h: matcher handles, device buffer cache, pass
+// sequencing and per-kernel HIP-event timing.  The reference equivalents are cited in dsx.h.
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/dsx.h"
+#include "dsx_internal.h"
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string &msg) {
+    g_err = msg;
+    return code;
+}
+
+#define DSX_HIP(expr)                                                                       \
+    do {                                                                                    \
+        hipError_t e_ = (expr);                                                             \
+        if (e_ != hipSuccess)                                                               \
+            return fail(e_ == hipErrorOutOfMemory ? DSX_ENOMEM : DSX_EHIP,                  \
+                        std::string(#expr) + ": " + hipGetErrorString(e_));                 \
+    } while (0)
+
+int bits_for(int n) {  // smallest b with (1 << b) >= n
+    int b = 0;
+    while ((1 << b) < n) ++b;
+    return b < 1 ? 1 : b;
+}
+
+// Dp = TX * TPP, Dp a multiple of 64 (whole waves, one lane per disparity).
+bool pick_geometry(int D, dsx::Geometry &g) {
+    static const int table[][3] = {{64, 32, 2}, {128, 32, 4}, {192, 48, 4}, {256, 32, 8}, {384, 48, 8}, {512, 32, 16}};
+    for (auto &t : table) {
+        if (D <= t[0]) {
+            g.Dp = t[0];
+            g.TX = t[1];
+            g.TPP = t[2];
+            g.DB = bits_for(g.Dp);
+            return true;
+        }
+    }
+    return false;
+}
+
+uint64_t max_cost(const dsx_params &p) {
+    const uint64_t n = (uint64_t)p.block_size * p.block_size;
+    return n * (p.cost == DSX_COST_SSD ? 255ull * 255ull : 255ull);
+}
+
+int check(const dsx_params *p) {
+    if (!p) return fail(DSX_EINVAL, "params is NULL");
+    if (p->block_size < 1 || p->block_size > 15 || (p->block_size & 1) == 0)
+        return fail(DSX_EINVAL, "block_size must be odd and in [1, 15]");
+    if (p->num_disp < 1 || p->num_disp > 512) return fail(DSX_EINVAL, "num_disp must be in [1, 512]");
+    if (p->cost != DSX_COST_SAD && p->cost != DSX_COST_SSD) return fail(DSX_EINVAL, "cost must be SAD (0) or SSD (1)");
+    if (p->uniqueness_ratio < 0 || p->uniqueness_ratio >= 100)
+        return fail(DSX_EINVAL, "uniqueness_ratio must be in [0, 100)");
+    if (p->float_mode != DSX_FLOAT_FIXED && p->float_mode != DSX_FLOAT_PARABOLA)
+        return fail(DSX_EINVAL, "float_mode must be 0 or 1");
+    if (p->path != DSX_PATH_FUSED && p->path != DSX_PATH_VOLUME) return fail(DSX_EINVAL, "path must be 0 or 1");
+    if (p->min_disp < -2047 || p->min_disp + p->num_disp > 2047)
+        return fail(DSX_EINVAL, "min_disp/num_disp out of the int16 x16 fixed-point range");
+    dsx::Geometry g;
+    pick_geometry(p->num_disp, g);
+    if (max_cost(*p) >= (1ull << (32 - g.DB)) - 1)
+        return fail(DSX_EINVAL, "block_size/cost/num_disp combination exceeds the 32-bit (cost<<DB|d) key");
+    return DSX_OK;
+}
+
+struct TimedLaunch {
+    int kernel;
+    hipEvent_t a, b;
+};
+
+}  // namespace
+
+struct dsx_handle {
+    int device = 0;
+    dsx_params p{};
+    dsx::Geometry g{};
+    hipStream_t stream = nullptr;  // for dsx_compute_host
+    // buffer cache keyed by (H, W, geometry); single entry like RectificationCache (rectify.py:49-50)
+    int cH = 0, cW = 0, cDp = 0, cCostBytes = 0;
+    uint8_t *dL = nullptr, *dR = nullptr;
+    int16_t *dFixed = nullptr;
+    float *dFloat = nullptr;
+    int16_t *dRmap = nullptr;
+    void *vol = nullptr;
+    size_t vol_bytes = 0;
+    // timing
+    std::vector<std::string> knames;
+    std::vector<double> ktotal;
+    std::vector<int> kcount;
+    std::vector<TimedLaunch> pending;
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> free_events;
+};
+
+namespace {
+
+void free_buffers(dsx_handle *h) {
+    (void)hipFree(h->dL);
+    (void)hipFree(h->dR);
+    (void)hipFree(h->dFixed);
+    (void)hipFree(h->dFloat);
+    (void)hipFree(h->dRmap);
+    (void)hipFree(h->vol);
+    h->dL = h->dR = nullptr;
+    h->dFixed = nullptr;
+    h->dFloat = nullptr;
+    h->dRmap = nullptr;
+    h->vol = nullptr;
+    h->vol_bytes = 0;
+    h->cH = h->cW = h->cDp = h->cCostBytes = 0;
+}
+
+int ensure_buffers(dsx_handle *h, int H, int W, bool host_staging) {
+    const int cbytes = h->p.cost == DSX_COST_SSD ? 4 : 2;
+    if (h->cH != H || h->cW != W || h->cDp != h->g.Dp || h->cCostBytes != cbytes) free_buffers(h);
+    const size_t n = (size_t)H * W;
+    if (host_staging && !h->dL) {
+        DSX_HIP(hipMalloc(&h->dL, n));
+        DSX_HIP(hipMalloc(&h->dR, n));
+        DSX_HIP(hipMalloc(&h->dFixed, n * 2));
+        DSX_HIP(hipMalloc(&h->dFloat, n * 4));
+    }
+    if (h->p.disp12_max_diff >= 0 && h->p.path == DSX_PATH_FUSED && !h->dRmap) DSX_HIP(hipMalloc(&h->dRmap, n * 2));
+    if (h->p.path == DSX_PATH_VOLUME && !h->vol) {
+        h->vol_bytes = n * h->g.Dp * cbytes;
+        DSX_HIP(hipMalloc(&h->vol, h->vol_bytes));
+    }
+    h->cH = H;
+    h->cW = W;
+    h->cDp = h->g.Dp;
+    h->cCostBytes = cbytes;
+    return DSX_OK;
+}
+
+int kernel_id(dsx_handle *h, const char *name) {
+    for (size_t i = 0; i < h->knames.size(); ++i)
+        if (h->knames[i] == name) return (int)i;
+    h->knames.emplace_back(name);
+    h->ktotal.push_back(0.0);
+    h->kcount.push_back(0);
+    return (int)h->knames.size() - 1;
+}
+
+int begin_timed(dsx_handle *h, const char *name, hipStream_t st, TimedLaunch &t) {
+    t.kernel = kernel_id(h, name);
+    if (!h->free_events.empty()) {
+        t.a = h->free_events.back().first;
+        t.b = h->free_events.back().second;
+        h->free_events.pop_back();
+    } else {
+        DSX_HIP(hipEventCreate(&t.a));
+        DSX_HIP(hipEventCreate(&t.b));
+    }
+    DSX_HIP(hipEventRecord(t.a, st));
+    return DSX_OK;
+}
+
+int end_timed(dsx_handle *h, hipStream_t st, TimedLaunch &t) {
+    DSX_HIP(hipEventRecord(t.b, st));
+    h->pending.push_back(t);
+    return DSX_OK;
+}
+
+int collect_times(dsx_handle *h) {
+    for (auto &t : h->pending) {
+        DSX_HIP(hipEventSynchronize(t.b));
+        float ms = 0.f;
+        DSX_HIP(hipEventElapsedTime(&ms, t.a, t.b));
+        h->ktotal[t.kernel] += ms;
+        h->kcount[t.kernel] += 1;
+        h->free_events.emplace_back(t.a, t.b);
+    }
+    h->pending.clear();
+    return DSX_OK;
+}
+
+dsx::PassArgs base_args(dsx_handle *h, int H, int W, int64_t stride) {
+    dsx::PassArgs a{};
+    a.stride = stride;
+    a.H = H;
+    a.W = W;
+    a.m = h->p.min_disp;
+    a.D = h->p.num_disp;
+    a.Dp = h->g.Dp;
+    a.DB = h->g.DB;
+    a.TPP = h->g.TPP;
+    a.TY = dsx::kRowsPerBlock;
+    a.uniq = h->p.uniqueness_ratio;
+    a.lr = h->p.disp12_max_diff;
+    a.subpix = h->p.subpixel;
+    a.float_mode = h->p.float_mode;
+    const uint32_t keymax = (uint32_t)((1ull << (32 - h->g.DB)) - 1ull);
+    a.padv = h->p.cost == DSX_COST_SSD ? keymax : (keymax < 0xFFFFu ? keymax : 0xFFFFu);
+    return a;
+}
+
+#define DSX_LAUNCH(h, name, st, call)                                    \
+    do {                                                                 \
+        TimedLaunch t_;                                                  \
+        if ((h)->p.timing) {                                             \
+            int rc_ = begin_timed((h), (name), (st), t_);                \
+            if (rc_) return rc_;                                         \
+        }                                                                \
+        hipError_t e_ = (call);                                          \
+        if (e_ != hipSuccess) return fail(DSX_EHIP, std::string(name) + " launch: " + hipGetErrorString(e_)); \
+        if ((h)->p.timing) {                                             \
+            int rc_ = end_timed((h), (st), t_);                          \
+            if (rc_) return rc_;                                         \
+        }                                                                \
+    } while (0)
+
+int run_right_pass(dsx_handle *h, const void *dL, const void *dR, int H, int W, int64_t stride, int16_t *out,
+                   hipStream_t st) {
+    dsx::PassArgs a = base_args(h, H, W, stride);
+    a.ref = static_cast<const uint8_t *>(dR);
+    a.src = static_cast<const uint8_t *>(dL);
+    a.out_dR = out;
+    const int radius = h->p.block_size / 2;
+    DSX_LAUNCH(h, "bm_pass_right", st, dsx::launch_pass(dsx::SIDE_RIGHT, radius, h->g.TX, h->p.cost == DSX_COST_SSD, a, st));
+    return DSX_OK;
+}
+
+int run(dsx_handle *h, const void *dL, const void *dR, int H, int W, int64_t stride, void *outFixed, void *outFloat,
+        hipStream_t st) {
+    const int radius = h->p.block_size / 2;
+    const bool ssd = h->p.cost == DSX_COST_SSD;
+    if (h->p.path == DSX_PATH_FUSED) {
+        if (h->p.disp12_max_diff >= 0) {
+            int rc = run_right_pass(h, dL, dR, H, W, stride, h->dRmap, st);
+            if (rc) return rc;
+        }
+        dsx::PassArgs a = base_args(h, H, W, stride);
+        a.ref = static_cast<const uint8_t *>(dL);
+        a.src = static_cast<const uint8_t *>(dR);
+        a.dRmap = h->dRmap;
+        a.out_fixed = static_cast<int16_t *>(outFixed);
+        a.out_float = static_cast<float *>(outFloat);
+        DSX_LAUNCH(h, "bm_pass_left", st, dsx::launch_pass(dsx::SIDE_LEFT, radius, h->g.TX, ssd, a, st));
+    } else {
+        dsx::PassArgs a = base_args(h, H, W, stride);
+        a.ref = static_cast<const uint8_t *>(dL);
+        a.src = static_cast<const uint8_t *>(dR);
+        a.vol = h->vol;
+        DSX_LAUNCH(h, "cost_volume", st, dsx::launch_pass(dsx::SIDE_VOLUME, radius, h->g.TX, ssd, a, st));
+        dsx::VolArgs v{};
+        v.vol = h->vol;
+        v.H = H;
+        v.W = W;
+        v.m = h->p.min_disp;
+        v.D = h->p.num_disp;
+        v.Dp = h->g.Dp;
+        v.DB = h->g.DB;
+        v.TPP = h->g.TPP;
+        v.uniq = h->p.uniqueness_ratio;
+        v.lr = h->p.disp12_max_diff;
+        v.subpix = h->p.subpixel;
+        v.float_mode = h->p.float_mode;
+        v.out_fixed = static_cast<int16_t *>(outFixed);
+        v.out_float = static_cast<float *>(outFloat);
+        if (dsx::volume_smem_bytes(h->g.TX, ssd, h->g.Dp, h->g.TPP, W) > 160 * 1024)
+            return fail(DSX_EINVAL, "image too wide for the volume path's row kernel");
+        DSX_LAUNCH(h, "volume_wta", st, dsx::launch_volume_wta(h->g.TX, ssd, v, st));
+    }
+    return DSX_OK;
+}
+
+int check_shape(int H, int W, int64_t stride) {
+    if (H <= 0 || W <= 0) return fail(DSX_EINVAL, "image must be non-empty");
+    if (stride < W) return fail(DSX_EINVAL, "stride_bytes must be >= W");
+    if ((int64_t)H * W > (int64_t)1 << 31) return fail(DSX_EINVAL, "image too large");
+    return DSX_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int dsx_version(void) { return DSX_VERSION; }
+
+int dsx_device_count(int *n) {
+    if (!n) return fail(DSX_EINVAL, "n is NULL");
+    int c = 0;
+    hipError_t e = hipGetDeviceCount(&c);
+    if (e != hipSuccess) {
+        *n = 0;
+        if (e == hipErrorNoDevice) return DSX_OK;
+        return fail(DSX_EHIP, std::string("hipGetDeviceCount: ") + hipGetErrorString(e));
+    }
+    *n = c;
+    return DSX_OK;
+}
+
+void dsx_default_params(dsx_params *p) {
+    if (!p) return;
+    std::memset(p, 0, sizeof(*p));
+    p->min_disp = 0;
+    p->num_disp = 128;
+    p->block_size = 5;
+    p->cost = DSX_COST_SAD;
+    p->uniqueness_ratio = 10;
+    p->disp12_max_diff = 1;
+    p->subpixel = 1;
+    p->float_mode = DSX_FLOAT_FIXED;
+    p->path = DSX_PATH_FUSED;
+    p->timing = 0;
+}
+
+int dsx_check_params(const dsx_params *p) {
+    g_err.clear();
+    return check(p);
+}
+
+int dsx_create(int device, const dsx_params *p, dsx_handle **out) {
+    g_err.clear();
+    if (!out) return fail(DSX_EINVAL, "out is NULL");
+    *out = nullptr;
+    int rc = check(p);
+    if (rc) return rc;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n == 0) return fail(DSX_EHIP, "no HIP device available");
+    if (device < 0 || device >= n) return fail(DSX_EINVAL, "device index out of range");
+    DSX_HIP(hipSetDevice(device));
+    dsx_handle *h = new dsx_handle();
+    h->device = device;
+    h->p = *p;
+    pick_geometry(p->num_disp, h->g);
+    hipError_t e = hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking);
+    if (e != hipSuccess) {
+        delete h;
+        return fail(DSX_EHIP, std::string("hipStreamCreate: ") + hipGetErrorString(e));
+    }
+    *out = h;
+    return DSX_OK;
+}
+
+int dsx_set_params(dsx_handle *h, const dsx_params *p) {
+    g_err.clear();
+    if (!h) return fail(DSX_EINVAL, "handle is NULL");
+    int rc = check(p);
+    if (rc) return rc;
+    DSX_HIP(hipSetDevice(h->device));
+    DSX_HIP(hipStreamSynchronize(h->stream));
+    h->p = *p;
+    pick_geometry(p->num_disp, h->g);
+    return DSX_OK;
+}
+
+int dsx_compute_device(dsx_handle *h, const void *dL, const void *dR, int32_t H, int32_t W, int64_t stride_bytes,
+                       void *d_out_fixed, void *d_out_float, void *hip_stream) {
+    g_err.clear();
+    if (!h) return fail(DSX_EINVAL, "handle is NULL");
+    if (!dL || !dR) return fail(DSX_EINVAL, "input pointers are NULL");
+    if (!d_out_fixed && !d_out_float) return fail(DSX_EINVAL, "at least one output is required");
+    int rc = check_shape(H, W, stride_bytes);
+    if (rc) return rc;
+    DSX_HIP(hipSetDevice(h->device));
+    rc = ensure_buffers(h, H, W, false);
+    if (rc) return rc;
+    return run(h, dL, dR, H, W, stride_bytes, d_out_fixed, d_out_float, static_cast<hipStream_t>(hip_stream));
+}
+
+int dsx_right_map_device(dsx_handle *h, const void *dL, const void *dR, int32_t H, int32_t W, int64_t stride_bytes,
+                         void *d_out_dR, void *hip_stream) {
+    g_err.clear();
+    if (!h || !dL || !dR || !d_out_dR) return fail(DSX_EINVAL, "NULL argument");
+    int rc = check_shape(H, W, stride_bytes);
+    if (rc) return rc;
+    DSX_HIP(hipSetDevice(h->device));
+    return run_right_pass(h, dL, dR, H, W, stride_bytes, static_cast<int16_t *>(d_out_dR),
+                          static_cast<hipStream_t>(hip_stream));
+}
+
+int dsx_compute_host(dsx_handle *h, const uint8_t *L, const uint8_t *R, int32_t H, int32_t W, int64_t stride_bytes,
+                     int16_t *out_fixed, float *out_float) {
+    g_err.clear();
+    if (!h) return fail(DSX_EINVAL, "handle is NULL");
+    if (!L || !R || !out_fixed) return fail(DSX_EINVAL, "NULL argument (out_fixed is required)");
+    int rc = check_shape(H, W, stride_bytes);
+    if (rc) return rc;
+    DSX_HIP(hipSetDevice(h->device));
+    rc = ensure_buffers(h, H, W, true);
+    if (rc) return rc;
+    hipStream_t st = h->stream;
+    DSX_HIP(hipMemcpy2DAsync(h->dL, W, L, stride_bytes, W, H, hipMemcpyHostToDevice, st));
+    DSX_HIP(hipMemcpy2DAsync(h->dR, W, R, stride_bytes, W, H, hipMemcpyHostToDevice, st));
+    rc = run(h, h->dL, h->dR, H, W, W, h->dFixed, out_float ? h->dFloat : nullptr, st);
+    if (rc) return rc;
+    DSX_HIP(hipMemcpyAsync(out_fixed, h->dFixed, (size_t)H * W * 2, hipMemcpyDeviceToHost, st));
+    if (out_float) DSX_HIP(hipMemcpyAsync(out_float, h->dFloat, (size_t)H * W * 4, hipMemcpyDeviceToHost, st));
+    DSX_HIP(hipStreamSynchronize(st));
+    return DSX_OK;
+}
+
+int dsx_kernel_times(dsx_handle *h, char *names, int names_cap, float *ms, int *counts, int cap, int *n) {
+    g_err.clear();
+    if (!h || !n) return fail(DSX_EINVAL, "NULL argument");
+    DSX_HIP(hipSetDevice(h->device));
+    int rc = collect_times(h);
+    if (rc) return rc;
+    std::string all;
+    const int k = (int)h->knames.size();
+    for (int i = 0; i < k; ++i) {
+        if (i) all += ";";
+        all += h->knames[i];
+        if (i < cap) {
+            if (ms) ms[i] = h->kcount[i] ? (float)(h->ktotal[i] / h->kcount[i]) : 0.f;
+            if (counts) counts[i] = h->kcount[i];
+        }
+    }
+    if (names && names_cap > 0) {
+        std::strncpy(names, all.c_str(), (size_t)names_cap - 1);
+        names[names_cap - 1] = '\0';
+    }
+    *n = k;
+    return DSX_OK;
+}
+
+int dsx_reset_times(dsx_handle *h) {
+    g_err.clear();
+    if (!h) return fail(DSX_EINVAL, "handle is NULL");
+    int rc = collect_times(h);
+    if (rc) return rc;
+    for (size_t i = 0; i < h->ktotal.size(); ++i) {
+        h->ktotal[i] = 0.0;
+        h->kcount[i] = 0;
+    }
+    return DSX_OK;
+}
+
+int dsx_workspace_bytes(dsx_handle *h, int64_t *bytes) {
+    if (!h || !bytes) return fail(DSX_EINVAL, "NULL argument");
+    const int64_t n = (int64_t)h->cH * h->cW;
+    int64_t b = 0;
+    if (h->dL) b += n * (1 + 1 + 2 + 4);
+    if (h->dRmap) b += n * 2;
+    b += (int64_t)h->vol_bytes;
+    *bytes = b;
+    return DSX_OK;
+}
+
+int dsx_destroy(dsx_handle *h) {
+    g_err.clear();
+    if (!h) return DSX_OK;
+    (void)hipSetDevice(h->device);
+    (void)hipStreamSynchronize(h->stream);
+    collect_times(h);
+    for (auto &e : h->free_events) {
+        (void)hipEventDestroy(e.first);
+        (void)hipEventDestroy(e.second);
+    }
+    free_buffers(h);
+    (void)hipStreamDestroy(h->stream);
+    delete h;
+    return DSX_OK;
+}
+
+const char *dsx_last_error(void) { return g_err.c_str(); }
+
+}  // extern "C"

@@ -1,0 +1,172 @@
+"""HipBlockMatcher: the MI355X replacement for the matcher object the reference builds with
+``cv2.StereoSGBM_create`` (depthlib/stereo_core.py:63-75) and calls as
+``self.sgbm.compute(rectified_L, rectified_R)`` (stereo_core.py:231).
+
+``compute`` keeps cv2's ``StereoMatcher.compute`` contract: two uint8 H x W arrays of the same
+size -> int16 H x W disparity x16 (4 fractional bits), invalid = (min_disp - 1) * 16, so
+``StereoCore.compute_disparity``'s ``/ 16.0`` and ``_process_pair``'s crop apply unchanged.
+Mismatched inputs raise ValueError (cv2 raises cv2.error there).
+
+Device-resident callers use ``compute_device`` with torch tensors (or raw device pointers) on a
+HIP stream; nothing is copied through the host.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+
+from . import _dsx
+
+
+def _ptr(t):
+    """Device pointer of a torch tensor (or an int already)."""
+    if t is None:
+        return None
+    if isinstance(t, int):
+        return t
+    return t.data_ptr()
+
+
+class HipBlockMatcher:
+    """SAD/SSD block matcher running on one HIP device (one handle per thread / GPU)."""
+
+    def __init__(self, min_disp=0, num_disp=128, block_size=5, cost="sad", uniqueness_ratio=10,
+                 disp12_max_diff=1, subpixel=True, float_mode="fixed", path="fused", device=0,
+                 timing=False):
+        self.device = int(device)
+        self._params = _dsx.make_params(min_disp, num_disp, block_size, cost, uniqueness_ratio,
+                                        disp12_max_diff, subpixel, float_mode, path, timing)
+        _dsx.check_params(self._params)  # validates on the host, no device needed
+        self._h = None
+        self._cfg = dict(min_disp=min_disp, num_disp=num_disp, block_size=block_size, cost=cost,
+                         uniqueness_ratio=uniqueness_ratio, disp12_max_diff=disp12_max_diff,
+                         subpixel=subpixel, float_mode=float_mode, path=path, timing=timing)
+
+    # -- lifetime ---------------------------------------------------------------------------
+    def _handle(self):
+        if self._h is None:
+            L = _dsx.lib()
+            n = _dsx.device_count()
+            if n == 0:
+                raise RuntimeError("HipBlockMatcher: no HIP device visible (the engine has no CPU fallback)")
+            h = ctypes.c_void_p()
+            _dsx.check(L.dsx_create(self.device, ctypes.byref(self._params), ctypes.byref(h)), "dsx_create")
+            self._h = h
+        return self._h
+
+    def close(self):
+        if self._h is not None:
+            _dsx.lib().dsx_destroy(self._h)
+            self._h = None
+
+    def __del__(self):  # pragma: no cover - GC timing
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @property
+    def params(self) -> dict:
+        return dict(self._cfg)
+
+    # -- cv2.StereoMatcher-style getters (cv2 names used by depthlib docs) --------------------
+    def getMinDisparity(self):
+        return self._cfg["min_disp"]
+
+    def getNumDisparities(self):
+        return self._cfg["num_disp"]
+
+    def getBlockSize(self):
+        return self._cfg["block_size"]
+
+    def getUniquenessRatio(self):
+        return self._cfg["uniqueness_ratio"]
+
+    def getDisp12MaxDiff(self):
+        return self._cfg["disp12_max_diff"]
+
+    # -- compute ----------------------------------------------------------------------------
+    @staticmethod
+    def _as_gray(a, name):
+        a = np.asarray(a)
+        if a.dtype != np.uint8 or a.ndim != 2:
+            raise ValueError(f"{name} must be a uint8 H x W (grayscale, rectified) array")
+        if a.strides[1] != 1:
+            a = np.ascontiguousarray(a)
+        return a
+
+    def compute(self, left, right, out_float=None):
+        """cv2 StereoMatcher.compute contract (stereo_core.py:231): int16 H x W, x16."""
+        L = self._as_gray(left, "left")
+        R = self._as_gray(right, "right")
+        if L.shape != R.shape:
+            raise ValueError("left and right images must have the same size")
+        if L.strides[0] != R.strides[0]:
+            L = np.ascontiguousarray(L)
+            R = np.ascontiguousarray(R)
+        H, W = L.shape
+        out = np.empty((H, W), np.int16)
+        fptr = None
+        if out_float is not None:
+            if out_float.shape != (H, W) or out_float.dtype != np.float32 or not out_float.flags.c_contiguous:
+                raise ValueError("out_float must be a contiguous float32 H x W array")
+            fptr = out_float.ctypes.data
+        rc = _dsx.lib().dsx_compute_host(self._handle(), L.ctypes.data, R.ctypes.data, H, W, L.strides[0],
+                                         out.ctypes.data, fptr)
+        _dsx.check(rc, "dsx_compute_host")
+        return out
+
+    def compute_device(self, left, right, out_fixed=None, out_float=None, stream=None, stride=None):
+        """Async device compute. ``left``/``right``: uint8 CUDA/HIP tensors (H x W, unit column
+        stride) or (ptr, H, W) tuples.  Outputs are caller-owned contiguous device buffers."""
+        if isinstance(left, tuple):
+            lp, H, W = left
+            rp = right[0] if isinstance(right, tuple) else _ptr(right)
+            st = W if stride is None else stride
+        else:
+            if left.dtype != right.dtype or left.shape != right.shape or left.dim() != 2:
+                raise ValueError("left and right must be uint8 H x W tensors of the same shape")
+            if str(left.dtype) != "torch.uint8" or left.stride(1) != 1 or right.stride(1) != 1 or \
+                    left.stride(0) != right.stride(0):
+                raise ValueError("inputs must be uint8 with unit column stride and equal row strides")
+            if not left.is_cuda or not right.is_cuda:
+                raise ValueError("compute_device needs device tensors (use compute() for host arrays)")
+            H, W = left.shape
+            lp, rp, st = left.data_ptr(), right.data_ptr(), left.stride(0)
+        if stream is None:
+            sptr = None
+        elif isinstance(stream, int):
+            sptr = stream
+        else:
+            sptr = stream.cuda_stream
+        rc = _dsx.lib().dsx_compute_device(self._handle(), lp, rp, H, W, st, _ptr(out_fixed), _ptr(out_float), sptr)
+        _dsx.check(rc, "dsx_compute_device")
+
+    def right_map_device(self, left, right, out_dR, stream=None):
+        H, W = left.shape
+        sptr = None if stream is None else (stream if isinstance(stream, int) else stream.cuda_stream)
+        rc = _dsx.lib().dsx_right_map_device(self._handle(), left.data_ptr(), right.data_ptr(), H, W,
+                                             left.stride(0), out_dR.data_ptr(), sptr)
+        _dsx.check(rc, "dsx_right_map_device")
+
+    # -- timing -----------------------------------------------------------------------------
+    def kernel_times(self) -> dict:
+        """{kernel name: (avg ms per launch, launches)} recorded with HIP events (timing=True)."""
+        cap = 16
+        names = ctypes.create_string_buffer(1024)
+        ms = (ctypes.c_float * cap)()
+        cnt = (ctypes.c_int * cap)()
+        n = ctypes.c_int(0)
+        rc = _dsx.lib().dsx_kernel_times(self._handle(), names, 1024, ms, cnt, cap, ctypes.byref(n))
+        _dsx.check(rc, "dsx_kernel_times")
+        keys = names.value.decode().split(";") if n.value else []
+        return {k: (float(ms[i]), int(cnt[i])) for i, k in enumerate(keys[:cap])}
+
+    def reset_times(self):
+        _dsx.check(_dsx.lib().dsx_reset_times(self._handle()), "dsx_reset_times")
+
+    def workspace_bytes(self) -> int:
+        b = ctypes.c_int64(0)
+        _dsx.check(_dsx.lib().dsx_workspace_bytes(self._handle(), ctypes.byref(b)), "dsx_workspace_bytes")
+        return b.value

@@ -1,0 +1,129 @@
+/*
+ * dsx.h - C-ABI of the MI355X stereo block-matching engine (libdsx.so).
+ *
+ * This is the drop-in boundary for the reference's hot path. In the reference
+ * (mspaintenjoyer/DepthEstimation, Python) the path is a third-party matcher object:
+ *
+ *   depthlib/stereo_core.py:63-75   self.sgbm = cv2.StereoSGBM_create(minDisparity=..., ...)
+ *   depthlib/stereo_core.py:231     disp_fixed = self.sgbm.compute(rectified_L, rectified_R)
+ *   depthlib/stereo_core.py:232     return disp_fixed.astype(np.float32) / 16.0
+ *
+ * A reference-side binding (ctypes) maps
+ *   cv2.StereoSGBM_create(...)  -> dsx_create()          (matcher construction)
+ *   matcher.compute(L, R)       -> dsx_compute_host()     (int16 x16 fixed-point result)
+ *   (device-resident callers)   -> dsx_compute_device()   (async, HIP stream)
+ *   matcher lifetime (GC)       -> dsx_destroy()
+ *
+ * Plain C types only: pointers, sizes, int32/int64. No torch / HIP types in signatures
+ * (streams are passed as void*). All functions return 0 on success or a negative
+ * DSX_E* code; they never abort or throw across the ABI. dsx_last_error() returns a
+ * thread-local message for the last failure on the calling thread.
+ *
+ * Threading: a handle is not thread-safe; use one handle per thread / GPU. Different
+ * handles are independent. Every call does hipSetDevice(handle device) first.
+ */
+#ifndef DSX_H
+#define DSX_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define DSX_VERSION 100 /* 1.0.0 */
+
+#define DSX_OK 0
+#define DSX_EINVAL (-1) /* bad argument (mirrors ValueError / cv2.error on bad input) */
+#define DSX_EHIP (-2)   /* HIP runtime error */
+#define DSX_ECOMM (-3)  /* reserved: collective error */
+#define DSX_ENOMEM (-4) /* device allocation failed */
+
+#define DSX_COST_SAD 0
+#define DSX_COST_SSD 1
+
+#define DSX_FLOAT_FIXED 0    /* out_float = out_fixed / 16 (stereo_core.py:232 contract) */
+#define DSX_FLOAT_PARABOLA 1 /* out_float = continuous parabola vertex (north-star 1e-3 path) */
+
+#define DSX_PATH_FUSED 0  /* cost computed in LDS, never written to HBM (default) */
+#define DSX_PATH_VOLUME 1 /* K1 writes the [H][W][D] cost volume to HBM, K2 reduces it */
+
+/* Matcher parameters. Field meaning follows StereoCore.sgbm_params
+ * (depthlib/stereo_core.py:16-39) for the keys that exist there. */
+typedef struct dsx_params {
+    int32_t min_disp;         /* 'min_disp'          (stereo_core.py:17, cv2 minDisparity)    */
+    int32_t num_disp;         /* 'num_disp'          (stereo_core.py:18, cv2 numDisparities)  */
+    int32_t block_size;       /* 'block_size'        (stereo_core.py:19), odd, 1..15          */
+    int32_t cost;             /* DSX_COST_SAD | DSX_COST_SSD (build key 'cost')               */
+    int32_t uniqueness_ratio; /* 'uniqueness_ratio'  (stereo_core.py:22), 0 disables, <100    */
+    int32_t disp12_max_diff;  /* 'disp12_max_diff'   (stereo_core.py:20), <0 disables LR      */
+    int32_t subpixel;         /* build key 'subpixel': 1 = 1/16-px parabola, 0 = integer      */
+    int32_t float_mode;       /* DSX_FLOAT_FIXED | DSX_FLOAT_PARABOLA                          */
+    int32_t path;             /* DSX_PATH_FUSED | DSX_PATH_VOLUME                              */
+    int32_t timing;           /* 1 = record per-kernel HIP-event timings (dsx_kernel_times)   */
+    int32_t reserved[6];
+} dsx_params;
+
+typedef struct dsx_handle dsx_handle;
+
+/* Library version (DSX_VERSION). */
+int dsx_version(void);
+
+/* Number of visible HIP devices. */
+int dsx_device_count(int *n);
+
+/* Fill *p with the defaults of StereoCore.sgbm_params (stereo_core.py:16-39) plus the build
+ * keys: min 0, num 128, block 5, SAD, uniqueness 10, disp12 1, subpixel 1, fixed floats,
+ * fused path. */
+void dsx_default_params(dsx_params *p);
+
+/* Validate parameters without creating a handle (DSX_EINVAL + message if unsupported). */
+int dsx_check_params(const dsx_params *p);
+
+/* Create a matcher on `device` (replaces cv2.StereoSGBM_create, stereo_core.py:63-75). */
+int dsx_create(int device, const dsx_params *p, dsx_handle **out);
+
+/* Replace the parameters of an existing matcher (configure_sgbm -> _build_sgbm,
+ * stereo_core.py:77-123). Cached device buffers are invalidated when sizes change. */
+int dsx_set_params(dsx_handle *h, const dsx_params *p);
+
+/* Synchronous host-buffer compute (replaces matcher.compute, stereo_core.py:231).
+ * L, R: uint8 H x W with row stride `stride_bytes` (>= W).  out_fixed: int16 H x W
+ * (required, contiguous).  out_float: float32 H x W or NULL. */
+int dsx_compute_host(dsx_handle *h, const uint8_t *L, const uint8_t *R, int32_t H, int32_t W,
+                     int64_t stride_bytes, int16_t *out_fixed, float *out_float);
+
+/* Asynchronous device-pointer compute on `hip_stream` (hipStream_t, NULL = default stream).
+ * dL, dR: device uint8 H x W, row stride `stride_bytes`.  d_out_fixed (int16) and
+ * d_out_float (float32) are contiguous H x W device buffers; either may be NULL but not
+ * both.  No host synchronisation, no allocation when the size matches the cached one. */
+int dsx_compute_device(dsx_handle *h, const void *dL, const void *dR, int32_t H, int32_t W,
+                       int64_t stride_bytes, void *d_out_fixed, void *d_out_float,
+                       void *hip_stream);
+
+/* Right-view winner map only (the LR check's dR, int16 H x W, -1 where the search range is
+ * empty). Exposed for parity tests of the right pass. Async on hip_stream. */
+int dsx_right_map_device(dsx_handle *h, const void *dL, const void *dR, int32_t H, int32_t W,
+                         int64_t stride_bytes, void *d_out_dR, void *hip_stream);
+
+/* Per-kernel timings accumulated since the last reset (params.timing = 1): names are
+ * written as a ';'-separated list into `names` (capacity `names_cap`), average ms per
+ * launch into ms[i], launch counts into counts[i]; *n = number of kernels. */
+int dsx_kernel_times(dsx_handle *h, char *names, int names_cap, float *ms, int *counts, int cap,
+                     int *n);
+int dsx_reset_times(dsx_handle *h);
+
+/* Device bytes currently held by the handle's buffer cache. */
+int dsx_workspace_bytes(dsx_handle *h, int64_t *bytes);
+
+/* Destroy the matcher and free its device buffers. */
+int dsx_destroy(dsx_handle *h);
+
+/* Thread-local message of the last error on this thread ("" if none). */
+const char *dsx_last_error(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* DSX_H */

@@ -1,0 +1,137 @@
+"""GPU parity: the HIP path (through the C-ABI) against the CPU oracle on identical seeded
+inputs. Integer disparities (int16 x16) are bit-exact; the float parabola output is checked
+against the oracle within 1e-3 (north_star tolerance) and is in fact bit-exact."""
+from __future__ import annotations
+
+import zlib
+
+import numpy as np
+import pytest
+
+from depthestimation_amd.synthetic import stereo_pair
+from oracle.stereo_bm import stereo_bm, right_argmin, cost_volume
+from oracle.cref import CRef
+
+pytestmark = pytest.mark.gpu
+
+FLOAT_TOL = 1e-3
+
+
+@pytest.fixture(scope="module")
+def torch_dev():
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    return torch
+
+
+def _run(L, R, path="fused", float_mode="fixed", **kw):
+    from depthestimation_amd.matcher import HipBlockMatcher
+    m = HipBlockMatcher(path=path, float_mode=float_mode, **kw)
+    out_f = np.empty(L.shape, np.float32)
+    fixed = m.compute(L, R, out_float=out_f)
+    m.close()
+    return fixed, out_f
+
+
+CASES = [
+    # (H, W, min_disp, num_disp, block, cost, uniq, lr)
+    (48, 96, 0, 16, 5, "sad", 0, -1),
+    (40, 130, 0, 64, 5, "sad", 10, 1),
+    (37, 200, 3, 64, 9, "sad", 10, 0),
+    (33, 160, 0, 128, 9, "sad", 0, -1),
+    (45, 300, 0, 128, 9, "sad", 15, 1),
+    (30, 170, -4, 40, 3, "sad", 10, 2),
+    (36, 300, 0, 192, 15, "sad", 10, 1),
+    (35, 320, 0, 256, 11, "ssd", 10, 1),
+    (34, 140, 2, 60, 7, "ssd", 0, -1),
+    (20, 90, 0, 20, 1, "sad", 5, 1),
+    (25, 600, 0, 500, 5, "sad", 10, 1),
+    (9, 70, 0, 64, 13, "ssd", 0, 1),
+]
+
+
+@pytest.mark.parametrize("path", ["fused", "volume"])
+@pytest.mark.parametrize("case", CASES, ids=lambda c: "x".join(map(str, c)))
+def test_parity_vs_oracle(torch_dev, case, path):
+    H, W, m, D, bs, cost, u, lr = case
+    L, R, _ = stereo_pair(H, W, m, D, seed=zlib.crc32(repr(case).encode()) & 0xFFFF)
+    ref = stereo_bm(L, R, m, D, bs, cost, u, lr, True)
+    fixed, fl = _run(L, R, path=path, min_disp=m, num_disp=D, block_size=bs, cost=cost,
+                     uniqueness_ratio=u, disp12_max_diff=lr, subpixel=True)
+    mism = np.argwhere(fixed != ref["fixed"])
+    assert mism.size == 0, f"{len(mism)} mismatches, first {mism[:5].tolist()}: got {fixed[tuple(mism[0])]} want {ref['fixed'][tuple(mism[0])]}"
+    np.testing.assert_array_equal(fl, ref["disp"])
+
+
+@pytest.mark.parametrize("case", CASES[:8], ids=lambda c: "x".join(map(str, c)))
+def test_parabola_float(torch_dev, case):
+    H, W, m, D, bs, cost, u, lr = case
+    L, R, _ = stereo_pair(H, W, m, D, seed=7)
+    ref = stereo_bm(L, R, m, D, bs, cost, u, lr, True)
+    _, fl = _run(L, R, float_mode="parabola", min_disp=m, num_disp=D, block_size=bs, cost=cost,
+                 uniqueness_ratio=u, disp12_max_diff=lr)
+    assert np.max(np.abs(fl - ref["parabola"])) <= FLOAT_TOL
+    assert (fl.view(np.int32) == ref["parabola"].view(np.int32)).mean() > 0.999
+
+
+def test_right_map(torch_dev):
+    torch = torch_dev
+    from depthestimation_amd.matcher import HipBlockMatcher
+    for (H, W, m, D, bs, cost) in [(30, 150, 0, 64, 5, "sad"), (24, 200, 3, 128, 9, "ssd"), (20, 100, -2, 40, 3, "sad")]:
+        L, R, _ = stereo_pair(H, W, m, D, seed=3)
+        C = cost_volume(L, R, m, D, bs, cost)
+        want = right_argmin(C, m)
+        mt = HipBlockMatcher(min_disp=m, num_disp=D, block_size=bs, cost=cost)
+        tL = torch.from_numpy(L).cuda()
+        tR = torch.from_numpy(R).cuda()
+        out = torch.empty((H, W), dtype=torch.int16, device="cuda")
+        mt.right_map_device(tL, tR, out)
+        torch.cuda.synchronize()
+        np.testing.assert_array_equal(out.cpu().numpy().astype(np.int32), want)
+        mt.close()
+
+
+def test_subpixel_off_and_edge_cases(torch_dev):
+    # tiny images (smaller than the window), num_disp > width, all-equal images
+    for (H, W, D, bs) in [(1, 1, 1, 1), (2, 3, 5, 3), (4, 5, 64, 15), (7, 33, 16, 5)]:
+        L, R, _ = stereo_pair(H, W, 0, D, seed=11)
+        for sub in (False, True):
+            ref = stereo_bm(L, R, 0, D, bs, "sad", 10, 1, sub)
+            fixed, _ = _run(L, R, min_disp=0, num_disp=D, block_size=bs, uniqueness_ratio=10,
+                            disp12_max_diff=1, subpixel=sub)
+            np.testing.assert_array_equal(fixed, ref["fixed"])
+    z = np.zeros((16, 80), np.uint8)
+    ref = stereo_bm(z, z, 0, 16, 3, "sad", 10, 1, True)
+    fixed, _ = _run(z, z, min_disp=0, num_disp=16, block_size=3)
+    np.testing.assert_array_equal(fixed, ref["fixed"])
+
+
+def test_strided_device_inputs(torch_dev):
+    torch = torch_dev
+    from depthestimation_amd.matcher import HipBlockMatcher
+    H, W, D = 40, 150, 64
+    L, R, _ = stereo_pair(H, W, 0, D, seed=5)
+    ref = stereo_bm(L, R, 0, D, 5, "sad", 10, 1, True)
+    bigL = torch.zeros((H, W + 37), dtype=torch.uint8, device="cuda")
+    bigR = torch.zeros((H, W + 37), dtype=torch.uint8, device="cuda")
+    bigL[:, :W] = torch.from_numpy(L).cuda()
+    bigR[:, :W] = torch.from_numpy(R).cuda()
+    out = torch.empty((H, W), dtype=torch.int16, device="cuda")
+    mt = HipBlockMatcher(num_disp=D, block_size=5)
+    mt.compute_device(bigL[:, :W], bigR[:, :W], out_fixed=out)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(out.cpu().numpy(), ref["fixed"])
+    mt.close()
+
+
+def test_large_vs_c_oracle(torch_dev):
+    """1080p-class sizes against the C restatement (bit-exact)."""
+    c = CRef()
+    for (H, W, D, bs, cost, u, lr) in [(270, 480, 128, 9, "sad", 0, -1), (200, 640, 256, 11, "ssd", 10, 1)]:
+        L, R, _ = stereo_pair(H, W, 0, D, seed=21)
+        ref = c(L, R, 0, D, bs, cost, u, lr, True)
+        for path in ("fused", "volume"):
+            fixed, _ = _run(L, R, path=path, num_disp=D, block_size=bs, cost=cost,
+                            uniqueness_ratio=u, disp12_max_diff=lr)
+            np.testing.assert_array_equal(fixed, ref["fixed"])
