@@ -44,7 +44,8 @@ class DsxParams(ctypes.Structure):
         ("float_mode", ctypes.c_int32),
         ("path", ctypes.c_int32),
         ("timing", ctypes.c_int32),
-        ("reserved", ctypes.c_int32 * 6),
+        ("grid_blocks", ctypes.c_int32),
+        ("reserved", ctypes.c_int32 * 5),
     ]
 
 
@@ -122,7 +123,7 @@ def default_params() -> DsxParams:
 
 def make_params(min_disp=0, num_disp=128, block_size=5, cost="sad", uniqueness_ratio=10,
                 disp12_max_diff=1, subpixel=True, float_mode="fixed", path="fused",
-                timing=False) -> DsxParams:
+                timing=False, grid_blocks=0) -> DsxParams:
     p = default_params()
     p.min_disp = int(min_disp)
     p.num_disp = int(num_disp)
@@ -140,6 +141,7 @@ def make_params(min_disp=0, num_disp=128, block_size=5, cost="sad", uniqueness_r
         raise ValueError(f"path must be one of {list(PATH)}")
     p.path = PATH[path]
     p.timing = int(bool(timing))
+    p.grid_blocks = int(grid_blocks)
     return p
 
 

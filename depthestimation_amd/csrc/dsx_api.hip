@@ -3,6 +3,8 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
+#include <cstdlib>
+#include <algorithm>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -33,19 +35,20 @@ int bits_for(int n) {  // smallest b with (1 << b) >= n
     return b < 1 ? 1 : b;
 }
 
-// Dp = TX * TPP, Dp a multiple of 64 (whole waves, one lane per disparity).
-bool pick_geometry(int D, dsx::Geometry &g) {
-    static const int table[][3] = {{64, 32, 2}, {128, 32, 4}, {192, 48, 4}, {256, 32, 8}, {384, 48, 8}, {512, 32, 16}};
-    for (auto &t : table) {
-        if (D <= t[0]) {
-            g.Dp = t[0];
-            g.TX = t[1];
-            g.TPP = t[2];
-            g.DB = bits_for(g.Dp);
-            return true;
-        }
-    }
-    return false;
+// bm2 geometry: SAD lanes own disparity pairs (Dp = 128 * nw, nw in {1,2,4}); SSD lanes own
+// one disparity (Dp = 64 * nw, nw in {1,2,4,8}).  K2 (vol_wta) reuses Dp with 32-d slices.
+bool pick_geometry(int D, int cost, dsx::Geometry &g) {
+    const int unit = cost == DSX_COST_SSD ? 64 : 128;
+    const int maxnw = cost == DSX_COST_SSD ? 8 : 4;
+    int nw = 1;
+    while (nw * unit < D) nw *= 2;
+    if (nw > maxnw) return false;
+    g.NW = nw;
+    g.Dp = nw * unit;
+    g.TX = 32;
+    g.TPP = g.Dp / 32;
+    g.DB = bits_for(g.Dp);
+    return true;
 }
 
 uint64_t max_cost(const dsx_params &p) {
@@ -64,10 +67,11 @@ int check(const dsx_params *p) {
     if (p->float_mode != DSX_FLOAT_FIXED && p->float_mode != DSX_FLOAT_PARABOLA)
         return fail(DSX_EINVAL, "float_mode must be 0 or 1");
     if (p->path != DSX_PATH_FUSED && p->path != DSX_PATH_VOLUME) return fail(DSX_EINVAL, "path must be 0 or 1");
+    if (p->grid_blocks < 0) return fail(DSX_EINVAL, "grid_blocks must be >= 0");
     if (p->min_disp < -2047 || p->min_disp + p->num_disp > 2047)
         return fail(DSX_EINVAL, "min_disp/num_disp out of the int16 x16 fixed-point range");
     dsx::Geometry g;
-    pick_geometry(p->num_disp, g);
+    if (!pick_geometry(p->num_disp, p->cost, g)) return fail(DSX_EINVAL, "num_disp too large");
     if (max_cost(*p) >= (1ull << (32 - g.DB)) - 1)
         return fail(DSX_EINVAL, "block_size/cost/num_disp combination exceeds the 32-bit (cost<<DB|d) key");
     return DSX_OK;
@@ -91,6 +95,8 @@ struct dsx_handle {
     int16_t *dFixed = nullptr;
     float *dFloat = nullptr;
     int16_t *dRmap = nullptr;
+    uint16_t *dL16 = nullptr, *dR16 = nullptr;  // u16-expanded reference rows (bm2 scalar operand)
+    int pitch16 = 0, cRadius = -1;
     void *vol = nullptr;
     size_t vol_bytes = 0;
     // timing
@@ -109,7 +115,12 @@ void free_buffers(dsx_handle *h) {
     (void)hipFree(h->dFixed);
     (void)hipFree(h->dFloat);
     (void)hipFree(h->dRmap);
+    (void)hipFree(h->dL16);
+    (void)hipFree(h->dR16);
     (void)hipFree(h->vol);
+    h->dL16 = h->dR16 = nullptr;
+    h->pitch16 = 0;
+    h->cRadius = -1;
     h->dL = h->dR = nullptr;
     h->dFixed = nullptr;
     h->dFloat = nullptr;
@@ -121,8 +132,12 @@ void free_buffers(dsx_handle *h) {
 
 int ensure_buffers(dsx_handle *h, int H, int W, bool host_staging) {
     const int cbytes = h->p.cost == DSX_COST_SSD ? 4 : 2;
-    if (h->cH != H || h->cW != W || h->cDp != h->g.Dp || h->cCostBytes != cbytes) free_buffers(h);
+    const int radius = h->p.block_size / 2;
+    if (h->cH != H || h->cW != W || h->cDp != h->g.Dp || h->cCostBytes != cbytes || h->cRadius != radius) free_buffers(h);
     const size_t n = (size_t)H * W;
+    h->pitch16 = dsx::expand_pitch16(W, radius);
+    h->cRadius = radius;
+
     if (host_staging && !h->dL) {
         DSX_HIP(hipMalloc(&h->dL, n));
         DSX_HIP(hipMalloc(&h->dR, n));
@@ -139,6 +154,11 @@ int ensure_buffers(dsx_handle *h, int H, int W, bool host_staging) {
     h->cDp = h->g.Dp;
     h->cCostBytes = cbytes;
     return DSX_OK;
+}
+
+uint32_t pad_value(dsx_handle *h) {
+    const uint32_t keymax = (uint32_t)((1ull << (32 - h->g.DB)) - 1ull);
+    return h->p.cost == DSX_COST_SSD ? keymax : (keymax < 0xFFFFu ? keymax : 0xFFFFu);
 }
 
 int kernel_id(dsx_handle *h, const char *name) {
@@ -183,23 +203,21 @@ int collect_times(dsx_handle *h) {
     return DSX_OK;
 }
 
-dsx::PassArgs base_args(dsx_handle *h, int H, int W, int64_t stride) {
-    dsx::PassArgs a{};
+dsx::Bm2Args base_args(dsx_handle *h, int H, int W, int64_t stride) {
+    dsx::Bm2Args a{};
     a.stride = stride;
     a.H = H;
     a.W = W;
     a.m = h->p.min_disp;
     a.D = h->p.num_disp;
-    a.Dp = h->g.Dp;
-    a.DB = h->g.DB;
-    a.TPP = h->g.TPP;
-    a.TY = dsx::kRowsPerBlock;
     a.uniq = h->p.uniqueness_ratio;
     a.lr = h->p.disp12_max_diff;
     a.subpix = h->p.subpixel;
     a.float_mode = h->p.float_mode;
-    const uint32_t keymax = (uint32_t)((1ull << (32 - h->g.DB)) - 1ull);
-    a.padv = h->p.cost == DSX_COST_SSD ? keymax : (keymax < 0xFFFFu ? keymax : 0xFFFFu);
+    a.padv = pad_value(h);
+    a.strip_begin = 0;
+    a.strip_count = (W + dsx::kStripWidth - 1) / dsx::kStripWidth;
+    a.grid_override = h->p.grid_blocks;
     return a;
 }
 
@@ -218,14 +236,23 @@ dsx::PassArgs base_args(dsx_handle *h, int H, int W, int64_t stride) {
         }                                                                \
     } while (0)
 
+int expand(dsx_handle *h, const char *name, const void *img, uint16_t *out, int H, int W, int64_t stride,
+           hipStream_t st) {
+    DSX_LAUNCH(h, name, st,
+               dsx::launch_expand_u16(static_cast<const uint8_t *>(img), stride, H, W, h->p.block_size / 2, out,
+                                      h->pitch16, st));
+    return DSX_OK;
+}
+
 int run_right_pass(dsx_handle *h, const void *dL, const void *dR, int H, int W, int64_t stride, int16_t *out,
                    hipStream_t st) {
-    dsx::PassArgs a = base_args(h, H, W, stride);
+    dsx::Bm2Args a = base_args(h, H, W, stride);
+    a.side = dsx::SIDE_RIGHT;
     a.ref = static_cast<const uint8_t *>(dR);
     a.src = static_cast<const uint8_t *>(dL);
     a.out_dR = out;
     const int radius = h->p.block_size / 2;
-    DSX_LAUNCH(h, "bm_pass_right", st, dsx::launch_pass(dsx::SIDE_RIGHT, radius, h->g.TX, h->p.cost == DSX_COST_SSD, a, st));
+    DSX_LAUNCH(h, "bm_pass_right", st, dsx::launch_bm2(radius, h->p.cost == DSX_COST_SSD, h->g.NW, a, st));
     return DSX_OK;
 }
 
@@ -238,19 +265,47 @@ int run(dsx_handle *h, const void *dL, const void *dR, int H, int W, int64_t str
             int rc = run_right_pass(h, dL, dR, H, W, stride, h->dRmap, st);
             if (rc) return rc;
         }
-        dsx::PassArgs a = base_args(h, H, W, stride);
+        dsx::Bm2Args a = base_args(h, H, W, stride);
+        a.side = dsx::SIDE_LEFT;
         a.ref = static_cast<const uint8_t *>(dL);
         a.src = static_cast<const uint8_t *>(dR);
         a.dRmap = h->dRmap;
         a.out_fixed = static_cast<int16_t *>(outFixed);
         a.out_float = static_cast<float *>(outFloat);
-        DSX_LAUNCH(h, "bm_pass_left", st, dsx::launch_pass(dsx::SIDE_LEFT, radius, h->g.TX, ssd, a, st));
+        // only strips meeting the valid band [m + D - 1, W - 1 + m] need a search (stereo_core.py:168 crops the rest)
+        const int xlo = std::max(0, h->p.min_disp + h->p.num_disp - 1);
+        const int xhi = std::min(W - 1, W - 1 + h->p.min_disp);
+        if (xlo > xhi) {
+            a.strip_begin = 0;
+            a.strip_count = 0;
+        } else {
+            a.strip_begin = xlo / dsx::kStripWidth;
+            a.strip_count = xhi / dsx::kStripWidth + 1 - a.strip_begin;
+        }
+        uint64_t *tl = nullptr;
+        const char *tlpath = getenv("DSX_TIMELINE");
+        if (tlpath && *tlpath) DSX_HIP(hipMalloc(&tl, 12 * 8 * 65536));
+        if (tl) DSX_HIP(hipMemsetAsync(tl, 0, 12 * 8 * 65536, st));
+        a.timeline = tl;
+        DSX_LAUNCH(h, "bm_pass_left", st, dsx::launch_bm2(radius, ssd, h->g.NW, a, st));
+        if (tl) {
+            std::vector<uint64_t> host(12 * 65536);
+            DSX_HIP(hipStreamSynchronize(st));
+            DSX_HIP(hipMemcpy(host.data(), tl, host.size() * 8, hipMemcpyDeviceToHost));
+            FILE *f = fopen(tlpath, "wb");
+            if (f) {
+                fwrite(host.data(), 8, host.size(), f);
+                fclose(f);
+            }
+            (void)hipFree(tl);
+        }
     } else {
-        dsx::PassArgs a = base_args(h, H, W, stride);
+        dsx::Bm2Args a = base_args(h, H, W, stride);
+        a.side = dsx::SIDE_VOLUME;
         a.ref = static_cast<const uint8_t *>(dL);
         a.src = static_cast<const uint8_t *>(dR);
         a.vol = h->vol;
-        DSX_LAUNCH(h, "cost_volume", st, dsx::launch_pass(dsx::SIDE_VOLUME, radius, h->g.TX, ssd, a, st));
+        DSX_LAUNCH(h, "cost_volume", st, dsx::launch_bm2(radius, ssd, h->g.NW, a, st));
         dsx::VolArgs v{};
         v.vol = h->vol;
         v.H = H;
@@ -332,7 +387,7 @@ int dsx_create(int device, const dsx_params *p, dsx_handle **out) {
     dsx_handle *h = new dsx_handle();
     h->device = device;
     h->p = *p;
-    pick_geometry(p->num_disp, h->g);
+    pick_geometry(p->num_disp, p->cost, h->g);
     hipError_t e = hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking);
     if (e != hipSuccess) {
         delete h;
@@ -350,7 +405,7 @@ int dsx_set_params(dsx_handle *h, const dsx_params *p) {
     DSX_HIP(hipSetDevice(h->device));
     DSX_HIP(hipStreamSynchronize(h->stream));
     h->p = *p;
-    pick_geometry(p->num_disp, h->g);
+    pick_geometry(p->num_disp, p->cost, h->g);
     return DSX_OK;
 }
 
@@ -375,6 +430,8 @@ int dsx_right_map_device(dsx_handle *h, const void *dL, const void *dR, int32_t 
     int rc = check_shape(H, W, stride_bytes);
     if (rc) return rc;
     DSX_HIP(hipSetDevice(h->device));
+    rc = ensure_buffers(h, H, W, false);
+    if (rc) return rc;
     return run_right_pass(h, dL, dR, H, W, stride_bytes, static_cast<int16_t *>(d_out_dR),
                           static_cast<hipStream_t>(hip_stream));
 }
@@ -442,6 +499,8 @@ int dsx_workspace_bytes(dsx_handle *h, int64_t *bytes) {
     int64_t b = 0;
     if (h->dL) b += n * (1 + 1 + 2 + 4);
     if (h->dRmap) b += n * 2;
+    if (h->dL16) b += (int64_t)h->cH * h->pitch16 * 2;
+    if (h->dR16) b += (int64_t)h->cH * h->pitch16 * 2;
     b += (int64_t)h->vol_bytes;
     *bytes = b;
     return DSX_OK;

@@ -1,0 +1,735 @@
+// bm2: fused block-matching pass for gfx950 (SURVEY.md 8a row A5'; replaces the arithmetic
+// of cv2.StereoSGBM::compute called at depthlib/stereo_core.py:231).
+//
+// Work decomposition
+//   * One block = NW waves = Dp disparities. SAD lanes own a disparity PAIR (d0, d0+1) whose
+//     costs live in the two u16 halves of one VGPR (v_pk_{max,min,add,sub}_u16: two
+//     disparities per VALU op, SAD window sums <= 225*255 fit u16); SSD lanes own one
+//     disparity in u32.
+//   * The image is cut into vertical strips of TX = 32 output columns.  The (strip, row)
+//     space is split evenly over a persistent grid (blocks = resident capacity), each block
+//     sweeping down contiguous rows of a strip with running column sums (2 absolute
+//     differences per column per row: the entering and the leaving row), so there is no
+//     tail generation and no per-tile re-initialisation except at segment starts.
+//   * Rows are staged through an LDS ring of 2R+2 rows.  The searched row is stored as
+//     S[j] = {src(pos(j)), src(pos(j+1))} u16 pairs in "disparity order" (j grows with d),
+//     so a lane reads the pair for its two disparities with one aligned ds_read_b64 per two
+//     columns; the reference row is wave-uniform and is consumed from SGPRs.  The next row
+//     is prefetched from HBM into VGPRs while the current row computes.
+//   * Per row the TX x Dp costs go to an LDS tile; the epilogue re-reads it with TPP = 2*NW
+//     lanes per pixel (DSL = Dp/TPP disparities each), finds the minimum with packed block
+//     minima (8 disparities per 16-B read), the lowest winning d with a short scan of the
+//     winning block, combines the TPP lanes with DPP quad_perm / ds_swizzle, and applies the
+//     uniqueness test, the parabola sub-pixel and the left-right check.
+//   side 0 (left)   : full epilogue -> int16 x16 + float disparity
+//   side 1 (right)  : argmin only   -> right-view winners dR (LR check input)
+//   side 2 (volume) : tile copied to the [H][W][Dp] cost volume (north-star "K1")
+#include "dsx_internal.h"
+
+namespace dsx {
+
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ u16x2 as2(uint32_t v) { return __builtin_bit_cast(u16x2, v); }
+__device__ __forceinline__ uint32_t as1(u16x2 v) { return __builtin_bit_cast(uint32_t, v); }
+__device__ __forceinline__ int clampi2(int v, int lo, int hi) { return v < lo ? lo : (v > hi ? hi : v); }
+__device__ __forceinline__ uint32_t umin2(uint32_t a, uint32_t b) { return a < b ? a : b; }
+__host__ __device__ constexpr int rnd16(int v) { return (v + 15) & ~15; }
+
+template <int R, bool SSD, int NW>
+struct Geo {
+    static constexpr int TX = 32;
+    static constexpr int NC = TX + 2 * R;     // column sums per lane (even)
+    static constexpr int KD = SSD ? 1 : 2;    // disparities per lane
+    static constexpr int LDW = 64 * KD;       // disparities per wave
+    static constexpr int Dp = NW * LDW;
+    static constexpr int NT = 64 * NW;
+    static constexpr int TPP = NT / TX;       // epilogue lanes per pixel (2*NW)
+    static constexpr int DSL = Dp / TPP;      // disparities per epilogue lane (64 SAD, 32 SSD)
+    static constexpr int CB = SSD ? 4 : 2;    // cost bytes
+    static constexpr int PITCH = Dp * CB + 16;
+    static constexpr int NJ = NC + Dp;        // S entries per staged row
+    static constexpr int REFW = rnd16(NC + 4);  // >= 4 * ceil(NC / 4)
+    static constexpr int SROW = rnd16(NJ * 4 + 16);  // >= 16 * ceil(NJ / 4): whole-lane b128 stores
+    static constexpr int MAXJ = (NJ + NT - 1) / NT;
+    static constexpr int NB = DSL / 8;        // 8-disparity blocks per epilogue lane
+    static constexpr int REFB = rnd16(2 * (NC + 8));  // reference row as u16 pairs (broadcast reads)
+    static constexpr int SLOT = SROW + REFB;
+    static constexpr int DRN = TX + Dp;  // staged dR values per row (LR check)
+    static constexpr int SMEM0 = 4 * SLOT + TX * PITCH + rnd16(2 * DRN * 2);
+    static constexpr int SMEM = SMEM0 > (2 * R + 1) * SLOT ? SMEM0 : (2 * R + 1) * SLOT;
+};
+
+// Diagnostic build (-DDSX_STAMPS, libdsx_diag.so): per-phase s_memtime sums per block.
+#ifdef DSX_STAMPS
+#define DSX_STAMP(i)                                                                        \
+    do {                                                                                    \
+        __builtin_amdgcn_sched_barrier(0);                                                  \
+        uint64_t t_;                                                                        \
+        asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");          \
+        __builtin_amdgcn_sched_barrier(0);                                                  \
+        if ((i) > 0) ph[(i)-1] += t_ - t_prev;                                              \
+        t_prev = t_;                                                                        \
+    } while (0)
+#else
+#define DSX_STAMP(i) \
+    do {             \
+    } while (0)
+#endif
+
+// Workgroup barrier that orders LDS only: global loads (the next-row prefetch) stay in flight
+// across it, unlike __syncthreads() which drains vmcnt as well.
+__device__ __forceinline__ void lds_barrier() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
+// Block-level LDS ordering: a single-wave block needs no barrier (a wave's LDS operations
+// execute in order), only a compiler fence; multi-wave blocks use the LDS-only barrier.
+template <int NW>
+__device__ __forceinline__ void block_sync() {
+    if constexpr (NW == 1) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront", "local");
+    } else {
+        lds_barrier();
+    }
+}
+
+template <int TPP>
+__device__ __forceinline__ uint32_t gmin(uint32_t v) {
+    if constexpr (TPP > 1) v = umin2(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xF, 0xF, false));
+    if constexpr (TPP > 2) v = umin2(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x4E, 0xF, 0xF, false));
+    if constexpr (TPP > 4) v = umin2(v, (uint32_t)__builtin_amdgcn_ds_swizzle((int)v, 0x101F));
+    if constexpr (TPP > 8) v = umin2(v, (uint32_t)__builtin_amdgcn_ds_swizzle((int)v, 0x201F));
+    return v;
+}
+
+// q = trunc(num / den2) (C semantics), den2 > 0, |q| small: float estimate + exact fix-up.
+__device__ __forceinline__ int div_trunc_small(int num, int den2) {
+    int q = (int)__builtin_truncf((float)num * __builtin_amdgcn_rcpf((float)den2));
+    int r = num - q * den2;
+    if (num >= 0) {
+        if (r < 0) { --q; r += den2; }
+        if (r >= den2) { ++q; }
+    } else {
+        if (r > 0) { ++q; r -= den2; }
+        if (r <= -den2) { --q; }
+    }
+    return q;
+}
+
+typedef const __attribute__((address_space(4))) uint32_t cu32;
+
+// One segment: strip x0, rows [yb, ye). FAST: every staged search position lies inside the
+// image (one unaligned dword + one byte load per lane and row); otherwise replicate-clamped
+// byte loads. All per-row state is in plain registers (no structs / arrays with runtime
+// indices, which hipcc would demote to scratch).
+template <int R, bool SSD, int NW, int SIDE, bool FAST>
+__device__ __forceinline__ void bm2_segment(const Bm2Args &a, uint8_t *smem, int x0, int yb, int ye, bool lr_on
+#ifdef DSX_STAMPS
+                                            , uint64_t (&ph)[8], uint64_t &t_prev, uint64_t &nsteps
+#endif
+) {
+    using G = Geo<R, SSD, NW>;
+    constexpr int TX = G::TX, NC = G::NC, Dp = G::Dp, NT = G::NT, TPP = G::TPP, DSL = G::DSL, CB = G::CB,
+                  PITCH = G::PITCH, NJ = G::NJ, SLOT = G::SLOT, NB = G::NB, NJ4 = (NJ + 3) / 4,
+                  NCH = (NC + 7) / 8;
+    constexpr int side = SIDE;
+    typedef typename std::conditional<SSD, uint32_t, u16x2>::type acc_t;
+    uint8_t *tile = smem + 4 * SLOT;
+    int16_t *dRs = reinterpret_cast<int16_t *>(smem + 4 * SLOT + TX * PITCH);  // 2 x G::DRN staged dR rows
+
+    const int tid = threadIdx.x;
+    const int wv = tid >> 6, ln = tid & 63;
+    const int H = a.H, W = a.W, m = a.m, D = a.D;
+    const int64_t stride = a.stride;
+    const int d0 = SSD ? (wv * 64 + ln) : (wv * 128 + 2 * ln);
+    const uint32_t padv = a.padv;
+    // S index j -> search position: left  j = d + NC-1-c, pos = PB - j  (pos = x' - m - d)
+    //                               right j = d + c,      pos = PB + j  (pos = x' + m + d)
+    const int PB = side == 1 ? (x0 - R + m) : (x0 - R - m + NC - 1);
+    const int sgn = side == 1 ? 1 : -1;
+    const int xr0 = x0 - m - (D - 1);  // first right-view column the LR check can reference
+
+    // ---- raw row loads (registers) and their LDS stores ----
+    // FAST: w0 = dword of 4 search bytes, w1 = the 5th byte; SLOW: w0..w3 = finished S words
+    constexpr int NC4 = (NC + 3) / 4;
+    auto ld = [&](int r, uint32_t &w0, uint32_t &w1, uint32_t &w2, uint32_t &w3, uint32_t &rf) __attribute__((always_inline)) {
+        const int yy = clampi2(r, 0, H - 1);
+        const uint8_t *srow = a.src + (long)yy * stride;
+        const uint8_t *rrow = a.ref + (long)yy * stride;
+        if constexpr (FAST) {
+            rf = tid < NC4 ? *reinterpret_cast<const uint32_t *>(rrow + x0 - R + 4 * tid) : 0u;
+        } else {
+            uint32_t v = 0;
+            if (tid < NC4) {
+#pragma unroll
+                for (int q = 0; q < 4; ++q) v |= (uint32_t)rrow[clampi2(x0 - R + 4 * tid + q, 0, W - 1)] << (8 * q);
+            }
+            rf = v;
+        }
+        if constexpr (FAST) {
+            w0 = 0;
+            w1 = 0;
+            if (tid < NJ4) {
+                const uint8_t *p = side == 1 ? srow + PB + 4 * tid : srow + PB - 4 * tid - 3;
+                w0 = *reinterpret_cast<const uint32_t *>(p);
+                w1 = side == 1 ? p[4] : p[-1];
+            }
+        } else {
+            uint32_t v[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int j = 4 * tid + q;
+                uint32_t t = 0;
+                if (j < NJ) {
+                    const int pp = PB + sgn * j;
+                    t = srow[clampi2(pp, 0, W - 1)];
+                    if constexpr (!SSD) t |= (uint32_t)srow[clampi2(pp + sgn, 0, W - 1)] << 16;
+                }
+                v[q] = t;
+            }
+            w0 = v[0];
+            w1 = v[1];
+            w2 = v[2];
+            w3 = v[3];
+        }
+    };
+    auto st = [&](int sl, uint32_t w0, uint32_t w1, uint32_t w2, uint32_t w3, uint32_t rf) __attribute__((always_inline)) {
+        if (tid < NC4) {
+            const uint32_t r01 = __builtin_amdgcn_perm(0u, rf, 0x0C010C00u);  // {ref[4t], ref[4t+1]} as u16
+            const uint32_t r23 = __builtin_amdgcn_perm(0u, rf, 0x0C030C02u);
+            *reinterpret_cast<uint2 *>(smem + sl * SLOT + G::SROW + 8 * tid) = make_uint2(r01, r23);
+        }
+        if constexpr (FAST) {
+            const uint32_t dw = w0, e = w1;
+            if constexpr (SSD) {
+                if (side == 1) {
+                    w0 = dw & 0xFFu; w1 = (dw >> 8) & 0xFFu; w2 = (dw >> 16) & 0xFFu; w3 = dw >> 24;
+                } else {
+                    w0 = dw >> 24; w1 = (dw >> 16) & 0xFFu; w2 = (dw >> 8) & 0xFFu; w3 = dw & 0xFFu;
+                }
+            } else {
+                if (side == 1) {
+                    w0 = __builtin_amdgcn_perm(e, dw, 0x0C010C00u);
+                    w1 = __builtin_amdgcn_perm(e, dw, 0x0C020C01u);
+                    w2 = __builtin_amdgcn_perm(e, dw, 0x0C030C02u);
+                    w3 = __builtin_amdgcn_perm(e, dw, 0x0C040C03u);
+                } else {
+                    w0 = __builtin_amdgcn_perm(e, dw, 0x0C020C03u);
+                    w1 = __builtin_amdgcn_perm(e, dw, 0x0C010C02u);
+                    w2 = __builtin_amdgcn_perm(e, dw, 0x0C000C01u);
+                    w3 = __builtin_amdgcn_perm(e, dw, 0x0C040C00u);
+                }
+            }
+        }
+        if (tid < NJ4) *reinterpret_cast<uint4 *>(smem + sl * SLOT + 16 * tid) = make_uint4(w0, w1, w2, w3);
+    };
+    // right-view winners of row r (LR check), staged next to the tile
+    constexpr int DRQ = (G::DRN + NT - 1) / NT;
+    auto ld_dr = [&](int r, uint32_t(&v)[DRQ]) __attribute__((always_inline)) {
+        const int16_t *row = a.dRmap + (long)clampi2(r, 0, H - 1) * W;
+#pragma unroll
+        for (int q = 0; q < DRQ; ++q) {
+            const int j = tid + q * NT;
+            v[q] = j < G::DRN ? (uint16_t)row[clampi2(xr0 + j, 0, W - 1)] : 0u;
+        }
+    };
+    auto st_dr = [&](int buf, const uint32_t(&v)[DRQ]) __attribute__((always_inline)) {
+#pragma unroll
+        for (int q = 0; q < DRQ; ++q) {
+            const int j = tid + q * NT;
+            if (j < G::DRN) dRs[buf * G::DRN + j] = (int16_t)v[q];
+        }
+    };
+    // reference pixels of slot sl, columns [c0, c0+8): one broadcast 16-B LDS read (u16 pairs)
+    auto ref_chunk = [&](int sl, int c0, uint32_t(&rw)[4]) __attribute__((always_inline)) {
+        const uint4 v = *reinterpret_cast<const uint4 *>(smem + sl * SLOT + G::SROW + 2 * c0);
+        rw[0] = v.x;
+        rw[1] = v.y;
+        rw[2] = v.z;
+        rw[3] = v.w;
+    };
+    auto refpk = [](const uint32_t(&rw)[4], int c) __attribute__((always_inline)) -> u16x2 {
+        const u16x2 v = as2(rw[c >> 1]);
+        return (c & 1) ? v.yy : v.xx;
+    };
+    auto refv = [](const uint32_t(&rw)[4], int c) __attribute__((always_inline)) -> uint32_t {
+        return (c & 1) ? (rw[c >> 1] >> 16) : (rw[c >> 1] & 0xFFFFu);
+    };
+    // this lane's S words for columns [c0, c0+8) of slot sl
+    auto s_chunk = [&](int sl, int c0, uint32_t(&sw)[8]) __attribute__((always_inline)) {
+        const uint8_t *base = smem + sl * SLOT + d0 * 4;
+        if constexpr (side == 1) {
+            if constexpr (SSD) {
+#pragma unroll
+                for (int c = 0; c < 8; ++c) sw[c] = *reinterpret_cast<const uint32_t *>(base + (c0 + c) * 4);
+            } else {
+                base = (const uint8_t *)__builtin_assume_aligned(base, 8);
+#pragma unroll
+                for (int c = 0; c < 8; c += 2) {
+                    const uint2 v = *reinterpret_cast<const uint2 *>(base + (c0 + c) * 4);
+                    sw[c] = v.x;
+                    sw[c + 1] = v.y;
+                }
+            }
+        } else {
+            if constexpr (SSD) {
+#pragma unroll
+                for (int c = 0; c < 8; ++c) sw[c] = *reinterpret_cast<const uint32_t *>(base + (NC - 1 - c0 - c) * 4);
+            } else {
+                base = (const uint8_t *)__builtin_assume_aligned(base, 8);
+#pragma unroll
+                for (int c = 1; c < 8; c += 2) {
+                    const uint2 v = *reinterpret_cast<const uint2 *>(base + (NC - 1 - c0 - c) * 4);
+                    sw[c] = v.x;
+                    sw[c - 1] = v.y;
+                }
+            }
+        }
+    };
+
+    // ---- segment init: rows yb-R .. yb+R staged in slots 0..2R (may overlap the tile) ----
+    block_sync<NW>();
+    {
+        // groups of IG rows in flight: bounds the init phase's VGPRs below the main loop's
+        constexpr int IG = 3;
+#pragma unroll 1
+        for (int i0 = 0; i0 <= 2 * R; i0 += IG) {
+            uint32_t iw[IG][5];
+#pragma unroll
+            for (int i = 0; i < IG; ++i)
+                if (i0 + i <= 2 * R) ld(yb - R + i0 + i, iw[i][0], iw[i][1], iw[i][2], iw[i][3], iw[i][4]);
+#pragma unroll
+            for (int i = 0; i < IG; ++i)
+                if (i0 + i <= 2 * R) st(i0 + i, iw[i][0], iw[i][1], iw[i][2], iw[i][3], iw[i][4]);
+        }
+    }
+    block_sync<NW>();
+    acc_t cs[NC];
+#pragma unroll
+    for (int c = 0; c < NC; ++c) cs[c] = acc_t(0);
+#pragma unroll 1
+    for (int i = 0; i <= 2 * R; ++i) {  // runtime loop: a full unroll makes compile time explode
+#pragma unroll
+        for (int q = 0; q < NCH; ++q) {
+            const int c0 = 8 * q;
+            uint32_t sw[8], rw[4];
+            s_chunk(i, c0, sw);
+            ref_chunk(i, c0, rw);
+#pragma unroll
+            for (int c = 0; c < 8; ++c) {
+                if (c0 + c < NC) {
+                    if constexpr (SSD) {
+                        const int t = (int)refv(rw, c) - (int)sw[c];
+                        cs[c0 + c] += (uint32_t)(t * t);
+                    } else {
+                        const u16x2 Lp = refpk(rw, c), sv = as2(sw[c]);
+                        cs[c0 + c] += __builtin_elementwise_max(Lp, sv) - __builtin_elementwise_min(Lp, sv);
+                    }
+                }
+            }
+        }
+    }
+    block_sync<NW>();  // init rows (which overlap the tile) are consumed
+
+    // tile padding: disparities >= D never win
+    for (int q = tid; q < TX * (Dp - D); q += NT) {
+        const int k = q / (Dp - D), d = D + (q - k * (Dp - D));
+        if constexpr (SSD) *reinterpret_cast<uint32_t *>(tile + k * PITCH + d * 4) = padv;
+        else *reinterpret_cast<uint16_t *>(tile + k * PITCH + d * 2) = (uint16_t)padv;
+    }
+    // stage the first row's dR segment (left pass with LR check)
+    if (side == 0 && lr_on) {
+        uint32_t v[DRQ];
+        ld_dr(yb, v);
+        st_dr(yb & 1, v);
+    }
+    block_sync<NW>();
+
+    const bool edge = side == 1 && (x0 + m < 0 || x0 + TX - 1 + m + Dp - 1 > W - 1);
+    const bool dodd = !SSD && (D & 1);
+    const bool lane_writes = d0 < D;
+
+    for (int y = yb; y < ye; ++y) {
+#ifdef DSX_STAMPS
+        ++nsteps;
+#endif
+        DSX_STAMP(0);
+        const int par = (y & 1) * 2;  // slots {par, par+1} = {new row y+R, old row y-R-1}
+        const bool more = y + 1 < ye;
+        // prefetch the next step's entering / leaving rows (+ its dR segment); lands during this step
+        uint32_t pn0 = 0, pn1 = 0, pn2 = 0, pn3 = 0, pnr = 0, po0 = 0, po1 = 0, po2 = 0, po3 = 0, por = 0;
+        uint32_t pd[DRQ];
+        if (more) {
+            ld(y + 1 + R, pn0, pn1, pn2, pn3, pnr);
+            ld(y - R, po0, po1, po2, po3, por);
+            if (side == 0 && lr_on) ld_dr(y + 1, pd);
+        }
+        if (y > yb) {
+#pragma unroll
+            for (int q = 0; q < NCH; ++q) {
+                const int c0 = 8 * q;
+                uint32_t sn[8], so[8], rn[4], ro[4];
+                ref_chunk(par, c0, rn);
+                ref_chunk(par + 1, c0, ro);
+                s_chunk(par, c0, sn);
+                s_chunk(par + 1, c0, so);
+#pragma unroll
+                for (int c = 0; c < 8; ++c) {
+                    if (c0 + c < NC) {
+                        if constexpr (SSD) {
+                            const int tn = (int)refv(rn, c) - (int)sn[c];
+                            const int to = (int)refv(ro, c) - (int)so[c];
+                            cs[c0 + c] += (uint32_t)(tn * tn) - (uint32_t)(to * to);
+                        } else {
+                            const u16x2 Lnp = refpk(rn, c), Lop = refpk(ro, c);
+                            const u16x2 vn = as2(sn[c]), vo = as2(so[c]);
+                            cs[c0 + c] = cs[c0 + c] +
+                                         (__builtin_elementwise_max(Lnp, vn) - __builtin_elementwise_min(Lnp, vn)) -
+                                         (__builtin_elementwise_max(Lop, vo) - __builtin_elementwise_min(Lop, vo));
+                        }
+                    }
+                }
+            }
+        }
+        DSX_STAMP(1);
+        DSX_STAMP(2);
+        // ---- horizontal running box sum -> LDS tile (pixel k, disparity d0..) ----
+        {
+            uint8_t *tb = tile + d0 * CB;
+            acc_t acc = cs[0];
+#pragma unroll
+            for (int c = 1; c <= 2 * R; ++c) acc += cs[c];
+            if (lane_writes) {
+#pragma unroll
+                for (int k = 0; k < TX; ++k) {
+                    if (k > 0) acc = acc + cs[k + 2 * R] - cs[k - 1];
+                    if constexpr (SSD) *reinterpret_cast<uint32_t *>(tb + k * PITCH) = acc;
+                    else *reinterpret_cast<uint32_t *>(tb + k * PITCH) = as1(acc);
+                }
+            }
+            if (dodd && d0 + 1 == D) {  // odd D: the high half of the last pair is disparity D
+                for (int k = 0; k < TX; ++k) *reinterpret_cast<uint16_t *>(tb + k * PITCH + 2) = (uint16_t)padv;
+            }
+            if (edge && lane_writes) {  // right pass: x + m + d must stay inside [0, W-1]
+                const int base = x0 + m + d0;
+                for (int k = 0; k < TX; ++k) {
+                    const int p0 = base + k;
+                    if constexpr (SSD) {
+                        if (p0 < 0 || p0 > W - 1) *reinterpret_cast<uint32_t *>(tb + k * PITCH) = padv;
+                    } else {
+                        if (p0 < 0 || p0 > W - 1) *reinterpret_cast<uint16_t *>(tb + k * PITCH) = (uint16_t)padv;
+                        if (p0 + 1 < 0 || p0 + 1 > W - 1) *reinterpret_cast<uint16_t *>(tb + k * PITCH + 2) = (uint16_t)padv;
+                    }
+                }
+            }
+        }
+        DSX_STAMP(3);
+        block_sync<NW>();
+        DSX_STAMP(4);
+        if constexpr (side == 2) {
+            // ---- cost volume store: TX pixels x Dp costs, 16-B chunks ----
+            constexpr int CPP = Dp * CB / 16;
+            for (int q = tid; q < TX * CPP; q += NT) {
+                const int k = q / CPP, off = (q - k * CPP) * 16;
+                const int x = x0 + k;
+                if (x < W) {
+                    const uint4 v = *reinterpret_cast<const uint4 *>(tile + k * PITCH + off);
+                    *reinterpret_cast<uint4 *>(reinterpret_cast<uint8_t *>(a.vol) + ((size_t)y * W + x) * (Dp * CB) + off) = v;
+                }
+            }
+        } else {
+            // ---- epilogue: TPP lanes per pixel ----
+            const int k = tid / TPP, h = tid % TPP;
+            const int x = x0 + k;
+            const uint8_t *px = tile + k * PITCH + h * DSL * CB;
+            uint32_t bs[NB];
+#pragma unroll
+            for (int i = 0; i < NB; ++i) {
+                if constexpr (SSD) {
+                    const uint4 v0 = *reinterpret_cast<const uint4 *>(px + 32 * i);
+                    const uint4 v1 = *reinterpret_cast<const uint4 *>(px + 32 * i + 16);
+                    bs[i] = umin2(umin2(umin2(v0.x, v0.y), umin2(v0.z, v0.w)), umin2(umin2(v1.x, v1.y), umin2(v1.z, v1.w)));
+                } else {
+                    const uint4 v = *reinterpret_cast<const uint4 *>(px + 16 * i);
+                    const u16x2 mm = __builtin_elementwise_min(__builtin_elementwise_min(as2(v.x), as2(v.y)),
+                                                               __builtin_elementwise_min(as2(v.z), as2(v.w)));
+                    bs[i] = umin2(mm.x, mm.y);
+                }
+            }
+            uint32_t lmin = bs[0];
+#pragma unroll
+            for (int i = 1; i < NB; ++i) lmin = umin2(lmin, bs[i]);
+            const uint32_t cb = gmin<TPP>(lmin);
+            int bsel = -1;
+#pragma unroll
+            for (int i = NB - 1; i >= 0; --i) bsel = bs[i] == cb ? i : bsel;
+            uint32_t dl = 0xFFFFu;
+            if (bsel >= 0) {
+                uint32_t c8[8];
+                if constexpr (SSD) {
+                    const uint4 v0 = *reinterpret_cast<const uint4 *>(px + 32 * bsel);
+                    const uint4 v1 = *reinterpret_cast<const uint4 *>(px + 32 * bsel + 16);
+                    c8[0] = v0.x; c8[1] = v0.y; c8[2] = v0.z; c8[3] = v0.w;
+                    c8[4] = v1.x; c8[5] = v1.y; c8[6] = v1.z; c8[7] = v1.w;
+                } else {
+                    const uint4 v = *reinterpret_cast<const uint4 *>(px + 16 * bsel);
+                    c8[0] = v.x & 0xFFFFu; c8[1] = v.x >> 16; c8[2] = v.y & 0xFFFFu; c8[3] = v.y >> 16;
+                    c8[4] = v.z & 0xFFFFu; c8[5] = v.z >> 16; c8[6] = v.w & 0xFFFFu; c8[7] = v.w >> 16;
+                }
+                int e = 7;
+#pragma unroll
+                for (int q = 6; q >= 0; --q) e = c8[q] == cb ? q : e;
+                dl = (uint32_t)(h * DSL + 8 * bsel + e);
+            }
+            const int b = (int)gmin<TPP>(dl);
+            const long o = (long)y * W + x;
+            if constexpr (side == 1) {
+                if (h == 0 && x < W) a.out_dR[o] = cb == padv ? (int16_t)-1 : (int16_t)b;
+            } else {
+                bool valid = x < W && x >= m + D - 1 && x <= W - 1 + m;
+                if (a.uniq > 0) {
+                    const int rel = b - h * DSL;
+                    uint32_t nm = 0xFFFFFFFFu;
+#pragma unroll
+                    for (int i = 0; i < NB; ++i) {
+                        const bool hit = rel >= 8 * i - 1 && rel <= 8 * i + 8;
+                        nm = hit ? nm : umin2(nm, bs[i]);
+                    }
+                    const int ib0 = (rel - 1) >> 3, ib1 = (rel + 1) >> 3;
+#pragma unroll
+                    for (int t = 0; t < 2; ++t) {
+                        const int ib = t == 0 ? ib0 : ib1;
+                        if (ib >= 0 && ib < NB && (t == 0 || ib1 != ib0)) {
+#pragma unroll
+                            for (int e = 0; e < 8; ++e) {
+                                uint32_t c;
+                                if constexpr (SSD) c = reinterpret_cast<const uint32_t *>(px)[8 * ib + e];
+                                else c = reinterpret_cast<const uint16_t *>(px)[8 * ib + e];
+                                const int dd = 8 * ib + e - rel;
+                                if (dd > 1 || dd < -1) nm = umin2(nm, c);
+                            }
+                        }
+                    }
+                    nm = gmin<TPP>(nm);
+                    if ((uint64_t)nm * (uint64_t)(100 - a.uniq) < (uint64_t)cb * 100u) valid = false;
+                }
+                int32_t f = b * 16;
+                float pf = (float)(m + b);
+                if (a.subpix && b > 0 && b < D - 1) {
+                    int32_t cm, cp;
+                    const uint8_t *pk = tile + k * PITCH;
+                    if constexpr (SSD) {
+                        cm = (int32_t)reinterpret_cast<const uint32_t *>(pk)[b - 1];
+                        cp = (int32_t)reinterpret_cast<const uint32_t *>(pk)[b + 1];
+                    } else {
+                        cm = reinterpret_cast<const uint16_t *>(pk)[b - 1];
+                        cp = reinterpret_cast<const uint16_t *>(pk)[b + 1];
+                    }
+                    int32_t den = cm + cp - 2 * (int32_t)cb;
+                    den = den < 1 ? 1 : den;
+                    f += div_trunc_small((cm - cp) * 16 + den, 2 * den);
+                    if (a.float_mode == 1) pf = (float)(m + b) + (float)(cm - cp) / (float)(2 * den);
+                }
+                if (lr_on && valid) {
+                    const int dr = dRs[(y & 1) * G::DRN + (x - m - b - xr0)];
+                    const int df = dr - b;
+                    if (df > a.lr || df < -a.lr) valid = false;
+                }
+                if (h == 0 && x < W) {
+                    const int16_t fx = valid ? (int16_t)(m * 16 + f) : (int16_t)((m - 1) * 16);
+                    if (a.out_fixed) a.out_fixed[o] = fx;
+                    if (a.out_float) a.out_float[o] = a.float_mode == 0 ? (float)fx * 0.0625f : (valid ? pf : (float)(m - 1));
+                }
+            }
+        }
+        DSX_STAMP(5);
+        if (more) {
+            st(par ^ 2, pn0, pn1, pn2, pn3, pnr);
+            st((par ^ 2) + 1, po0, po1, po2, po3, por);
+            if (side == 0 && lr_on) st_dr((y + 1) & 1, pd);
+        }
+        DSX_STAMP(6);
+        block_sync<NW>();
+        DSX_STAMP(7);
+    }
+}
+
+template <int R, bool SSD, int NW, int SIDE>
+__global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(3))) void bm2(Bm2Args a) {
+    using G = Geo<R, SSD, NW>;
+    constexpr int TX = G::TX, NT = G::NT, NC = G::NC, NJ = G::NJ;
+    constexpr int side = SIDE;
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    const int tid = threadIdx.x;
+    const int H = a.H, W = a.W, m = a.m;
+    uint64_t t_start = 0;
+    if (a.timeline && tid == 0) t_start = __builtin_amdgcn_s_memrealtime();
+#ifdef DSX_STAMPS
+    uint64_t ph[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    uint64_t t_prev = 0;
+    uint64_t nsteps = 0;
+#endif
+
+    // ---- left pass: columns of strips that lie entirely in the invalid band ----
+    if (side == 0 && (a.out_fixed || a.out_float)) {
+        const int xa = a.strip_begin * TX, xb = min(W, (a.strip_begin + a.strip_count) * TX);
+        const int nin = xa + (W - xb);
+        const long total = (long)nin * H;
+        const int16_t fi = (int16_t)((m - 1) * 16);
+        for (long q = (long)blockIdx.x * NT + tid; q < total; q += (long)gridDim.x * NT) {
+            const int y = (int)(q / nin), c = (int)(q - (long)y * nin);
+            const int x = c < xa ? c : xb + (c - xa);
+            const long o = (long)y * W + x;
+            if (a.out_fixed) a.out_fixed[o] = fi;
+            if (a.out_float) a.out_float[o] = (float)(m - 1);
+        }
+    }
+
+    // ---- work partition: with at least one block per strip, every block owns ONE contiguous
+    // run of rows of ONE strip (balanced to +-1 block per strip); otherwise an even split of
+    // the linearised (strip, row) space.
+    const int NS = a.strip_count;
+    const long NG = gridDim.x, b = blockIdx.x;
+    long lin0, lin1;
+    if (NG >= NS && NS > 0) {
+        const int s = (int)(b * NS / NG);
+        const long bs0 = ((long)s * NG + NS - 1) / NS, bs1 = ((long)(s + 1) * NG + NS - 1) / NS;
+        const long j = b - bs0, cnt = bs1 - bs0;
+        lin0 = (long)s * H + j * H / cnt;
+        lin1 = (long)s * H + (j + 1) * H / cnt;
+    } else {
+        const long T = (long)NS * H;
+        lin0 = b * T / NG;
+        lin1 = (b + 1) * T / NG;
+    }
+    const bool lr_on = side == 0 && a.lr >= 0 && a.dRmap != nullptr;
+    for (long it = lin0; it < lin1;) {
+        const int s = a.strip_begin + (int)(it / H);
+        const int yb = (int)(it % H);
+        const int ye = (int)min((long)H, (long)yb + (lin1 - it));
+        it += ye - yb;
+        const int x0 = s * TX;
+        const int PB = side == 1 ? (x0 - R + m) : (x0 - R - m + NC - 1);
+        const int NJ4 = (NJ + 3) / 4;
+        const bool fast = (side == 1 ? (PB >= 0 && PB + 4 * NJ4 <= W - 1) : (PB - 4 * NJ4 >= 0 && PB <= W - 1)) &&
+                          x0 - R >= 0 && x0 - R + 4 * ((NC + 3) / 4) - 1 <= W - 1;
+        if (fast)
+            bm2_segment<R, SSD, NW, SIDE, true>(a, smem, x0, yb, ye, lr_on
+#ifdef DSX_STAMPS
+                                                , ph, t_prev, nsteps
+#endif
+            );
+        else
+            bm2_segment<R, SSD, NW, SIDE, false>(a, smem, x0, yb, ye, lr_on
+#ifdef DSX_STAMPS
+                                                 , ph, t_prev, nsteps
+#endif
+            );
+    }
+    if (a.timeline && tid == 0) {
+        const uint64_t t_end = __builtin_amdgcn_s_memrealtime();
+        uint64_t *tl = a.timeline + 4 * blockIdx.x;
+        tl[0] = t_start;
+        tl[1] = t_end;
+        tl[2] = (uint64_t)__builtin_amdgcn_s_getreg((4 << 0) | (0 << 6) | (31 << 11));   // HW_REG_HW_ID
+        tl[3] = (uint64_t)__builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (15 << 11));  // HW_REG_XCC_ID
+#ifdef DSX_STAMPS
+        uint64_t *ps = a.timeline + 4 * 65536 + 8 * blockIdx.x;
+        for (int i = 0; i < 7; ++i) ps[i] = ph[i];
+        ps[7] = nsteps;
+#endif
+    }
+}
+
+template <int R, bool SSD, int NW, int SIDE>
+static hipError_t launch_bm2_side(const Bm2Args &a, hipStream_t st) {
+    using G = Geo<R, SSD, NW>;
+    const void *fn = (const void *)bm2<R, SSD, NW, SIDE>;
+    static int blocks_per_cu[64] = {};
+    static int num_cu[64] = {};
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return e;
+    if (dev < 0 || dev >= 64) return hipErrorInvalidDevice;
+    if (!blocks_per_cu[dev]) {
+        e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, G::SMEM);
+        if (e != hipSuccess) return e;
+        int nb = 0;
+        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, fn, G::NT, G::SMEM);
+        if (e != hipSuccess) return e;
+        int cus = 0;
+        e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+        if (e != hipSuccess) return e;
+        // the occupancy API over-reports by one block per CU on gfx950 / ROCm 7.2 (measured with
+        // the DSX_TIMELINE census: 9 of 10 reported 1-wave blocks were co-resident), and a
+        // persistent grid that does not fit runs a second generation
+        blocks_per_cu[dev] = nb > 1 ? nb - 1 : 1;
+        num_cu[dev] = cus > 0 ? cus : 1;
+    }
+    const long T = (long)a.strip_count * a.H;
+    long grid = (long)blocks_per_cu[dev] * num_cu[dev];
+    if (a.grid_override > 0) grid = a.grid_override;
+    if (grid > T) grid = T;
+    if (grid < 1) grid = 1;
+    hipLaunchKernelGGL((bm2<R, SSD, NW, SIDE>), dim3((unsigned)grid), dim3(G::NT), G::SMEM, st, a);
+    return hipGetLastError();
+}
+
+template <int R, bool SSD, int NW>
+static hipError_t launch_bm2_one(const Bm2Args &a, hipStream_t st) {
+    switch (a.side) {
+        case 0: return launch_bm2_side<R, SSD, NW, 0>(a, st);
+        case 1: return launch_bm2_side<R, SSD, NW, 1>(a, st);
+        default: return launch_bm2_side<R, SSD, NW, 2>(a, st);
+    }
+}
+
+template <int R>
+static hipError_t launch_bm2_r(bool ssd, int nw, const Bm2Args &a, hipStream_t st) {
+    if (!ssd) {
+        switch (nw) {
+            case 1: return launch_bm2_one<R, false, 1>(a, st);
+            case 2: return launch_bm2_one<R, false, 2>(a, st);
+            case 4: return launch_bm2_one<R, false, 4>(a, st);
+        }
+    } else {
+        switch (nw) {
+            case 1: return launch_bm2_one<R, true, 1>(a, st);
+            case 2: return launch_bm2_one<R, true, 2>(a, st);
+            case 4: return launch_bm2_one<R, true, 4>(a, st);
+            case 8: return launch_bm2_one<R, true, 8>(a, st);
+        }
+    }
+    return hipErrorInvalidValue;
+}
+
+#define DSX_DECL_BM2(r) hipError_t launch_bm2_radius_##r(bool, int, const Bm2Args &, hipStream_t);
+DSX_DECL_BM2(0) DSX_DECL_BM2(1) DSX_DECL_BM2(2) DSX_DECL_BM2(3)
+DSX_DECL_BM2(4) DSX_DECL_BM2(5) DSX_DECL_BM2(6) DSX_DECL_BM2(7)
+
+#ifdef DSX_RADIUS
+#define DSX_CAT2(x, y) x##y
+#define DSX_CAT(x, y) DSX_CAT2(x, y)
+hipError_t DSX_CAT(launch_bm2_radius_, DSX_RADIUS)(bool ssd, int nw, const Bm2Args &a, hipStream_t st) {
+    return launch_bm2_r<DSX_RADIUS>(ssd, nw, a, st);
+}
+#else
+hipError_t launch_bm2(int radius, bool ssd, int nw, const Bm2Args &a, hipStream_t st) {
+    switch (radius) {
+        case 0: return launch_bm2_radius_0(ssd, nw, a, st);
+        case 1: return launch_bm2_radius_1(ssd, nw, a, st);
+        case 2: return launch_bm2_radius_2(ssd, nw, a, st);
+        case 3: return launch_bm2_radius_3(ssd, nw, a, st);
+        case 4: return launch_bm2_radius_4(ssd, nw, a, st);
+        case 5: return launch_bm2_radius_5(ssd, nw, a, st);
+        case 6: return launch_bm2_radius_6(ssd, nw, a, st);
+        case 7: return launch_bm2_radius_7(ssd, nw, a, st);
+        default: return hipErrorInvalidValue;
+    }
+}
+#endif
+
+}  // namespace dsx

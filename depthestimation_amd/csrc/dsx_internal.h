@@ -7,33 +7,37 @@ namespace dsx {
 
 enum Side : int { SIDE_LEFT = 0, SIDE_RIGHT = 1, SIDE_VOLUME = 2 };
 
-// Launch geometry derived from num_disp (see pick_geometry in dsx_api.cpp).
-//   Dp  : padded disparity count = threads per block of the pass kernels (one lane per d)
-//   TX  : output columns per block = disparities per epilogue slice
-//   TPP : epilogue lanes per pixel (Dp = TX * TPP), reduced with DPP / ds_swizzle
-//   DB  : key shift bits, key = (cost << DB) | d
-struct Geometry {
-    int Dp, TX, TPP, DB;
-};
-
-constexpr int kRowsPerBlock = 32;   // TY: rows swept per block (running column sums)
 constexpr int kVolThreads = 256;    // K2 (volume WTA) block size
 
-struct PassArgs {
+// Launch geometry derived from (num_disp, cost), see pick_geometry in dsx_api.hip.
+//   NW : waves per bm2 block;  Dp : padded disparity count
+//   TX, TPP : K2 (vol_wta) tile = 32-disparity slices, TPP = Dp / 32 lanes per pixel
+//   DB : key shift bits for K2's packed (cost << DB | d) keys
+struct Geometry {
+    int NW, Dp, TX, TPP, DB;
+};
+
+// Arguments of the fused pass kernel bm2 (dsx_bm.hip).
+struct Bm2Args {
     const uint8_t *ref;  // reference image (L for left/volume passes, R for the right pass)
     const uint8_t *src;  // searched image
+    const uint16_t *ref16;  // reference image expanded to u16 with R replicate-padded columns
+    int pitch16;         // row pitch of ref16 in u16 elements (see expand_pitch16)
     int64_t stride;      // row stride of both images in bytes
     int H, W;
     int m;               // min_disp
-    int D, Dp, DB, TPP;
-    int TY;
+    int D;               // num_disp (padded internally to the kernel's Dp)
+    int side;            // 0 left (full epilogue), 1 right (dR map), 2 volume (K1 store)
     int uniq, lr, subpix, float_mode;
-    uint32_t padv;         // cost value stored for padded disparities d >= D
+    uint32_t padv;       // cost stored for disparities outside [0, D) / outside the image
+    int strip_begin, strip_count;  // 32-column strips forming the work space
+    int grid_override;   // >0: force the persistent grid size (tests)
     const int16_t *dRmap;  // right-view winners (left pass with LR)
     int16_t *out_fixed;    // left pass outputs (either may be null)
     float *out_float;
     int16_t *out_dR;       // right pass output
-    void *vol;             // SIDE_VOLUME output [H][W][Dp]
+    void *vol;             // side 2 output [H][W][Dp]
+    uint64_t *timeline;    // debug (DSX_TIMELINE env): per block {start, end, hw_id, xcc_id}
 };
 
 struct VolArgs {
@@ -44,10 +48,21 @@ struct VolArgs {
     float *out_float;
 };
 
-// Returns nullptr-free launch status (hipSuccess or an error).
-hipError_t launch_pass(int side, int radius, int TX, bool ssd, const PassArgs &a, hipStream_t st);
+constexpr int kStripWidth = 32;  // TX of bm2
+
+// nw = waves per block: SAD Dp = 128*nw (nw in {1,2,4}), SSD Dp = 64*nw (nw in {1,2,4,8}).
+hipError_t launch_bm2(int radius, bool ssd, int nw, const Bm2Args &a, hipStream_t st);
 hipError_t launch_volume_wta(int TX, bool ssd, const VolArgs &a, hipStream_t st);
-size_t pass_smem_bytes(int radius, int TX, bool ssd, int Dp, int TPP, int TY);
+
+// u16 expansion of a reference image with `radius` replicate-padded columns on the left:
+// out[y * pitch16 + c] = img[y][clamp(c - radius, 0, W - 1)]  (consumed by bm2 through scalar
+// loads, two columns per SGPR, selected with VOP3P op_sel).
+inline int expand_pitch16(int W, int radius) {
+    const int w32 = (W + 31) / 32 * 32;
+    return (w32 + 2 * radius + 16 + 7) / 8 * 8;
+}
+hipError_t launch_expand_u16(const uint8_t *img, int64_t stride, int H, int W, int radius, uint16_t *out,
+                             int pitch16, hipStream_t st);
 size_t volume_smem_bytes(int TX, bool ssd, int Dp, int TPP, int W);
 
 }  // namespace dsx

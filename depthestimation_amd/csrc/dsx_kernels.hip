@@ -5,8 +5,11 @@
 // matching + WTA + uniqueness + parabola sub-pixel + left-right check), restated on the CPU
 // in oracle/stereo_bm.py.
 //
+// This file holds the K2 reduction of the volume path; the fused pass / K1 is dsx_bm.hip.
+// (Historical v1 notes below describe the cost tile layout that vol_wta still uses.)
+//
 // Kernels
-//   bm_pass<R,TX,SSD,SIDE>  one block = TX output columns x TY rows x all Dp disparities,
+//   [v1 bm_pass, replaced by dsx_bm.hip] one block = TX output columns x TY rows x all Dp disparities,
 //                           one lane per disparity.  Rectified rows are staged once into LDS;
 //                           each lane keeps running column sums for its d in VGPRs and slides
 //                           them down the rows (2 byte-SADs per column per row), takes a
@@ -169,200 +172,6 @@ __device__ __forceinline__ void store_left(const PixelResult &r, bool valid, int
 }
 
 // ---------------------------------------------------------------------------------------
-// bm_pass: fused cost + epilogue (or cost-volume store)
-// ---------------------------------------------------------------------------------------
-template <int R, int TX, bool SSD, int SIDE>
-__global__ __launch_bounds__(512) void bm_pass(PassArgs a) {
-    using G = RowGeom<R, TX>;
-    constexpr int NC = G::NC, NWA = G::NWA, LWP = G::LWP;
-    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-
-    const int tid = threadIdx.x;
-    const int nthr = blockDim.x;  // == Dp
-    const int Dp = a.Dp, TPP = a.TPP, H = a.H, W = a.W, m = a.m;
-    const int x0 = blockIdx.x * TX;
-    const int y0 = blockIdx.y * a.TY;
-    const int rows = min(a.TY, H - y0);
-    const int NR = rows + 2 * R;
-    const int SWP = src_row_bytes(NC, Dp);
-
-    uint8_t *tile = smem;
-    const int tile_bytes = TX * TPP * slice_bytes<TX, SSD>();
-    uint8_t *refS = smem + tile_bytes;
-    uint8_t *srcS = refS + (a.TY + 2 * R) * LWP;
-
-    if constexpr (SIDE == SIDE_LEFT) {
-        // whole tile inside the invalid band: no search needed (cf. the crop at stereo_core.py:168)
-        const int lo = m + a.D - 1, hi = W - 1 + m;
-        if (x0 + TX - 1 < lo || x0 > hi) {
-            for (int idx = tid; idx < rows * TX; idx += nthr) {
-                const int yy = idx / TX, k = idx - yy * TX;
-                const int x = x0 + k;
-                if (x < W) {
-                    const long o = (long)(y0 + yy) * W + x;
-                    PixelResult r{};
-                    store_left(r, false, m, a.float_mode, o, a.out_fixed, a.out_float);
-                }
-            }
-            return;
-        }
-    }
-
-    // ---- stage rectified rows (replicate-clamped) into LDS ----
-    const int pbase = (SIDE == SIDE_RIGHT) ? (x0 - R + m) : (x0 - R - m - (Dp - 1));
-    {
-        const int total = NR * LWP;
-#pragma unroll 8
-        for (int idx = tid; idx < total; idx += nthr) {
-            const int i = idx / LWP, c = idx - i * LWP;
-            const int yy = clampi(y0 - R + i, 0, H - 1);
-            refS[i * LWP + c] = a.ref[(long)yy * a.stride + clampi(x0 - R + c, 0, W - 1)];
-        }
-        const int total2 = NR * SWP;
-#pragma unroll 8
-        for (int idx = tid; idx < total2; idx += nthr) {
-            const int i = idx / SWP, c = idx - i * SWP;
-            const int yy = clampi(y0 - R + i, 0, H - 1);
-            srcS[i * SWP + c] = a.src[(long)yy * a.stride + clampi(pbase + c, 0, W - 1)];
-        }
-        {
-            // padded disparities (d >= D) keep a cost larger than any real one
-            if (Dp > a.D) {
-                for (int idx = tid; idx < TX * (Dp - a.D); idx += nthr) {
-                    const int k = idx / (Dp - a.D);
-                    const int d = a.D + (idx - k * (Dp - a.D));
-                    const int s = d / TX, j = d - s * TX;
-                    uint8_t *p = tile + (size_t)(k * TPP + s) * slice_bytes<TX, SSD>();
-                    if constexpr (SSD) reinterpret_cast<uint32_t *>(p)[j] = a.padv;
-                    else reinterpret_cast<uint16_t *>(p)[j] = (uint16_t)a.padv;
-                }
-            }
-        }
-    }
-    __syncthreads();
-
-    // ---- per-lane column sums ----
-    const int d = tid;
-    const int a_d = (SIDE == SIDE_RIGHT) ? d : (Dp - 1 - d);
-    const int wbase = a_d >> 2;
-    const int sh = a_d & 3;
-    const bool lane_real = d < a.D;
-    uint8_t *tcol;
-    {
-        const int s = d / TX, j = d - s * TX;
-        tcol = tile + (size_t)s * slice_bytes<TX, SSD>() + j * (int)sizeof(cost_t<SSD>);
-    }
-    const int kstride = TPP * slice_bytes<TX, SSD>();
-
-    auto load_src = [&](int row, uint32_t(&al)[NWA]) {
-        const uint32_t *w = reinterpret_cast<const uint32_t *>(srcS + row * SWP) + wbase;
-        uint32_t raw[NWA + 1];
-#pragma unroll
-        for (int q = 0; q <= NWA; ++q) raw[q] = w[q];
-#pragma unroll
-        for (int q = 0; q < NWA; ++q) al[q] = __builtin_amdgcn_alignbyte(raw[q + 1], raw[q], sh);
-    };
-    auto load_ref = [&](int row, uint32_t(&rr)[NWA]) {
-        const uint32_t *w = reinterpret_cast<const uint32_t *>(refS + row * LWP);
-#pragma unroll
-        for (int q = 0; q < NWA; ++q) rr[q] = __builtin_amdgcn_readfirstlane(w[q]);
-    };
-    auto byte_of = [](const uint32_t(&v)[NWA], int c) -> uint32_t { return (v[c >> 2] >> ((c & 3) * 8)) & 0xFFu; };
-
-    uint32_t cs[NC];
-#pragma unroll
-    for (int c = 0; c < NC; ++c) cs[c] = 0;
-#pragma unroll
-    for (int i = 0; i <= 2 * R; ++i) {
-        uint32_t rr[NWA], al[NWA];
-        load_ref(i, rr);
-        load_src(i, al);
-#pragma unroll
-        for (int c = 0; c < NC; ++c) cs[c] = phi_acc<SSD>(byte_of(rr, c), byte_of(al, c), cs[c]);
-    }
-
-    for (int yy = 0; yy < rows; ++yy) {
-        if (yy > 0) {
-            uint32_t rn[NWA], an[NWA], ro[NWA], ao[NWA];
-            load_ref(yy + 2 * R, rn);
-            load_src(yy + 2 * R, an);
-            load_ref(yy - 1, ro);
-            load_src(yy - 1, ao);
-#pragma unroll
-            for (int c = 0; c < NC; ++c) {
-                const uint32_t add = phi_acc<SSD>(byte_of(rn, c), byte_of(an, c), cs[c]);
-                cs[c] = add - phi_acc<SSD>(byte_of(ro, c), byte_of(ao, c), 0u);
-            }
-        }
-        // running horizontal box sum -> tile
-        uint32_t acc = 0;
-#pragma unroll
-        for (int c = 0; c <= 2 * R; ++c) acc += cs[c];
-        if (lane_real) {
-#pragma unroll
-            for (int k = 0; k < TX; ++k) {
-                if (k > 0) acc = acc + cs[k + 2 * R] - cs[k - 1];
-                if constexpr (SSD) *reinterpret_cast<uint32_t *>(tcol + k * kstride) = acc;
-                else *reinterpret_cast<uint16_t *>(tcol + k * kstride) = (uint16_t)acc;
-            }
-        }
-        __syncthreads();
-
-        const int y = y0 + yy;
-        if constexpr (SIDE == SIDE_VOLUME) {
-            constexpr int CPC = 16 / (int)sizeof(cost_t<SSD>);  // costs per 16-B chunk
-            const int cpp = Dp / CPC;                          // chunks per pixel
-            const int nch = TX * cpp;
-            for (int q = tid; q < nch; q += nthr) {
-                const int k = q / cpp;
-                const int d0 = (q - k * cpp) * CPC;
-                const int x = x0 + k;
-                if (x < W) {
-                    const int s = d0 / TX, j0 = d0 - s * TX;
-                    const uint4 v = *reinterpret_cast<const uint4 *>(
-                        tile + (size_t)(k * TPP + s) * slice_bytes<TX, SSD>() + j0 * (int)sizeof(cost_t<SSD>));
-                    uint8_t *dst = reinterpret_cast<uint8_t *>(a.vol) +
-                                   (((size_t)y * W + x) * Dp + d0) * sizeof(cost_t<SSD>);
-                    *reinterpret_cast<uint4 *>(dst) = v;
-                }
-            }
-        } else {
-            const int k = tid / TPP, s = tid - k * TPP;
-            const int x = x0 + k;
-            if constexpr (SIDE == SIDE_RIGHT) {
-                uint32_t c[TX];
-                read_slice<TX, SSD>(tile, k, s, TPP, c);
-                const int lo = max(0, -m - x), hi = min(a.D - 1, W - 1 - m - x);
-                uint32_t best = 0xFFFFFFFFu;
-#pragma unroll
-                for (int j = 0; j < TX; ++j) {
-                    const int dj = s * TX + j;
-                    const uint32_t key = (c[j] << a.DB) | (uint32_t)dj;
-                    best = (dj >= lo && dj <= hi) ? umin(best, key) : best;
-                }
-                best = group_min(best, TPP);
-                if (s == 0 && x < W) {
-                    const int16_t v = (hi < lo) ? (int16_t)-1 : (int16_t)(best & ((1u << a.DB) - 1u));
-                    a.out_dR[(long)y * W + x] = v;
-                }
-            } else {
-                const bool xvalid = x < W && x >= m + a.D - 1 && x <= W - 1 + m;
-                PixelResult r = left_epilogue<TX, SSD>(tile, k, s, TPP, a.D, a.DB, m, a.uniq, a.subpix, xvalid);
-                bool valid = r.valid;
-                if (a.lr >= 0 && valid) {
-                    const int xr = x - m - r.b;
-                    const int dr = a.dRmap[(long)y * W + xr];
-                    const int df = dr - r.b;
-                    if (df > a.lr || df < -a.lr) valid = false;
-                }
-                if (s == 0 && x < W) store_left(r, valid, m, a.float_mode, (long)y * W + x, a.out_fixed, a.out_float);
-            }
-        }
-        __syncthreads();
-    }
-}
-
-// ---------------------------------------------------------------------------------------
 // vol_wta: K2 of the volume path, one block per image row
 // ---------------------------------------------------------------------------------------
 template <int TX, bool SSD>
@@ -442,14 +251,30 @@ __global__ __launch_bounds__(kVolThreads) void vol_wta(VolArgs a) {
 // ---------------------------------------------------------------------------------------
 // Host-side dispatch
 // ---------------------------------------------------------------------------------------
-#ifndef DSX_RADIUS
-size_t pass_smem_bytes(int radius, int TX, bool ssd, int Dp, int TPP, int TY) {
-    const int NC = TX + 2 * radius;
-    const int slice = TX * (ssd ? 4 : 2) + 16;
-    const size_t tile = (size_t)TX * TPP * slice;
-    const size_t lwp = (size_t)round16(NC + 8);
-    const size_t swp = (size_t)src_row_bytes(NC, Dp);
-    return tile + (size_t)(TY + 2 * radius) * (lwp + swp);
+// ---------------------------------------------------------------------------------------
+// expand_u16: reference rows as u16 with replicate padding (bm2's scalar-load operand)
+// ---------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void expand_u16_kernel(const uint8_t *__restrict__ img, int64_t stride, int H, int W,
+                                                          int radius, uint16_t *__restrict__ out, int pitch16) {
+    const int y = blockIdx.y;
+    const int c0 = (blockIdx.x * 256 + threadIdx.x) * 8;
+    if (c0 >= pitch16) return;
+    const uint8_t *row = img + (int64_t)y * stride;
+    uint32_t w[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const int xa = clampi(c0 + 2 * q - radius, 0, W - 1);
+        const int xb = clampi(c0 + 2 * q + 1 - radius, 0, W - 1);
+        w[q] = (uint32_t)row[xa] | ((uint32_t)row[xb] << 16);
+    }
+    *reinterpret_cast<uint4 *>(out + (int64_t)y * pitch16 + c0) = make_uint4(w[0], w[1], w[2], w[3]);
+}
+
+hipError_t launch_expand_u16(const uint8_t *img, int64_t stride, int H, int W, int radius, uint16_t *out, int pitch16,
+                             hipStream_t st) {
+    dim3 grid((pitch16 / 8 + 255) / 256, H);
+    hipLaunchKernelGGL(expand_u16_kernel, grid, dim3(256), 0, st, img, stride, H, W, radius, out, pitch16);
+    return hipGetLastError();
 }
 
 size_t volume_smem_bytes(int TX, bool ssd, int Dp, int TPP, int W) {
@@ -457,67 +282,6 @@ size_t volume_smem_bytes(int TX, bool ssd, int Dp, int TPP, int W) {
     const size_t tile = (size_t)(kVolThreads / TPP) * TPP * slice;
     (void)Dp;
     return tile + (size_t)W * 4 + (size_t)round16(W * 4) + (size_t)W * 4;
-}
-
-#endif  // !DSX_RADIUS
-
-template <int R, int TX, bool SSD, int SIDE>
-static hipError_t launch_one(const PassArgs &a, hipStream_t st) {
-    const size_t smem = pass_smem_bytes(R, TX, SSD, a.Dp, a.TPP, a.TY);
-    static bool attr_done[64] = {};  // per instantiation and device
-    int dev = 0;
-    (void)hipGetDevice(&dev);
-    if (dev < 0 || dev >= 64 || !attr_done[dev]) {
-        hipError_t e = hipFuncSetAttribute((const void *)bm_pass<R, TX, SSD, SIDE>,
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-        if (e != hipSuccess) return e;
-        if (dev >= 0 && dev < 64) attr_done[dev] = true;
-    }
-    dim3 grid((a.W + TX - 1) / TX, (a.H + a.TY - 1) / a.TY);
-    hipLaunchKernelGGL((bm_pass<R, TX, SSD, SIDE>), grid, dim3(a.Dp), smem, st, a);
-    return hipGetLastError();
-}
-
-template <int R, int TX, bool SSD>
-static hipError_t launch_side(int side, const PassArgs &a, hipStream_t st) {
-    switch (side) {
-        case SIDE_LEFT: return launch_one<R, TX, SSD, SIDE_LEFT>(a, st);
-        case SIDE_RIGHT: return launch_one<R, TX, SSD, SIDE_RIGHT>(a, st);
-        default: return launch_one<R, TX, SSD, SIDE_VOLUME>(a, st);
-    }
-}
-
-template <int R>
-static hipError_t launch_r(int side, int TX, bool ssd, const PassArgs &a, hipStream_t st) {
-    if (TX == 32) return ssd ? launch_side<R, 32, true>(side, a, st) : launch_side<R, 32, false>(side, a, st);
-    return ssd ? launch_side<R, 48, true>(side, a, st) : launch_side<R, 48, false>(side, a, st);
-}
-
-// The 8 radii are compiled as separate translation units (-DDSX_RADIUS=r) so the build
-// parallelises; the dispatch TU (no DSX_RADIUS) holds launch_pass, vol_wta and the helpers.
-#define DSX_DECL_RADIUS(r) hipError_t launch_pass_radius_##r(int, int, bool, const PassArgs &, hipStream_t);
-DSX_DECL_RADIUS(0) DSX_DECL_RADIUS(1) DSX_DECL_RADIUS(2) DSX_DECL_RADIUS(3)
-DSX_DECL_RADIUS(4) DSX_DECL_RADIUS(5) DSX_DECL_RADIUS(6) DSX_DECL_RADIUS(7)
-
-#ifdef DSX_RADIUS
-#define DSX_CAT2(a, b) a##b
-#define DSX_CAT(a, b) DSX_CAT2(a, b)
-hipError_t DSX_CAT(launch_pass_radius_, DSX_RADIUS)(int side, int TX, bool ssd, const PassArgs &a, hipStream_t st) {
-    return launch_r<DSX_RADIUS>(side, TX, ssd, a, st);
-}
-#else
-hipError_t launch_pass(int side, int radius, int TX, bool ssd, const PassArgs &a, hipStream_t st) {
-    switch (radius) {
-        case 0: return launch_pass_radius_0(side, TX, ssd, a, st);
-        case 1: return launch_pass_radius_1(side, TX, ssd, a, st);
-        case 2: return launch_pass_radius_2(side, TX, ssd, a, st);
-        case 3: return launch_pass_radius_3(side, TX, ssd, a, st);
-        case 4: return launch_pass_radius_4(side, TX, ssd, a, st);
-        case 5: return launch_pass_radius_5(side, TX, ssd, a, st);
-        case 6: return launch_pass_radius_6(side, TX, ssd, a, st);
-        case 7: return launch_pass_radius_7(side, TX, ssd, a, st);
-        default: return hipErrorInvalidValue;
-    }
 }
 
 template <int TX, bool SSD>
@@ -540,6 +304,5 @@ hipError_t launch_volume_wta(int TX, bool ssd, const VolArgs &a, hipStream_t st)
     if (TX == 32) return ssd ? launch_vol_one<32, true>(a, st) : launch_vol_one<32, false>(a, st);
     return ssd ? launch_vol_one<48, true>(a, st) : launch_vol_one<48, false>(a, st);
 }
-#endif  // DSX_RADIUS
 
 }  // namespace dsx

@@ -62,7 +62,9 @@ typedef struct dsx_params {
     int32_t float_mode;       /* DSX_FLOAT_FIXED | DSX_FLOAT_PARABOLA                          */
     int32_t path;             /* DSX_PATH_FUSED | DSX_PATH_VOLUME                              */
     int32_t timing;           /* 1 = record per-kernel HIP-event timings (dsx_kernel_times)   */
-    int32_t reserved[6];
+    int32_t grid_blocks;      /* 0 = one persistent block per resident slot; >0 forces the   */
+                              /* persistent grid size (tests of the work partition)         */
+    int32_t reserved[5];
 } dsx_params;
 
 typedef struct dsx_handle dsx_handle;
