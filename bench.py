@@ -29,7 +29,6 @@ sys.path.insert(0, ROOT)
 
 METRIC = "disparity Mpix/s at 1080p d_max=128; 1/2/4/8-GPU scaling + %HBM roofline"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level parameters)
-CALIB_LEN = 45  # 9 + 9 + 5 + 5 + 9 + 3 + 5 float64 values
 
 # BASELINE.json configs. c1 is the reference's CPU-runnable case; c4 is the
 # video stream case (its per-GPU frame is timed the same way); c2 is the headline.
@@ -55,36 +54,35 @@ def algorithmic_bytes(cfg) -> dict:
     return {"frame": px * (2 + 2 * D * c + 4), "k1": px * (2 + D * c), "k2": px * (D * c + 4), "compulsory": px * 6}
 
 
-def dist_env():
-    ws = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", str(rank)))
-    return ws, rank, local
-
-
-def calibration_block(torch, dev):
-    """The calibration that StereoDepthEstimatorVideo would carry (assets/calib.txt values):
-    K_L, K_R (3x3), dist_L, dist_R (5), R (3x3), T (3), W, H, f, baseline, doffs."""
+def calibration_params():
+    """The calibration StereoDepthEstimatorVideo would carry (assets/calib.txt-style values):
+    packed by sharding.pack_calibration into the 45-float64 block rank 0 broadcasts."""
     f, B, doffs = 3997.684, 0.193001, 131.111
-    K = [f, 0, 1176.728, 0, f, 1011.728, 0, 0, 1]
-    K2 = [f, 0, 1307.839, 0, f, 1011.728, 0, 0, 1]
-    vals = K + K2 + [0.0] * 10 + [1, 0, 0, 0, 1, 0, 0, 0, 1] + [-B, 0, 0] + [2964, 1988, f, B, doffs]
-    return torch.tensor(vals, dtype=torch.float64, device=dev)
+    return {"cam_matrix_L": [[f, 0, 1176.728], [0, f, 1011.728], [0, 0, 1]],
+            "cam_matrix_R": [[f, 0, 1307.839], [0, f, 1011.728], [0, 0, 1]],
+            "dist_coeff_L": [0.0] * 5, "dist_coeff_R": [0.0] * 5, "rotation": np.eye(3),
+            "translation": [-B, 0.0, 0.0], "image_width": 2964, "image_height": 1988,
+            "focal_length": f, "baseline": B, "doffs": doffs}
 
 
-def time_cpu_baseline(cfg, L, R, threads: int, frames: int):
-    """C restatement (oracle/bm_ref.c) built -march=native on this host; returns Mpix/s."""
+def time_cpu_baseline(cfg, L, R, threads: int, min_seconds: float, max_frames: int = 1000):
+    """C restatement (oracle/bm_ref.c) built -march=native on this host, run on whole frames of
+    the bench workload until ``min_seconds`` have elapsed; returns (Mpix/s, seconds, frames)."""
     from oracle.cref import CRef, build
     so = build(out_dir=os.path.join(tempfile.gettempdir(), "dsx_oracle_native"), march="native")
     ref = CRef(so)
     kw = dict(min_disp=0, num_disp=cfg["num_disp"], block_size=cfg["block_size"], cost=cfg["cost"],
               uniqueness_ratio=cfg["uniqueness_ratio"], disp12_max_diff=cfg["disp12_max_diff"], subpixel=True)
     ref(L[:64], R[:64], nthreads=threads, **kw)  # warm
+    n = 0
     t0 = time.perf_counter()
-    for _ in range(frames):
-        out = ref(L, R, nthreads=threads, **kw)
+    while n < max_frames:
+        ref(L, R, nthreads=threads, **kw)
+        n += 1
+        if time.perf_counter() - t0 >= min_seconds:
+            break
     dt = time.perf_counter() - t0
-    return L.size * frames / dt / 1e6, dt, out
+    return L.size * n / dt / 1e6, dt, n
 
 
 def main():
@@ -98,18 +96,19 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-volume-roofline", action="store_true")
     ap.add_argument("--check", action="store_true", help="verify one frame against the C oracle")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline sample length")
     args = ap.parse_args()
 
     import torch
     import torch.distributed as dist
+    from depthestimation_amd import sharding
     from depthestimation_amd.matcher import HipBlockMatcher
     from depthestimation_amd.synthetic import stereo_pair
 
-    ws, rank, local = dist_env()
-    if ws > 1:
-        dist.init_process_group(backend="nccl")
     if not torch.cuda.is_available():
         raise RuntimeError("bench.py needs a HIP device")
+    env = sharding.init_distributed("nccl")
+    ws, rank, local = env.world_size, env.rank, env.local_rank
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
 
@@ -117,9 +116,8 @@ def main():
     H, W = cfg["H"], cfg["W"]
 
     # one-time RCCL broadcast of the calibration block from rank 0 (no per-frame collectives)
-    calib = calibration_block(torch, dev) if rank == 0 else torch.zeros(CALIB_LEN, dtype=torch.float64, device=dev)
-    if ws > 1:
-        dist.broadcast(calib, src=0)
+    calib = sharding.broadcast_calibration(calibration_params() if rank == 0 else None, device=dev)
+    assert calib["image_width"] == 2964, "calibration broadcast failed"
 
     # frame-sharded synthetic stream: global frame g = rank + ws * i
     frames = []
@@ -239,14 +237,12 @@ def main():
         if not args.no_cpu_baseline and ws == 1:
             L, R = host_first
             threads = min(16, os.cpu_count() or 1)
-            v_all, dt_all, _ = time_cpu_baseline(cfg, L, R, threads, frames=6)
-            v_one, dt_one, _ = time_cpu_baseline(cfg, L[: H // 4], R[: H // 4], 1, frames=2)
+            v_cpu, dt_cpu, n_cpu = time_cpu_baseline(cfg, L, R, threads, args.cpu_seconds)
             result["cpu_baseline"] = {
-                "value": round(v_all, 3), "unit": "Mpix/s", "cores": threads, "kind": "port",
-                "sample": f"6 frames of the same {W}x{H} workload (first synthetic frame), {threads} OpenMP threads, "
-                          f"{dt_all:.1f} s; oracle/bm_ref.c -O3 -march=native",
-                "value_1core": round(v_one, 3),
-                "sample_1core": f"2 x {W}x{H // 4} strips, 1 thread, {dt_one:.1f} s",
+                "value": round(v_cpu, 3), "unit": "Mpix/s", "cores": threads, "kind": "port",
+                "sample": f"{n_cpu} whole {W}x{H} frames of the bench workload (first synthetic frame) in "
+                          f"{dt_cpu:.1f} s on {threads} OpenMP threads; oracle/bm_ref.c -O3 -march=native "
+                          f"(C restatement of the same contract; OpenCV absent)",
             }
         print(json.dumps(result), flush=True)
 

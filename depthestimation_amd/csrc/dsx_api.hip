@@ -95,8 +95,6 @@ struct dsx_handle {
     int16_t *dFixed = nullptr;
     float *dFloat = nullptr;
     int16_t *dRmap = nullptr;
-    uint16_t *dL16 = nullptr, *dR16 = nullptr;  // u16-expanded reference rows (bm2 scalar operand)
-    int pitch16 = 0, cRadius = -1;
     void *vol = nullptr;
     size_t vol_bytes = 0;
     // timing
@@ -115,12 +113,7 @@ void free_buffers(dsx_handle *h) {
     (void)hipFree(h->dFixed);
     (void)hipFree(h->dFloat);
     (void)hipFree(h->dRmap);
-    (void)hipFree(h->dL16);
-    (void)hipFree(h->dR16);
     (void)hipFree(h->vol);
-    h->dL16 = h->dR16 = nullptr;
-    h->pitch16 = 0;
-    h->cRadius = -1;
     h->dL = h->dR = nullptr;
     h->dFixed = nullptr;
     h->dFloat = nullptr;
@@ -132,11 +125,8 @@ void free_buffers(dsx_handle *h) {
 
 int ensure_buffers(dsx_handle *h, int H, int W, bool host_staging) {
     const int cbytes = h->p.cost == DSX_COST_SSD ? 4 : 2;
-    const int radius = h->p.block_size / 2;
-    if (h->cH != H || h->cW != W || h->cDp != h->g.Dp || h->cCostBytes != cbytes || h->cRadius != radius) free_buffers(h);
+    if (h->cH != H || h->cW != W || h->cDp != h->g.Dp || h->cCostBytes != cbytes) free_buffers(h);
     const size_t n = (size_t)H * W;
-    h->pitch16 = dsx::expand_pitch16(W, radius);
-    h->cRadius = radius;
 
     if (host_staging && !h->dL) {
         DSX_HIP(hipMalloc(&h->dL, n));
@@ -235,14 +225,6 @@ dsx::Bm2Args base_args(dsx_handle *h, int H, int W, int64_t stride) {
             if (rc_) return rc_;                                         \
         }                                                                \
     } while (0)
-
-int expand(dsx_handle *h, const char *name, const void *img, uint16_t *out, int H, int W, int64_t stride,
-           hipStream_t st) {
-    DSX_LAUNCH(h, name, st,
-               dsx::launch_expand_u16(static_cast<const uint8_t *>(img), stride, H, W, h->p.block_size / 2, out,
-                                      h->pitch16, st));
-    return DSX_OK;
-}
 
 int run_right_pass(dsx_handle *h, const void *dL, const void *dR, int H, int W, int64_t stride, int16_t *out,
                    hipStream_t st) {
@@ -499,8 +481,6 @@ int dsx_workspace_bytes(dsx_handle *h, int64_t *bytes) {
     int64_t b = 0;
     if (h->dL) b += n * (1 + 1 + 2 + 4);
     if (h->dRmap) b += n * 2;
-    if (h->dL16) b += (int64_t)h->cH * h->pitch16 * 2;
-    if (h->dR16) b += (int64_t)h->cH * h->pitch16 * 2;
     b += (int64_t)h->vol_bytes;
     *bytes = b;
     return DSX_OK;

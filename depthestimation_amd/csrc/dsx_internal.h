@@ -21,8 +21,6 @@ struct Geometry {
 struct Bm2Args {
     const uint8_t *ref;  // reference image (L for left/volume passes, R for the right pass)
     const uint8_t *src;  // searched image
-    const uint16_t *ref16;  // reference image expanded to u16 with R replicate-padded columns
-    int pitch16;         // row pitch of ref16 in u16 elements (see expand_pitch16)
     int64_t stride;      // row stride of both images in bytes
     int H, W;
     int m;               // min_disp
@@ -54,15 +52,6 @@ constexpr int kStripWidth = 32;  // TX of bm2
 hipError_t launch_bm2(int radius, bool ssd, int nw, const Bm2Args &a, hipStream_t st);
 hipError_t launch_volume_wta(int TX, bool ssd, const VolArgs &a, hipStream_t st);
 
-// u16 expansion of a reference image with `radius` replicate-padded columns on the left:
-// out[y * pitch16 + c] = img[y][clamp(c - radius, 0, W - 1)]  (consumed by bm2 through scalar
-// loads, two columns per SGPR, selected with VOP3P op_sel).
-inline int expand_pitch16(int W, int radius) {
-    const int w32 = (W + 31) / 32 * 32;
-    return (w32 + 2 * radius + 16 + 7) / 8 * 8;
-}
-hipError_t launch_expand_u16(const uint8_t *img, int64_t stride, int H, int W, int radius, uint16_t *out,
-                             int pitch16, hipStream_t st);
 size_t volume_smem_bytes(int TX, bool ssd, int Dp, int TPP, int W);
 
 }  // namespace dsx

@@ -251,32 +251,6 @@ __global__ __launch_bounds__(kVolThreads) void vol_wta(VolArgs a) {
 // ---------------------------------------------------------------------------------------
 // Host-side dispatch
 // ---------------------------------------------------------------------------------------
-// ---------------------------------------------------------------------------------------
-// expand_u16: reference rows as u16 with replicate padding (bm2's scalar-load operand)
-// ---------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void expand_u16_kernel(const uint8_t *__restrict__ img, int64_t stride, int H, int W,
-                                                          int radius, uint16_t *__restrict__ out, int pitch16) {
-    const int y = blockIdx.y;
-    const int c0 = (blockIdx.x * 256 + threadIdx.x) * 8;
-    if (c0 >= pitch16) return;
-    const uint8_t *row = img + (int64_t)y * stride;
-    uint32_t w[4];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        const int xa = clampi(c0 + 2 * q - radius, 0, W - 1);
-        const int xb = clampi(c0 + 2 * q + 1 - radius, 0, W - 1);
-        w[q] = (uint32_t)row[xa] | ((uint32_t)row[xb] << 16);
-    }
-    *reinterpret_cast<uint4 *>(out + (int64_t)y * pitch16 + c0) = make_uint4(w[0], w[1], w[2], w[3]);
-}
-
-hipError_t launch_expand_u16(const uint8_t *img, int64_t stride, int H, int W, int radius, uint16_t *out, int pitch16,
-                             hipStream_t st) {
-    dim3 grid((pitch16 / 8 + 255) / 256, H);
-    hipLaunchKernelGGL(expand_u16_kernel, grid, dim3(256), 0, st, img, stride, H, W, radius, out, pitch16);
-    return hipGetLastError();
-}
-
 size_t volume_smem_bytes(int TX, bool ssd, int Dp, int TPP, int W) {
     const int slice = TX * (ssd ? 4 : 2) + 16;
     const size_t tile = (size_t)(kVolThreads / TPP) * TPP * slice;

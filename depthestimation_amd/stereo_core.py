@@ -1,0 +1,197 @@
+"""StereoCore - host-side mirror of depthlib/stereo_core.py with the MI355X block matcher.
+
+Same class, method names, parameter dict, validation and error behaviour as the reference
+(depthlib/stereo_core.py:7-293). The one seam that changes is the matcher object:
+``_build_sgbm`` (stereo_core.py:44-75) builds a :class:`HipBlockMatcher` (libdsx.so, C-ABI in
+include/dsx.h) instead of ``cv2.StereoSGBM_create``, and ``compute_disparity``
+(stereo_core.py:212-232) calls its ``compute`` with the same cv2 contract (int16 x16 -> /16).
+
+Keys added to ``sgbm_params`` (accepted by ``configure_sgbm`` like the reference's own keys):
+  'cost'     : 'sad' | 'ssd'          (block cost; north_star SAD/SSD)
+  'subpixel' : bool                   (1/16-px parabola refinement, on by default)
+  'device'   : int                    (HIP device of the matcher)
+Keys of the reference that have no block-matching meaning are kept, validated and reported
+but do not change the result: 'prefilter_cap', 'speckle_window_size', 'speckle_range',
+'sgbm_mode' (and the derived P1/P2, stereo_core.py:51-52) belong to OpenCV's semi-global
+aggregation, which the north-star path replaces with plain block matching (SURVEY.md 8a A5').
+
+There is no CPU fallback: without libdsx.so or a HIP device ``compute_disparity`` raises.
+"""
+from __future__ import annotations
+
+from typing import Dict, Optional, Tuple
+
+import numpy as np
+
+from .matcher import HipBlockMatcher
+from .postprocess import median_blur3, postprocess_disparity
+from .rectify import RectificationCache, rectify_images, to_grayscale_bgr
+
+_SGBM_MODES = ("sgbm", "hh", "sgbm_3way", "hh4")
+
+
+class StereoCore:
+    """Handles common stereo operations (stereo_core.py:7)."""
+
+    def __init__(self, downscale_factor=1.0, fast_mode=False) -> None:
+        self.downscale_factor = downscale_factor
+        self.fast_mode = fast_mode
+        self.sgbm = None
+        self._rect_cache = RectificationCache()
+        # stereo_core.py:16-39 defaults, then the build keys
+        self.sgbm_params = {
+            'min_disp': 0,
+            'num_disp': 128,
+            'block_size': 5,
+            'disp12_max_diff': 1,
+            'prefilter_cap': 31,
+            'uniqueness_ratio': 10,
+            'speckle_window_size': 50,
+            'speckle_range': 2,
+            'sgbm_mode': 'sgbm_3way',
+            'focal_length': None,
+            'baseline': None,
+            'doffs': 0.0,
+            'max_depth': None,
+            'cam_matrix_L': None,
+            'cam_matrix_R': None,
+            'image_width': None,
+            'image_height': None,
+            'dist_coeff_L': None,
+            'dist_coeff_R': None,
+            'rotation': None,
+            'translation': None,
+            'hole_filling': False,
+            'cost': 'sad',
+            'subpixel': True,
+            'device': 0,
+        }
+        self._build_sgbm()
+        self.disparity_map = None
+        self.depth_map = None
+
+    # -- matcher -------------------------------------------------------------------------
+    def _build_sgbm(self):
+        """stereo_core.py:44-75 -> HipBlockMatcher. P1/P2 and the mode are recorded for
+        reporting (SGM aggregation is not part of the block-matching contract)."""
+        p = self.sgbm_params
+        self.P1 = 8 * p['block_size'] ** 2
+        self.P2 = 32 * p['block_size'] ** 2
+        self.mode = p.get('sgbm_mode', 'sgbm_3way') if p.get('sgbm_mode') in _SGBM_MODES else 'sgbm_3way'
+        old = self.sgbm
+        self.sgbm = HipBlockMatcher(
+            min_disp=p['min_disp'],
+            num_disp=max(int(p['num_disp']), 1),
+            block_size=p['block_size'],
+            cost=p['cost'],
+            uniqueness_ratio=p['uniqueness_ratio'],
+            disp12_max_diff=p['disp12_max_diff'],
+            subpixel=p['subpixel'],
+            device=p['device'],
+        )
+        if old is not None:
+            old.close()
+
+    def configure_sgbm(self, **kwargs):
+        """stereo_core.py:77-123: unknown keys -> ValueError; num_disp / focal_length / doffs
+        scaled by downscale_factor (int() truncation for num_disp); matcher rebuilt."""
+        valid_params = self.sgbm_params.keys()
+        for key in kwargs:
+            if key not in valid_params:
+                raise ValueError(f"Invalid parameter '{key}'. Valid parameters: {list(valid_params)}")
+        if 'num_disp' in kwargs:
+            kwargs['num_disp'] = int(kwargs['num_disp'] * self.downscale_factor)
+        if 'focal_length' in kwargs:
+            kwargs['focal_length'] = kwargs['focal_length'] * self.downscale_factor
+        if 'doffs' in kwargs:
+            kwargs['doffs'] = kwargs['doffs'] * self.downscale_factor
+        self.sgbm_params.update(kwargs)
+        self._build_sgbm()
+
+    def get_sgbm_params(self) -> Dict[str, int]:
+        return self.sgbm_params.copy()
+
+    # -- pipeline ------------------------------------------------------------------------
+    def _prepare_rectified(self, left_img: np.ndarray, right_img: np.ndarray) -> Tuple[np.ndarray, np.ndarray]:
+        """stereo_core.py:125-160: rectify when calibrated, else BGR->gray."""
+        p = self.sgbm_params
+        if all(p.get(k) is not None for k in ('cam_matrix_L', 'cam_matrix_R', 'baseline', 'image_width',
+                                               'image_height')):
+            return rectify_images(left_img, right_img, p['cam_matrix_L'], p['cam_matrix_R'], p['baseline'],
+                                  p['image_width'], p['image_height'], dist_coeff_L=p.get('dist_coeff_L'),
+                                  dist_coeff_R=p.get('dist_coeff_R'), rotation=p.get('rotation'),
+                                  translation=p.get('translation'), alpha=1.0, cache=self._rect_cache)
+        if left_img.ndim == 3:
+            left_img = to_grayscale_bgr(left_img)
+        if right_img.ndim == 3:
+            right_img = to_grayscale_bgr(right_img)
+        return left_img, right_img
+
+    def _process_pair(self, left_img: np.ndarray, right_img: np.ndarray) -> Tuple[np.ndarray, Optional[np.ndarray]]:
+        """stereo_core.py:162-200: disparity -> crop [:, num_disp:] -> median (fast) or
+        postprocess -> depth when focal length and baseline are set."""
+        disparity_px = self.compute_disparity(left_img, right_img)
+        disparity_px = disparity_px[:, self.sgbm_params['num_disp']:]
+        if self.fast_mode:
+            disparity_px = median_blur3(disparity_px.astype(np.float32))
+        else:
+            disparity_px = postprocess_disparity(
+                disparity_px,
+                left_image=left_img,
+                max_speckle_size=int(100 * self.downscale_factor),
+                max_diff=1.0,
+                outlier_threshold=2.5,
+                fill_method='inpaint',
+                apply_outlier_removal=True,
+                apply_hole_filling=self.sgbm_params.get('hole_filling', False),
+            )
+        f_pixels = self.sgbm_params.get('focal_length', None)
+        baseline_m = self.sgbm_params.get('baseline', None)
+        doffs = self.sgbm_params.get('doffs', 0.0)
+        min_disparity = self.sgbm_params.get('min_disp', 5.0)
+        max_depth = self.sgbm_params.get('max_depth')
+        depth_m = None
+        if f_pixels is not None and baseline_m is not None:
+            depth_m = self.disparity_to_depth(disparity_px, f_pixels, baseline_m, doffs, eps=min_disparity,
+                                              max_depth=max_depth)
+        self.disparity_map = disparity_px
+        self.depth_map = depth_m
+        return disparity_px, depth_m
+
+    def compute_disparity(self, rectified_L: np.ndarray, rectified_R: np.ndarray) -> np.ndarray:
+        """stereo_core.py:212-232: float32 disparity in pixels (1/16-px steps), invalid
+        (min_disp - 1)."""
+        if self.sgbm is None:
+            self._build_sgbm()
+        disp_fixed = self.sgbm.compute(rectified_L, rectified_R)
+        return disp_fixed.astype(np.float32) / 16.0
+
+    def compute_disparity_device(self, left, right, out=None, stream=None):
+        """Device-resident variant: uint8 HIP tensors in, float32 HIP tensor out (the
+        kernel writes fixed/16 directly; nothing crosses PCIe)."""
+        import torch
+        if self.sgbm is None:
+            self._build_sgbm()
+        if out is None:
+            out = torch.empty(left.shape, dtype=torch.float32, device=left.device)
+        self.sgbm.compute_device(left, right, out_float=out, stream=stream)
+        return out
+
+    def disparity_to_depth(self, disp: np.ndarray, f_pixels: float, baseline_m: float, doffs: float = 0.0,
+                           eps: float = 1e-6, max_depth: Optional[float] = None) -> np.ndarray:
+        """stereo_core.py:234-272: Z = f*B / (d + doffs) where d + doffs > eps, else inf;
+        optional clamp to max_depth."""
+        adjusted_disp = disp + doffs
+        Z = np.full_like(disp, np.inf, dtype=np.float32)
+        valid_mask = adjusted_disp > eps
+        Z[valid_mask] = (f_pixels * baseline_m) / adjusted_disp[valid_mask]
+        if max_depth is not None:
+            Z[Z > max_depth] = max_depth
+        return Z
+
+    def estimate_depth(self, left_source, right_source) -> Tuple[np.ndarray, Optional[np.ndarray]]:
+        """stereo_core.py:274-293."""
+        if left_source is None or right_source is None:
+            raise ValueError("Left and right sources must be set before estimating depth.")
+        self.left_rectified, self.right_rectified = self._prepare_rectified(left_source, right_source)
+        return self._process_pair(self.left_rectified, self.right_rectified)

@@ -155,9 +155,11 @@ def stereo_bm(L, R, min_disp: int = 0, num_disp: int = 64, block_size: int = 5,
 
 
 def bm_bruteforce(L, R, min_disp, num_disp, block_size, cost="sad", uniqueness_ratio=0,
-                  disp12_max_diff=-1, subpixel=True):
+                  disp12_max_diff=-1, subpixel=True, with_parabola=False):
     """Pure-Python loop restatement straight from the A5' formula (tiny inputs only).
-    Independent of ``cost_volume`` (no cumulative sums) - used to pin the NumPy oracle."""
+    Independent of ``cost_volume`` (no cumulative sums) - used to pin the NumPy oracle and to
+    generate the committed golden fixtures (tests/golden/make_golden.py).
+    Returns the int16 map, or (int16 map, float32 parabola map) with ``with_parabola``."""
     L = np.asarray(L, np.int64)
     R = np.asarray(R, np.int64)
     H, W = L.shape
@@ -179,6 +181,7 @@ def bm_bruteforce(L, R, min_disp, num_disp, block_size, cost="sad", uniqueness_r
         return s
 
     out = np.zeros((H, W), np.int16)
+    par = np.full((H, W), np.float32(m - 1), np.float32)
     for y in range(H):
         for x in range(W):
             inv = (m - 1) * 16
@@ -200,10 +203,14 @@ def bm_bruteforce(L, R, min_disp, num_disp, block_size, cost="sad", uniqueness_r
                 if abs(dr - b) > disp12_max_diff:
                     ok = False
             f = b * 16
+            pv = np.float32(m + b)
             if subpixel and 0 < b < D - 1:
                 den = max(c[b - 1] + c[b + 1] - 2 * c[b], 1)
                 num = (c[b - 1] - c[b + 1]) * 16 + den
                 q = abs(num) // (2 * den)
                 f += q if num >= 0 else -q
+                pv = np.float32(pv + np.float32(c[b - 1] - c[b + 1]) / np.float32(2 * den))
             out[y, x] = m * 16 + f if ok else inv
-    return out
+            if ok:
+                par[y, x] = pv
+    return (out, par) if with_parabola else out

@@ -1,0 +1,112 @@
+"""CPU tests of the C-ABI boundary (include/dsx.h): the library loads, exports every declared
+symbol, validates parameters like the reference does (ValueError for bad params,
+stereo_core.py:106-109) and reports no devices cleanly - no compute call needs a GPU here."""
+from __future__ import annotations
+
+import ctypes
+import os
+import re
+import subprocess
+
+import pytest
+
+from depthestimation_amd import _dsx
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "dsx.h")
+
+
+def header_functions():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(dsx_[a-z_0-9]+)\s*\(", src)))
+
+
+def test_header_declares_the_bound_symbols():
+    assert header_functions() == sorted(_dsx.EXPORTS)
+
+
+def test_library_exports_every_header_symbol(dsx_lib_path):
+    lib = ctypes.CDLL(dsx_lib_path)
+    for name in header_functions():
+        assert hasattr(lib, name), name
+    out = subprocess.run(["nm", "-D", "--defined-only", dsx_lib_path], capture_output=True, text=True,
+                         check=True).stdout
+    exported = set(re.findall(r"\bT (dsx_\w+)", out))
+    assert set(header_functions()) <= exported
+
+
+def test_header_compiles_as_c(tmp_path):
+    c = tmp_path / "t.c"
+    c.write_text('#include "dsx.h"\nint main(void){dsx_params p; dsx_default_params(&p); return p.num_disp != 128;}\n')
+    subprocess.run(["gcc", "-std=c99", "-Wall", "-Werror", "-I", os.path.join(ROOT, "include"), "-c", str(c),
+                    "-o", str(tmp_path / "t.o")], check=True)
+
+
+def test_params_struct_layout():
+    assert ctypes.sizeof(_dsx.DsxParams) == 16 * 4
+
+
+def test_version_and_defaults():
+    lib = _dsx.lib()
+    assert lib.dsx_version() == 100
+    p = _dsx.default_params()
+    # StereoCore.sgbm_params defaults (stereo_core.py:16-39) + build keys
+    assert (p.min_disp, p.num_disp, p.block_size, p.uniqueness_ratio, p.disp12_max_diff) == (0, 128, 5, 10, 1)
+    assert (p.cost, p.subpixel, p.float_mode, p.path, p.timing, p.grid_blocks) == (0, 1, 0, 0, 0, 0)
+
+
+@pytest.mark.parametrize("kw", [
+    dict(block_size=4), dict(block_size=0), dict(block_size=17), dict(num_disp=0), dict(num_disp=1024),
+    dict(uniqueness_ratio=100), dict(uniqueness_ratio=-1), dict(min_disp=-3000), dict(min_disp=2000, num_disp=128),
+    dict(grid_blocks=-1),
+    dict(cost="ssd", num_disp=512, block_size=15),  # 225*255^2 << 9 overflows the 32-bit (cost, d) key
+])
+def test_bad_params_raise_value_error(kw):
+    with pytest.raises(ValueError):
+        _dsx.check_params(_dsx.make_params(**kw))
+    assert _dsx.last_error()
+
+
+@pytest.mark.parametrize("kw", [
+    dict(), dict(block_size=15, cost="ssd", num_disp=256), dict(block_size=1, num_disp=1), dict(min_disp=-16),
+    dict(num_disp=512, block_size=15), dict(num_disp=100), dict(cost="ssd", num_disp=256, block_size=15),
+])
+def test_good_params_accepted(kw):
+    _dsx.check_params(_dsx.make_params(**kw))
+
+
+def test_python_side_enum_validation():
+    with pytest.raises(ValueError):
+        _dsx.make_params(cost="census")
+    with pytest.raises(ValueError):
+        _dsx.make_params(float_mode="cubic")
+    with pytest.raises(ValueError):
+        _dsx.make_params(path="tiled")
+
+
+def test_null_arguments_are_errors_not_crashes():
+    lib = _dsx.lib()
+    assert lib.dsx_check_params(None) == _dsx.DSX_EINVAL
+    assert lib.dsx_create(0, None, None) == _dsx.DSX_EINVAL
+    assert lib.dsx_destroy(None) in (_dsx.DSX_OK, _dsx.DSX_EINVAL)
+    assert lib.dsx_compute_host(None, None, None, 4, 4, 4, None, None) == _dsx.DSX_EINVAL
+
+
+def test_device_count_without_gpu(gpu_available):
+    n = _dsx.device_count()
+    assert n >= 0
+    if not gpu_available:
+        assert n == 0
+
+
+def test_matcher_without_device_fails_loudly(gpu_available):
+    if gpu_available:
+        pytest.skip("a device is present")
+    import numpy as np
+
+    from depthestimation_amd.matcher import HipBlockMatcher
+
+    bm = HipBlockMatcher(num_disp=16)
+    with pytest.raises(RuntimeError, match="no HIP device"):
+        bm.compute(np.zeros((8, 32), np.uint8), np.zeros((8, 32), np.uint8))

@@ -3,6 +3,8 @@ inputs. Integer disparities (int16 x16) are bit-exact; the float parabola output
 against the oracle within 1e-3 (north_star tolerance) and is in fact bit-exact."""
 from __future__ import annotations
 
+import glob
+import os
 import zlib
 
 import numpy as np
@@ -135,3 +137,21 @@ def test_large_vs_c_oracle(torch_dev):
             fixed, _ = _run(L, R, path=path, num_disp=D, block_size=bs, cost=cost,
                             uniqueness_ratio=u, disp12_max_diff=lr)
             np.testing.assert_array_equal(fixed, ref["fixed"])
+
+
+GOLDEN = sorted(glob.glob(os.path.join(os.path.dirname(__file__), "golden", "*.npz")))
+
+
+@pytest.mark.parametrize("path", ["fused", "volume"])
+@pytest.mark.parametrize("golden", GOLDEN, ids=lambda p: p.rsplit("/", 1)[-1][:-4])
+def test_golden_fixtures(torch_dev, golden, path):
+    """The committed brute-force fixtures (tests/golden/make_golden.py) through the C-ABI."""
+    z = np.load(golden)
+    m, D, bs, cost, u, lr, sp = (int(v) for v in z["params"])
+    kw = dict(min_disp=m, num_disp=D, block_size=bs, cost=("sad", "ssd")[cost], uniqueness_ratio=u,
+              disp12_max_diff=lr, subpixel=bool(sp))
+    fixed, fl = _run(z["L"], z["R"], path=path, **kw)
+    np.testing.assert_array_equal(fixed, z["fixed"])
+    np.testing.assert_array_equal(fl, z["fixed"].astype(np.float32) / np.float32(16))
+    _, par = _run(z["L"], z["R"], path=path, float_mode="parabola", **kw)
+    assert np.max(np.abs(par - z["parabola"])) <= FLOAT_TOL
