@@ -65,6 +65,16 @@ def calibration_params():
             "focal_length": f, "baseline": B, "doffs": doffs}
 
 
+def load_traffic() -> dict:
+    """PMC-derived HBM bytes per launch (profiles/traffic.json, written by tools/make_profiles.py
+    from rocprofv3 FETCH_SIZE/WRITE_SIZE passes of this same command)."""
+    p = os.path.join(ROOT, "profiles", "traffic.json")
+    try:
+        return json.load(open(p))
+    except (OSError, ValueError):
+        return {}
+
+
 def time_cpu_baseline(cfg, L, R, threads: int, min_seconds: float, max_frames: int = 1000):
     """C restatement (oracle/bm_ref.c) built -march=native on this host, run on whole frames of
     the bench workload until ``min_seconds`` have elapsed; returns (Mpix/s, seconds, frames)."""
@@ -187,15 +197,11 @@ def main():
                       if args.path == "fused" else "SURVEY 8(d) D3 per-frame bytes over the K1+K2 pipeline"),
             "kernels_ms": {k: round(v[0], 5) for k, v in ktimes.items()},
         }
-        tr_path = os.path.join(ROOT, "profiles", "traffic.json")
-        if os.path.exists(tr_path):
-            try:
-                tr = json.load(open(tr_path)).get(f"{args.config}:{args.path}:{dom_name}")
-                if tr:
-                    roofline["traffic"] = tr["hbm_bytes_per_launch"]
-                    roofline["traffic_source"] = tr.get("source")
-            except Exception:
-                pass
+        traffic = load_traffic()
+        tr = traffic.get(f"{args.config}:{args.path}:{dom_name}")
+        if tr:
+            roofline["traffic"] = tr["hbm_bytes_per_launch"]
+            roofline["traffic_source"] = tr.get("source")
         result = {
             "metric": METRIC, "value": round(value, 1), "unit": "Mpix/s", "n_gpus": ws,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 5),
@@ -230,7 +236,9 @@ def main():
                     ms = kt[name][0]
                     a = ab[key] / (ms * 1e-3) / 1e9
                     rv[name] = {"kernel_ms": round(ms, 5), "algorithmic_bytes": ab[key], "achieved": round(a, 1),
-                                "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(a / HBM_PEAK_GBS, 4)}
+                                "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(a / HBM_PEAK_GBS, 4),
+                                "traffic": (traffic.get(f"{args.config}:volume:{name}") or {}).get(
+                                    "hbm_bytes_per_launch")}
             result["roofline_volume"] = rv
             vm.close()
 

@@ -11,11 +11,13 @@
 //     sweeping down contiguous rows of a strip with running column sums (2 absolute
 //     differences per column per row: the entering and the leaving row), so there is no
 //     tail generation and no per-tile re-initialisation except at segment starts.
-//   * Rows are staged through an LDS ring of 2R+2 rows.  The searched row is stored as
+//   * Each row step needs the entering row (y+R+1) and the leaving row (y-R); both are staged
+//     in double-buffered LDS slots.  The searched row is stored as
 //     S[j] = {src(pos(j)), src(pos(j+1))} u16 pairs in "disparity order" (j grows with d),
 //     so a lane reads the pair for its two disparities with one aligned ds_read_b64 per two
-//     columns; the reference row is wave-uniform and is consumed from SGPRs.  The next row
-//     is prefetched from HBM into VGPRs while the current row computes.
+//     columns; the reference row is wave-uniform: it is stored as u16 pairs and read with
+//     broadcast 16-B LDS loads (8 columns), then selected per column with VOP3P op_sel.  The
+//     next step's rows are prefetched from HBM into VGPRs while the current row computes.
 //   * Per row the TX x Dp costs go to an LDS tile; the epilogue re-reads it with TPP = 2*NW
 //     lanes per pixel (DSL = Dp/TPP disparities each), finds the minimum with packed block
 //     minima (8 disparities per 16-B read), the lowest winning d with a short scan of the

@@ -1,0 +1,66 @@
+"""Turn a tools/prof.sh output dir (gpurun_out/prof_<tag>) into committed summaries under profiles/:
+  profiles/<tag>_kernel_stats.csv   rocprofv3 --kernel-trace --stats summary (verbatim)
+  profiles/<tag>_pmc.txt            per-kernel average PMC values per dispatch
+  profiles/traffic.json             {"<config>:<path>:<kernel>": {"hbm_bytes_per_launch": ...}}
+HBM bytes follow MI355X_MICROARCH.md (HBM section): FETCH_SIZE/WRITE_SIZE are KiB from separate
+--pmc passes; on gfx950 FETCH_SIZE counts half the bytes of wide coalesced reads, so it is doubled
+(exact for K2's 16-B streaming reads; an upper bound for the fused pass's 4-B row loads).
+
+usage: python tools/make_profiles.py <prof dir> <tag> <config> <path>
+"""
+import csv
+import glob
+import json
+import os
+import shutil
+import sys
+from collections import defaultdict
+
+NAMES = {", 0>": "bm_pass_left", ", 1>": "bm_pass_right", ", 2>": "cost_volume", "vol_wta": "volume_wta"}
+
+
+def short(k):
+    for pat, n in NAMES.items():
+        if pat in k:
+            return n
+    return k
+
+
+def main(src, tag, config, path):
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    prof = os.path.join(root, "profiles")
+    os.makedirs(prof, exist_ok=True)
+    stats = glob.glob(os.path.join(src, "trace", "*kernel_stats.csv"))[0]
+    shutil.copy(stats, os.path.join(prof, f"{tag}_kernel_stats.csv"))
+    avg_ns = {r["Name"]: float(r["AverageNs"]) for r in csv.DictReader(open(stats))}
+    acc = defaultdict(lambda: defaultdict(list))
+    for f in sorted(glob.glob(os.path.join(src, "pmc*", "*counter_collection.csv"))):
+        for r in csv.DictReader(open(f)):
+            acc[r["Kernel_Name"]][r["Counter_Name"]].append(float(r["Counter_Value"]))
+    lines = [f"# rocprofv3 PMC, average per dispatch ({tag}; {config}, path={path})",
+             "# FETCH_SIZE / WRITE_SIZE in KiB; separate --pmc passes per counter group (tools/prof.sh)"]
+    tp = os.path.join(prof, "traffic.json")
+    traffic = json.load(open(tp)) if os.path.exists(tp) else {}
+    for k, cs in acc.items():
+        if "rocclr" in k:
+            continue
+        lines.append(f"{k}  [{short(k)}]  avg_ns={avg_ns.get(k)}")
+        for c, v in sorted(cs.items()):
+            lines.append(f"    {c:28s} {sum(v) / len(v):18.1f}")
+        m = {c: sum(v) / len(v) for c, v in cs.items()}
+        if "FETCH_SIZE" in m and "WRITE_SIZE" in m:
+            rd = 2 * m["FETCH_SIZE"] * 1024
+            wr = m["WRITE_SIZE"] * 1024
+            traffic[f"{config}:{path}:{short(k)}"] = {
+                "hbm_bytes_per_launch": round(rd + wr), "read_bytes": round(rd), "write_bytes": round(wr),
+                "avg_ns": avg_ns.get(k), "source": f"profiles/{tag}_pmc.txt (2*FETCH_SIZE + WRITE_SIZE, KiB->B)"}
+            lines.append(f"    => HBM bytes/launch (2*FETCH + WRITE) {rd + wr:,.0f}")
+        if "SQ_WAVE_CYCLES" in m and "SQ_BUSY_CYCLES" in m:
+            lines.append(f"    => VALU instr/wave {m.get('SQ_INSTS_VALU', 0) / max(m.get('SQ_WAVES', 1), 1):,.0f}; "
+                         f"wait_any/wave_cycles {m['SQ_WAIT_ANY'] / m['SQ_WAVE_CYCLES']:.2f}")
+    open(os.path.join(prof, f"{tag}_pmc.txt"), "w").write("\n".join(lines) + "\n")
+    json.dump(traffic, open(tp, "w"), indent=1, sort_keys=True)
+
+
+if __name__ == "__main__":
+    main(*sys.argv[1:5])
