@@ -28,6 +28,7 @@ PATH = {"fused": 0, "volume": 1}
 EXPORTS = (
     "dsx_version", "dsx_device_count", "dsx_default_params", "dsx_check_params", "dsx_create",
     "dsx_set_params", "dsx_compute_host", "dsx_compute_device", "dsx_right_map_device",
+    "dsx_postprocess_fast_device", "dsx_rectify_device",
     "dsx_kernel_times", "dsx_reset_times", "dsx_workspace_bytes", "dsx_destroy", "dsx_last_error",
 )
 
@@ -66,6 +67,10 @@ def _bind(lib):
         "dsx_compute_host": (ctypes.c_int, [vp, vp, vp, i32, i32, i64, vp, vp]),
         "dsx_compute_device": (ctypes.c_int, [vp, vp, vp, i32, i32, i64, vp, vp, vp]),
         "dsx_right_map_device": (ctypes.c_int, [vp, vp, vp, i32, i32, i64, vp, vp]),
+        "dsx_rectify_device": (ctypes.c_int, [vp, i32, i32, i64, i32, vp, vp, i32, i32, vp, vp]),
+        "dsx_postprocess_fast_device": (ctypes.c_int, [vp, i32, i32, i64, i32, vp, vp, ctypes.c_double,
+                                                        ctypes.c_double, ctypes.c_double, ctypes.c_double,
+                                                        ctypes.c_double, i32, vp]),
         "dsx_kernel_times": (ctypes.c_int, [vp, ctypes.c_char_p, ctypes.c_int, ctypes.POINTER(ctypes.c_float),
                                              ctypes.POINTER(ctypes.c_int), ctypes.c_int, ctypes.POINTER(ctypes.c_int)]),
         "dsx_reset_times": (ctypes.c_int, [vp]),

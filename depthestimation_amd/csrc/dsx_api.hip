@@ -135,6 +135,7 @@ int ensure_buffers(dsx_handle *h, int H, int W, bool host_staging) {
         DSX_HIP(hipMalloc(&h->dFloat, n * 4));
     }
     if (h->p.disp12_max_diff >= 0 && h->p.path == DSX_PATH_FUSED && !h->dRmap) DSX_HIP(hipMalloc(&h->dRmap, n * 2));
+
     if (h->p.path == DSX_PATH_VOLUME && !h->vol) {
         h->vol_bytes = n * h->g.Dp * cbytes;
         DSX_HIP(hipMalloc(&h->vol, h->vol_bytes));
@@ -403,6 +404,57 @@ int dsx_compute_device(dsx_handle *h, const void *dL, const void *dR, int32_t H,
     rc = ensure_buffers(h, H, W, false);
     if (rc) return rc;
     return run(h, dL, dR, H, W, stride_bytes, d_out_fixed, d_out_float, static_cast<hipStream_t>(hip_stream));
+}
+
+int dsx_postprocess_fast_device(const void *d_disp, int32_t H, int32_t W, int64_t in_pitch, int32_t crop,
+                                void *d_out_disp, void *d_out_depth, double focal_length, double baseline,
+                                double doffs, double eps, double max_depth, int32_t has_max_depth,
+                                void *hip_stream) {
+    g_err.clear();
+    if (!d_disp) return fail(DSX_EINVAL, "d_disp is NULL");
+    if (H <= 0 || W <= 0 || in_pitch < W) return fail(DSX_EINVAL, "bad shape / pitch");
+    if (crop < 0) return fail(DSX_EINVAL, "crop must be >= 0");
+    if (crop >= W || (!d_out_disp && !d_out_depth)) return DSX_OK;  // empty result, as disp[:, crop:] is
+    dsx::PostArgs a{};
+    a.disp = static_cast<const float *>(d_disp);
+    a.in_pitch = in_pitch;
+    a.H = H;
+    a.W = W;
+    a.crop = crop;
+    a.out_disp = static_cast<float *>(d_out_disp);
+    a.out_depth = static_cast<float *>(d_out_depth);
+    a.fB = (float)(focal_length * baseline);
+    a.doffs = (float)doffs;
+    a.eps = (float)eps;
+    a.max_depth = (float)max_depth;
+    a.has_max = has_max_depth ? 1 : 0;
+    DSX_HIP(dsx::launch_post_fast(a, static_cast<hipStream_t>(hip_stream)));
+    return DSX_OK;
+}
+
+int dsx_rectify_device(const void *d_img, int32_t Hs, int32_t Ws, int64_t stride_bytes, int32_t channels,
+                       const float *d_mapx, const float *d_mapy, int32_t H, int32_t W, void *d_out,
+                       void *hip_stream) {
+    g_err.clear();
+    if (!d_img || !d_out) return fail(DSX_EINVAL, "NULL image or output");
+    if (channels != 1 && channels != 3) return fail(DSX_EINVAL, "channels must be 1 or 3");
+    if (Hs <= 0 || Ws <= 0 || stride_bytes < (int64_t)Ws * channels) return fail(DSX_EINVAL, "bad source shape");
+    if ((d_mapx == nullptr) != (d_mapy == nullptr)) return fail(DSX_EINVAL, "give both maps or neither");
+    if (!d_mapx && (H != Hs || W != Ws || channels != 3))
+        return fail(DSX_EINVAL, "gray conversion alone needs a 3-channel image and H, W = Hs, Ws");
+    if (H <= 0 || W <= 0) return fail(DSX_EINVAL, "bad output shape");
+    dsx::RectArgs a{};
+    a.img = static_cast<const uint8_t *>(d_img);
+    a.stride = stride_bytes;
+    a.Hs = Hs;
+    a.Ws = Ws;
+    a.mapx = d_mapx;
+    a.mapy = d_mapy;
+    a.H = H;
+    a.W = W;
+    a.out = static_cast<uint8_t *>(d_out);
+    DSX_HIP(dsx::launch_rectify(a, channels, static_cast<hipStream_t>(hip_stream)));
+    return DSX_OK;
 }
 
 int dsx_right_map_device(dsx_handle *h, const void *dL, const void *dR, int32_t H, int32_t W, int64_t stride_bytes,

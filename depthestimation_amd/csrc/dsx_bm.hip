@@ -107,19 +107,6 @@ __device__ __forceinline__ uint32_t gmin(uint32_t v) {
     return v;
 }
 
-// q = trunc(num / den2) (C semantics), den2 > 0, |q| small: float estimate + exact fix-up.
-__device__ __forceinline__ int div_trunc_small(int num, int den2) {
-    int q = (int)__builtin_truncf((float)num * __builtin_amdgcn_rcpf((float)den2));
-    int r = num - q * den2;
-    if (num >= 0) {
-        if (r < 0) { --q; r += den2; }
-        if (r >= den2) { ++q; }
-    } else {
-        if (r > 0) { ++q; r -= den2; }
-        if (r <= -den2) { --q; }
-    }
-    return q;
-}
 
 typedef const __attribute__((address_space(4))) uint32_t cu32;
 

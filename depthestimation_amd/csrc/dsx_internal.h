@@ -48,10 +48,50 @@ struct VolArgs {
 
 constexpr int kStripWidth = 32;  // TX of bm2
 
+// q = trunc(num / den2) (C semantics), den2 > 0, |q| small (the sub-pixel correction): float
+// reciprocal estimate + exact integer fix-up; replaces the ~40-instruction integer division.
+__device__ __forceinline__ int div_trunc_small(int num, int den2) {
+    int q = (int)__builtin_truncf((float)num * __builtin_amdgcn_rcpf((float)den2));
+    int r = num - q * den2;
+    if (num >= 0) {
+        if (r < 0) { --q; r += den2; }
+        if (r >= den2) { ++q; }
+    } else {
+        if (r > 0) { ++q; r -= den2; }
+        if (r <= -den2) { --q; }
+    }
+    return q;
+}
+
 // nw = waves per block: SAD Dp = 128*nw (nw in {1,2,4}), SSD Dp = 64*nw (nw in {1,2,4,8}).
 hipError_t launch_bm2(int radius, bool ssd, int nw, const Bm2Args &a, hipStream_t st);
 hipError_t launch_volume_wta(int TX, bool ssd, const VolArgs &a, hipStream_t st);
 
 size_t volume_smem_bytes(int TX, bool ssd, int Dp, int TPP, int W);
+
+// Fast-mode epilogue (dsx_post.hip): crop + 3x3 median + optional depth.
+struct PostArgs {
+    const float *disp;  // H x W float disparity, row pitch in_pitch elements
+    int64_t in_pitch;
+    int H, W, crop;
+    float *out_disp;   // H x (W - crop) or null
+    float *out_depth;  // H x (W - crop) or null
+    float fB, doffs, eps, max_depth;  // float32(f * B), float32(doffs), float32(eps), float32(max_depth)
+    int has_max;
+};
+hipError_t launch_post_fast(const PostArgs &a, hipStream_t st);
+
+// Rectification (dsx_rectify.hip): gray conversion fused with the fixed-point bilinear remap.
+struct RectArgs {
+    const uint8_t *img;  // Hs x Ws x channels (channels 1 or 3, BGR order), row stride in bytes
+    int64_t stride;
+    int Hs, Ws;
+    const float *mapx, *mapy;  // H x W float32 maps (null: gray conversion only, output Hs x Ws)
+    int H, W;
+    uint8_t *out;              // H x W uint8, contiguous
+};
+hipError_t launch_rectify(const RectArgs &a, int channels, hipStream_t st);
+
+
 
 }  // namespace dsx

@@ -172,3 +172,59 @@ class HipBlockMatcher:
         b = ctypes.c_int64(0)
         _dsx.check(_dsx.lib().dsx_workspace_bytes(self._handle(), ctypes.byref(b)), "dsx_workspace_bytes")
         return b.value
+
+
+def postprocess_fast_device(disp, crop, focal_length=None, baseline=None, doffs=0.0, eps=1e-6, max_depth=None,
+                            out_disp=None, out_depth=None, stream=None):
+    """Fast-mode epilogue on the device (dsx_postprocess_fast_device; stereo_core.py:168-196):
+    crop ``[:, crop:]`` -> 3x3 median (cv2.medianBlur semantics) -> depth when focal length and
+    baseline are given.  ``disp``: float32 H x W HIP tensor (unit column stride).  Returns
+    (disp_cropped, depth or None) as HIP tensors."""
+    import torch
+
+    if disp.dtype != torch.float32 or disp.dim() != 2 or disp.stride(1) != 1 or not disp.is_cuda:
+        raise ValueError("disp must be a float32 H x W device tensor with unit column stride")
+    H, W = disp.shape
+    Wc = max(W - int(crop), 0)
+    if out_disp is None:
+        out_disp = torch.empty((H, Wc), dtype=torch.float32, device=disp.device)
+    want_depth = focal_length is not None and baseline is not None
+    if want_depth and out_depth is None:
+        out_depth = torch.empty((H, Wc), dtype=torch.float32, device=disp.device)
+    sptr = None if stream is None else (stream if isinstance(stream, int) else stream.cuda_stream)
+    rc = _dsx.lib().dsx_postprocess_fast_device(
+        disp.data_ptr(), H, W, disp.stride(0), int(crop), _ptr(out_disp) if Wc else None,
+        _ptr(out_depth) if (want_depth and Wc) else None, float(focal_length or 0.0), float(baseline or 0.0),
+        float(doffs or 0.0), float(eps), float(max_depth or 0.0), int(max_depth is not None), sptr)
+    _dsx.check(rc, "dsx_postprocess_fast_device")
+    return out_disp, (out_depth if want_depth else None)
+
+
+def rectify_device(img, mapx=None, mapy=None, out=None, stream=None):
+    """BGR->gray fused with the fixed-point bilinear remap on the device (dsx_rectify_device;
+    rectify.py:183-186 + stereo_core.py:155-159).  ``img``: uint8 H x W x 3 (BGR) or H x W HIP
+    tensor; ``mapx``/``mapy``: float32 HIP maps (None: gray conversion only).  Returns uint8."""
+    import torch
+
+    if img.dtype != torch.uint8 or not img.is_cuda or img.dim() not in (2, 3):
+        raise ValueError("img must be a uint8 H x W (x 3) device tensor")
+    ch = 1 if img.dim() == 2 else img.shape[2]
+    if ch not in (1, 3) or img.stride(-1) != 1 or (ch == 3 and img.stride(1) != 3):
+        raise ValueError("img must be gray or packed 3-channel with unit element stride")
+    Hs, Ws = img.shape[0], img.shape[1]
+    if mapx is None:
+        if ch == 1:
+            return img if out is None else out.copy_(img)
+        H, W = Hs, Ws
+    else:
+        if mapx.dtype != torch.float32 or mapx.shape != mapy.shape or not mapx.is_contiguous() or not mapy.is_contiguous():
+            raise ValueError("maps must be contiguous float32 tensors of the same shape")
+        H, W = mapx.shape
+    if out is None:
+        out = torch.empty((H, W), dtype=torch.uint8, device=img.device)
+    sptr = None if stream is None else (stream if isinstance(stream, int) else stream.cuda_stream)
+    rc = _dsx.lib().dsx_rectify_device(img.data_ptr(), Hs, Ws, img.stride(0), ch,
+                                       None if mapx is None else mapx.data_ptr(),
+                                       None if mapy is None else mapy.data_ptr(), H, W, out.data_ptr(), sptr)
+    _dsx.check(rc, "dsx_rectify_device")
+    return out

@@ -23,7 +23,7 @@ from typing import Dict, Optional, Tuple
 
 import numpy as np
 
-from .matcher import HipBlockMatcher
+from .matcher import HipBlockMatcher, postprocess_fast_device, rectify_device
 from .postprocess import median_blur3, postprocess_disparity
 from .rectify import RectificationCache, rectify_images, to_grayscale_bgr
 
@@ -38,6 +38,7 @@ class StereoCore:
         self.fast_mode = fast_mode
         self.sgbm = None
         self._rect_cache = RectificationCache()
+        self._dev_maps = None  # (host maps dict id, device, (map1_L, map2_L, map1_R, map2_R) on the device)
         # stereo_core.py:16-39 defaults, then the build keys
         self.sgbm_params = {
             'min_disp': 0,
@@ -176,6 +177,61 @@ class StereoCore:
             out = torch.empty(left.shape, dtype=torch.float32, device=left.device)
         self.sgbm.compute_device(left, right, out_float=out, stream=stream)
         return out
+
+    def _prepare_rectified_device(self, left, right, stream=None):
+        """Device version of ``_prepare_rectified`` (stereo_core.py:125-160): uint8 HIP frames
+        (H x W x 3 BGR or gray) -> rectified gray on the device.  The maps come from the same
+        host RectificationCache (computed once per calibration) and stay resident in HBM."""
+        import torch
+        p = self.sgbm_params
+        if all(p.get(k) is not None for k in ('cam_matrix_L', 'cam_matrix_R', 'baseline', 'image_width',
+                                               'image_height')):
+            W, H = int(p['image_width']), int(p['image_height'])
+            if tuple(left.shape[:2]) != (H, W) or tuple(right.shape[:2]) != (H, W):
+                raise ValueError("device rectification needs frames of the calibrated size "
+                                 f"{W}x{H} (host rectify_images resizes)")
+            maps = self._rect_cache.get_maps(p['cam_matrix_L'], p['cam_matrix_R'], p['baseline'], W, H,
+                                             p.get('dist_coeff_L'), p.get('dist_coeff_R'), p.get('rotation'),
+                                             p.get('translation'), 1.0)
+            if self._dev_maps is None or self._dev_maps[0] is not maps or self._dev_maps[1] != left.device:
+                dm = tuple(torch.from_numpy(maps[k]).to(left.device) for k in ('map1_L', 'map2_L', 'map1_R', 'map2_R'))
+                self._dev_maps = (maps, left.device, dm)
+            m1L, m2L, m1R, m2R = self._dev_maps[2]
+            return rectify_device(left, m1L, m2L, stream=stream), rectify_device(right, m1R, m2R, stream=stream)
+        return rectify_device(left, stream=stream), rectify_device(right, stream=stream)
+
+    def estimate_depth_device(self, left_source, right_source, stream=None):
+        """``estimate_depth`` (stereo_core.py:274-293) with every step on the device: raw uint8
+        HIP frames -> rectify / gray -> matcher -> crop + median (+ depth).  Returns HIP tensors."""
+        if left_source is None or right_source is None:
+            raise ValueError("Left and right sources must be set before estimating depth.")
+        self.left_rectified, self.right_rectified = self._prepare_rectified_device(left_source, right_source, stream)
+        return self.process_pair_device(self.left_rectified, self.right_rectified, stream=stream)
+
+    def process_pair_device(self, left, right, stream=None):
+        """Device-resident ``_process_pair`` (stereo_core.py:162-200) for rectified uint8 HIP
+        tensors: matcher -> crop -> 3x3 median -> depth, all in HBM (fast mode; SURVEY.md 8f
+        row F1).  Returns (disparity_px, depth_m or None) as float32 HIP tensors.  Without
+        fast_mode the post-processing runs on the host (GPU post-processing is row F2) and the
+        results are copied back to the device."""
+        import torch
+        disp = self.compute_disparity_device(left, right, stream=stream)
+        p = self.sgbm_params
+        f, B = p.get('focal_length'), p.get('baseline')
+        doffs, eps, max_depth = p.get('doffs', 0.0), p.get('min_disp', 5.0), p.get('max_depth')
+        if self.fast_mode:
+            return postprocess_fast_device(disp, p['num_disp'], f, B, doffs, eps, max_depth, stream=stream)
+        if stream is not None:
+            stream.synchronize()
+        else:
+            torch.cuda.synchronize(disp.device)
+        d = postprocess_disparity(disp.cpu().numpy()[:, p['num_disp']:], max_speckle_size=int(100 * self.downscale_factor),
+                                  max_diff=1.0, outlier_threshold=2.5, fill_method='inpaint',
+                                  apply_outlier_removal=True, apply_hole_filling=p.get('hole_filling', False))
+        depth = None
+        if f is not None and B is not None:
+            depth = torch.from_numpy(self.disparity_to_depth(d, f, B, doffs, eps=eps, max_depth=max_depth)).to(disp.device)
+        return torch.from_numpy(d).to(disp.device), depth
 
     def disparity_to_depth(self, disp: np.ndarray, f_pixels: float, baseline_m: float, doffs: float = 0.0,
                            eps: float = 1e-6, max_depth: Optional[float] = None) -> np.ndarray:

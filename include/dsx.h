@@ -109,6 +109,31 @@ int dsx_compute_device(dsx_handle *h, const void *dL, const void *dR, int32_t H,
 int dsx_right_map_device(dsx_handle *h, const void *dL, const void *dR, int32_t H, int32_t W,
                          int64_t stride_bytes, void *d_out_dR, void *hip_stream);
 
+/* Fast-mode epilogue on the device, replacing the host steps after the
+ * matcher in StereoCore._process_pair with fast_mode=True (stereo_core.py:168-196):
+ *   out_disp  = medianBlur(disp[:, crop:], 3)               (:168 crop by num_disp, :173 median,
+ *                                                            replicated border of the cropped map)
+ *   out_depth = f*B / (out_disp + doffs) where out_disp + doffs > eps, else +inf;
+ *               clamped to max_depth when has_max_depth     (:186-196 -> disparity_to_depth :234-272)
+ * d_disp: float32 H x W, row pitch `in_pitch` elements (>= W).  d_out_disp / d_out_depth: contiguous
+ * float32 H x (W - crop); either may be NULL.  Scalars follow numpy-2 float32 rules (f*B, doffs,
+ * eps, max_depth are rounded to float32), so results equal the host path bit for bit.
+ * No handle: stateless, asynchronous on hip_stream. */
+int dsx_postprocess_fast_device(const void *d_disp, int32_t H, int32_t W, int64_t in_pitch, int32_t crop,
+                                void *d_out_disp, void *d_out_depth, double focal_length, double baseline,
+                                double doffs, double eps, double max_depth, int32_t has_max_depth,
+                                void *hip_stream);
+
+/* Per-frame rectification on the device, replacing cv2.cvtColor(BGR2GRAY)
+ * + cv2.remap(INTER_LINEAR) of rectify.py:183-186 (cached-maps path) and stereo_core.py:155-159:
+ * d_img: uint8 Hs x Ws x channels (channels 1 or 3, BGR), row stride `stride_bytes`;
+ * d_mapx, d_mapy: float32 H x W maps (initUndistortRectifyMap CV_32FC1 semantics), or both NULL
+ *   for the gray conversion alone (then H, W must equal Hs, Ws);
+ * d_out: uint8 H x W.  Fixed-point bilinear (1/32 px, 15-bit weights), border 0.  Async. */
+int dsx_rectify_device(const void *d_img, int32_t Hs, int32_t Ws, int64_t stride_bytes, int32_t channels,
+                       const float *d_mapx, const float *d_mapy, int32_t H, int32_t W, void *d_out,
+                       void *hip_stream);
+
 /* Per-kernel timings accumulated since the last reset (params.timing = 1): names are
  * written as a ';'-separated list into `names` (capacity `names_cap`), average ms per
  * launch into ms[i], launch counts into counts[i]; *n = number of kernels. */

@@ -73,3 +73,102 @@ def test_video_estimator_on_gpu():
     v.configure_sgbm(num_disp=32, focal_length=500.0, baseline=0.2)
     out = list(v.estimate_depth())
     assert len(out) == 4 and all(o.shape == (48, 200 - 32) for o in out)
+
+
+@pytest.mark.parametrize("crop,depth,max_depth", [(0, False, None), (64, True, None), (7, True, 40.0),
+                                                  (130, True, 5.0)])
+def test_postprocess_fast_device_matches_host(crop, depth, max_depth):
+    """F1 kernel vs the host restatement: crop + cv2-style 3x3 median + disparity_to_depth."""
+    import torch
+    from depthestimation_amd.matcher import postprocess_fast_device
+    rng = np.random.default_rng(crop)
+    H, W = 37, 150
+    d = (rng.integers(-16, 64 * 16, (H, W)) / 16.0).astype(np.float32)
+    d[rng.random((H, W)) < 0.1] = -1.0  # invalid pixels
+    f, B, doffs, eps = (700.0, 0.12, 0.5, 0.0) if depth else (None, None, 0.0, 1e-6)
+    dd = torch.from_numpy(d).cuda()
+    od, oz = postprocess_fast_device(dd, crop, f, B, doffs, eps, max_depth)
+    torch.cuda.synchronize()
+    ref = median_blur3(d[:, crop:])
+    np.testing.assert_array_equal(od.cpu().numpy(), ref)
+    if depth:
+        zref = StereoCore.disparity_to_depth(None, ref, f, B, doffs, eps=eps, max_depth=max_depth)
+        np.testing.assert_array_equal(oz.cpu().numpy(), zref)
+    else:
+        assert oz is None
+
+
+def test_process_pair_device_fast_mode_matches_host():
+    import torch
+    Lg, Rg, _ = stereo_pair(64, 256, 0, 64, seed=31)
+    core = StereoCore(fast_mode=True)
+    core.configure_sgbm(num_disp=64, block_size=7, focal_length=800.0, baseline=0.1, max_depth=30.0)
+    host_d, host_z = core._process_pair(Lg, Rg)
+    dev_d, dev_z = core.process_pair_device(torch.from_numpy(Lg).cuda(), torch.from_numpy(Rg).cuda())
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(dev_d.cpu().numpy(), host_d)
+    np.testing.assert_array_equal(dev_z.cpu().numpy(), host_z)
+
+
+def _calib(W, H):
+    K1 = np.array([[0.9 * W, 0, W / 2 + 3.5], [0, 0.9 * W, H / 2 - 2.0], [0, 0, 1]])
+    K2 = np.array([[0.92 * W, 0, W / 2 - 4.0], [0, 0.92 * W, H / 2 + 1.5], [0, 0, 1]])
+    from depthestimation_amd.rectify import rodrigues
+    return dict(cam_matrix_L=K1, cam_matrix_R=K2, dist_coeff_L=np.array([-0.12, 0.05, 0.001, -0.0005, 0.0]),
+                dist_coeff_R=np.array([-0.1, 0.03, -0.0008, 0.0004, 0.0]), rotation=rodrigues([0.01, -0.02, 0.005]),
+                translation=np.array([-0.12, 0.002, 0.001]), baseline=0.12, image_width=W, image_height=H)
+
+
+@pytest.mark.parametrize("channels", [1, 3])
+def test_rectify_device_matches_host(channels):
+    """F3 kernel vs the host restatement (gray + fixed-point remap), bit-exact."""
+    import torch
+    from depthestimation_amd.matcher import rectify_device
+    from depthestimation_amd.rectify import compute_maps, remap_linear_u8
+    H, W = 90, 160
+    rng = np.random.default_rng(channels)
+    img = rng.integers(0, 256, (H, W, 3) if channels == 3 else (H, W), dtype=np.uint8)
+    c = _calib(W, H)
+    maps = compute_maps(c['cam_matrix_L'], c['cam_matrix_R'], c['baseline'], W, H, c['dist_coeff_L'],
+                        c['dist_coeff_R'], c['rotation'], c['translation'], alpha=1.0)
+    ref = remap_linear_u8(to_grayscale_bgr(img), maps['map1_L'], maps['map2_L'])
+    got = rectify_device(torch.from_numpy(img).cuda(), torch.from_numpy(maps['map1_L']).cuda(),
+                         torch.from_numpy(maps['map2_L']).cuda())
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(got.cpu().numpy(), ref)
+    if channels == 3:
+        g = rectify_device(torch.from_numpy(img).cuda())
+        np.testing.assert_array_equal(g.cpu().numpy(), to_grayscale_bgr(img))
+
+
+def test_rectify_device_degenerate_maps():
+    """NaN / inf map entries (identity-K calibrations) land outside the image -> 0, like the host."""
+    import torch
+    from depthestimation_amd.matcher import rectify_device
+    from depthestimation_amd.rectify import remap_linear_u8
+    img = np.random.default_rng(3).integers(0, 256, (20, 30), dtype=np.uint8)
+    mx = np.tile(np.arange(30, dtype=np.float32), (20, 1)) + 0.3
+    my = np.tile(np.arange(20, dtype=np.float32)[:, None], (1, 30)) - 0.6
+    mx[2, :5] = np.nan
+    mx[3, :3] = np.inf
+    my[4, :4] = -np.inf
+    ref = remap_linear_u8(img, mx, my)
+    got = rectify_device(torch.from_numpy(img).cuda(), torch.from_numpy(mx).cuda(), torch.from_numpy(my).cuda())
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(got.cpu().numpy(), ref)
+
+
+def test_estimate_depth_device_calibrated_matches_host():
+    """Raw BGR frames -> device rectify -> matcher -> fast epilogue, equal to the host pipeline."""
+    import torch
+    H, W = 96, 200
+    Lg, Rg, _ = stereo_pair(H, W, 0, 48, seed=41)
+    L = np.stack([Lg, np.roll(Lg, 1, 0), Lg // 2], 2).astype(np.uint8)
+    R = np.stack([Rg, np.roll(Rg, 1, 0), Rg // 2], 2).astype(np.uint8)
+    core = StereoCore(fast_mode=True)
+    core.configure_sgbm(num_disp=48, block_size=5, focal_length=180.0, **_calib(W, H))
+    hd, hz = core.estimate_depth(L, R)
+    dd, dz = core.estimate_depth_device(torch.from_numpy(L).cuda(), torch.from_numpy(R).cuda())
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(dd.cpu().numpy(), hd)
+    np.testing.assert_array_equal(dz.cpu().numpy(), hz)
