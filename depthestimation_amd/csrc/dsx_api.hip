@@ -432,6 +432,47 @@ int dsx_postprocess_fast_device(const void *d_disp, int32_t H, int32_t W, int64_
     return DSX_OK;
 }
 
+size_t dsx_postprocess_workspace_bytes(int32_t H, int32_t W, int32_t crop) {
+    if (H <= 0 || W <= 0 || crop < 0) return 0;
+    return dsx::post_full_workspace(H, W, crop);
+}
+
+int dsx_postprocess_full_device(const void *d_disp, int32_t H, int32_t W, int64_t in_pitch, int32_t crop,
+                                int32_t max_speckle_size, double max_diff, int32_t apply_outlier_removal,
+                                double outlier_threshold, int32_t outlier_kernel, void *d_out_disp,
+                                void *d_out_depth, double focal_length, double baseline, double doffs, double eps,
+                                double max_depth, int32_t has_max_depth, void *d_workspace,
+                                size_t workspace_bytes, void *hip_stream) {
+    g_err.clear();
+    if (!d_disp) return fail(DSX_EINVAL, "d_disp is NULL");
+    if (H <= 0 || W <= 0 || in_pitch < W || crop < 0) return fail(DSX_EINVAL, "bad shape / pitch / crop");
+    if (outlier_kernel < 1 || (outlier_kernel & 1) == 0) return fail(DSX_EINVAL, "outlier_kernel must be odd");
+    if (crop >= W || (!d_out_disp && !d_out_depth)) return DSX_OK;
+    if (!d_workspace || workspace_bytes < dsx::post_full_workspace(H, W, crop))
+        return fail(DSX_EINVAL, "workspace too small (dsx_postprocess_workspace_bytes)");
+    if ((int64_t)H * (W - crop) > 0x7FFFFFFF) return fail(DSX_EINVAL, "image too large for int32 labels");
+    dsx::PostFullArgs a{};
+    a.disp = static_cast<const float *>(d_disp);
+    a.in_pitch = in_pitch;
+    a.H = H;
+    a.W = W;
+    a.crop = crop;
+    a.max_speckle = max_speckle_size;
+    a.max_diff16 = (int)(max_diff * 16);  // int(max_diff * 16), postprocess.py:30
+    a.apply_outliers = apply_outlier_removal ? 1 : 0;
+    a.kernel = outlier_kernel;
+    a.thr = (float)outlier_threshold;
+    a.out_disp = static_cast<float *>(d_out_disp);
+    a.out_depth = static_cast<float *>(d_out_depth);
+    a.fB = (float)(focal_length * baseline);
+    a.doffs = (float)doffs;
+    a.eps = (float)eps;
+    a.max_depth = (float)max_depth;
+    a.has_max = has_max_depth ? 1 : 0;
+    DSX_HIP(dsx::launch_post_full(a, d_workspace, static_cast<hipStream_t>(hip_stream)));
+    return DSX_OK;
+}
+
 int dsx_rectify_device(const void *d_img, int32_t Hs, int32_t Ws, int64_t stride_bytes, int32_t channels,
                        const float *d_mapx, const float *d_mapy, int32_t H, int32_t W, void *d_out,
                        void *hip_stream) {

@@ -81,6 +81,24 @@ struct PostArgs {
 };
 hipError_t launch_post_fast(const PostArgs &a, hipStream_t st);
 
+// Full post-processing (speckles + outliers + median + depth), dsx_post.hip.
+struct PostFullArgs {
+    const float *disp;
+    int64_t in_pitch;
+    int H, W, crop;
+    int max_speckle, max_diff16, apply_outliers, kernel;
+    float thr;
+    float *out_disp, *out_depth;
+    float fB, doffs, eps, max_depth;
+    int has_max;
+    // workspace views (set by launch_post_full)
+    int *parent, *count, *root;
+    int16_t *v16;
+    float *t0, *t1;
+};
+size_t post_full_workspace(int H, int W, int crop);
+hipError_t launch_post_full(PostFullArgs a, void *ws, hipStream_t st);
+
 // Rectification (dsx_rectify.hip): gray conversion fused with the fixed-point bilinear remap.
 struct RectArgs {
     const uint8_t *img;  // Hs x Ws x channels (channels 1 or 3, BGR order), row stride in bytes

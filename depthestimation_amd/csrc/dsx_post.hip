@@ -8,6 +8,8 @@
 // (python scalars are cast to float32 first), so the result is bit-identical to the host path.
 #include "dsx_internal.h"
 
+#include <algorithm>
+
 namespace dsx {
 
 __device__ __forceinline__ void sort2(float &a, float &b) {
@@ -64,6 +66,178 @@ hipError_t launch_post_fast(const PostArgs &a, hipStream_t st) {
     const dim3 grid((Wc + kPostTX - 1) / kPostTX, (a.H + kPostTY - 1) / kPostTY);
     hipLaunchKernelGGL(post_fast, grid, dim3(kPostTX, kPostTY), 0, st, a);
     return hipGetLastError();
+}
+
+
+// ---------------------------------------------------------------------------------------------
+// Full post-processing: postprocess_disparity (depthlib/postprocess.py:
+// 120-171) without hole filling, on the cropped map:
+//   1. filter_speckles (:6-35): d16 = int16(trunc(d * 16)); 4-connected components over edges
+//      whose values differ by <= max_diff16 (pixels equal to 0 = newVal never join); components
+//      of <= max_speckle pixels -> 0; result d16 / 16.
+//   2. detect_outliers (:37-70, :152-158): 5x5 BORDER_REFLECT_101 box mean / mean of squares
+//      (exact float64 window sums x 1/k^2 -> float32), |d - mean| > thr * std on d > 0 -> 0.
+//   3. 3x3 median (:169) and depth: post_fast with crop 0.
+// Components use atomic union-find (parents only ever point to smaller indices, CAS links a root
+// under the smaller root), a flatten + size-count pass and an apply pass.
+// ---------------------------------------------------------------------------------------------
+#pragma clang fp contract(off)
+
+__device__ __forceinline__ int uf_load(const int *parent, int x) {
+    return __hip_atomic_load(parent + x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__device__ __forceinline__ int uf_find(const int *parent, int x) {
+    int p = uf_load(parent, x);
+    while (p != x) {
+        x = p;
+        p = uf_load(parent, x);
+    }
+    return x;
+}
+
+__device__ __forceinline__ void uf_unite(int *parent, int a, int b) {
+    while (true) {
+        a = uf_find(parent, a);
+        b = uf_find(parent, b);
+        if (a == b) return;
+        if (a < b) {
+            const int t = a;
+            a = b;
+            b = t;
+        }
+        int expected = a;
+        if (__hip_atomic_compare_exchange_strong(parent + a, &expected, b, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_AGENT))
+            return;
+    }
+}
+
+__global__ __launch_bounds__(256) void speckle_init(PostFullArgs a) {
+    const int Wc = a.W - a.crop;
+    const int64_t n = (int64_t)a.H * Wc;
+    for (int64_t p = (int64_t)blockIdx.x * 256 + threadIdx.x; p < n; p += (int64_t)gridDim.x * 256) {
+        const int y = (int)(p / Wc), x = (int)(p - (int64_t)y * Wc);
+        const float v = a.disp[(int64_t)y * a.in_pitch + a.crop + x];
+        const int16_t d16 = (int16_t)(int)__builtin_truncf(v * 16.0f);
+        a.v16[p] = d16;
+        a.parent[p] = d16 != 0 ? (int)p : -1;
+        a.count[p] = 0;
+    }
+}
+
+__global__ __launch_bounds__(256) void speckle_union(PostFullArgs a) {
+    const int Wc = a.W - a.crop;
+    const int64_t n = (int64_t)a.H * Wc;
+    for (int64_t p = (int64_t)blockIdx.x * 256 + threadIdx.x; p < n; p += (int64_t)gridDim.x * 256) {
+        const int v = a.v16[p];
+        if (v == 0) continue;
+        const int y = (int)(p / Wc), x = (int)(p - (int64_t)y * Wc);
+        if (x > 0) {
+            const int u = a.v16[p - 1];
+            if (u != 0 && abs(u - v) <= a.max_diff16) uf_unite(a.parent, (int)p, (int)p - 1);
+        }
+        if (y > 0) {
+            const int u = a.v16[p - Wc];
+            if (u != 0 && abs(u - v) <= a.max_diff16) uf_unite(a.parent, (int)p, (int)(p - Wc));
+        }
+    }
+}
+
+__global__ __launch_bounds__(256) void speckle_count(PostFullArgs a) {
+    const int64_t n = (int64_t)a.H * (a.W - a.crop);
+    for (int64_t p = (int64_t)blockIdx.x * 256 + threadIdx.x; p < n; p += (int64_t)gridDim.x * 256) {
+        if (a.v16[p] == 0) continue;
+        const int r = uf_find(a.parent, (int)p);
+        atomicAdd(a.count + r, 1);
+        a.root[p] = r;
+    }
+}
+
+__global__ __launch_bounds__(256) void speckle_apply(PostFullArgs a) {
+    const int64_t n = (int64_t)a.H * (a.W - a.crop);
+    for (int64_t p = (int64_t)blockIdx.x * 256 + threadIdx.x; p < n; p += (int64_t)gridDim.x * 256) {
+        int v = a.v16[p];
+        if (v != 0 && a.count[a.root[p]] <= a.max_speckle) v = 0;
+        a.t0[p] = (float)v / 16.0f;
+    }
+}
+
+__device__ __forceinline__ int reflect101(int i, int n) {
+    if (n == 1) return 0;
+    const int period = 2 * (n - 1);
+    i = abs(i) % period;
+    return i >= n ? period - i : i;
+}
+
+__global__ __launch_bounds__(256) void outliers(PostFullArgs a) {
+    const int Wc = a.W - a.crop;
+    const int64_t n = (int64_t)a.H * Wc;
+    const int r = a.kernel / 2;
+    const double scale = 1.0 / (double)(a.kernel * a.kernel);
+    for (int64_t p = (int64_t)blockIdx.x * 256 + threadIdx.x; p < n; p += (int64_t)gridDim.x * 256) {
+        const int y = (int)(p / Wc), x = (int)(p - (int64_t)y * Wc);
+        double s = 0.0, s2 = 0.0;
+        for (int j = -r; j <= r; ++j) {
+            const float *row = a.t0 + (int64_t)reflect101(y + j, a.H) * Wc;
+            for (int i = -r; i <= r; ++i) {
+                const float v = row[reflect101(x + i, Wc)];
+                s += (double)v;
+                s2 += (double)(v * v);
+            }
+        }
+        const float mean = (float)(s * scale), msq = (float)(s2 * scale);
+        const float var = msq - mean * mean;
+        const float sd = sqrtf(var > 0.0f ? var : 0.0f);
+        const float d = a.t0[p];
+        const bool out = d > 0.0f && fabsf(d - mean) > a.thr * sd;
+        a.t1[p] = out ? 0.0f : d;
+    }
+}
+
+#pragma clang fp contract(on)
+
+size_t post_full_workspace(int H, int W, int crop) {
+    const size_t n = (size_t)H * (size_t)(W > crop ? W - crop : 0);
+    const auto r = [](size_t b) { return (b + 255) & ~(size_t)255; };
+    return r(n * 4) * 3 + r(n * 2) + r(n * 4) * 2;  // parent, count, root | v16 | t0, t1
+}
+
+hipError_t launch_post_full(PostFullArgs a, void *ws, hipStream_t st) {
+    const int Wc = a.W - a.crop;
+    const size_t n = (size_t)a.H * Wc;
+    const auto r = [](size_t b) { return (b + 255) & ~(size_t)255; };
+    uint8_t *w = static_cast<uint8_t *>(ws);
+    a.parent = reinterpret_cast<int *>(w);
+    a.count = reinterpret_cast<int *>(w + r(n * 4));
+    a.root = reinterpret_cast<int *>(w + 2 * r(n * 4));
+    a.v16 = reinterpret_cast<int16_t *>(w + 3 * r(n * 4));
+    a.t0 = reinterpret_cast<float *>(w + 3 * r(n * 4) + r(n * 2));
+    a.t1 = reinterpret_cast<float *>(w + 3 * r(n * 4) + r(n * 2) + r(n * 4));
+    const int grid = (int)std::min<size_t>((n + 255) / 256, 4096);
+    hipLaunchKernelGGL(speckle_init, dim3(grid), dim3(256), 0, st, a);
+    hipLaunchKernelGGL(speckle_union, dim3(grid), dim3(256), 0, st, a);
+    hipLaunchKernelGGL(speckle_count, dim3(grid), dim3(256), 0, st, a);
+    hipLaunchKernelGGL(speckle_apply, dim3(grid), dim3(256), 0, st, a);
+    const float *med_in = a.t0;
+    if (a.apply_outliers) {
+        hipLaunchKernelGGL(outliers, dim3(grid), dim3(256), 0, st, a);
+        med_in = a.t1;
+    }
+    PostArgs m{};
+    m.disp = med_in;
+    m.in_pitch = Wc;
+    m.H = a.H;
+    m.W = Wc;
+    m.crop = 0;
+    m.out_disp = a.out_disp;
+    m.out_depth = a.out_depth;
+    m.fB = a.fB;
+    m.doffs = a.doffs;
+    m.eps = a.eps;
+    m.max_depth = a.max_depth;
+    m.has_max = a.has_max;
+    return launch_post_fast(m, st);
 }
 
 }  // namespace dsx

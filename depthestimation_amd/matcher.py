@@ -228,3 +228,34 @@ def rectify_device(img, mapx=None, mapy=None, out=None, stream=None):
                                        None if mapy is None else mapy.data_ptr(), H, W, out.data_ptr(), sptr)
     _dsx.check(rc, "dsx_rectify_device")
     return out
+
+
+def postprocess_full_device(disp, crop, max_speckle_size=50, max_diff=1.0, apply_outlier_removal=True,
+                            outlier_threshold=3.0, outlier_kernel=5, focal_length=None, baseline=None, doffs=0.0,
+                            eps=1e-6, max_depth=None, stream=None):
+    """postprocess_disparity (postprocess.py:120-171, hole filling off) + depth on the device
+    (dsx_postprocess_full_device).  ``disp``: float32 H x W HIP tensor.
+    Returns (disp_cropped, depth or None) as HIP tensors."""
+    import torch
+
+    if disp.dtype != torch.float32 or disp.dim() != 2 or disp.stride(1) != 1 or not disp.is_cuda:
+        raise ValueError("disp must be a float32 H x W device tensor with unit column stride")
+    H, W = disp.shape
+    Wc = max(W - int(crop), 0)
+    out_disp = torch.empty((H, Wc), dtype=torch.float32, device=disp.device)
+    want_depth = focal_length is not None and baseline is not None
+    out_depth = torch.empty((H, Wc), dtype=torch.float32, device=disp.device) if want_depth else None
+    if Wc == 0:
+        return out_disp, out_depth
+    L = _dsx.lib()
+    nbytes = L.dsx_postprocess_workspace_bytes(H, W, int(crop))
+    ws = torch.empty(nbytes, dtype=torch.uint8, device=disp.device)
+    sptr = None if stream is None else (stream if isinstance(stream, int) else stream.cuda_stream)
+    rc = L.dsx_postprocess_full_device(
+        disp.data_ptr(), H, W, disp.stride(0), int(crop), int(max_speckle_size), float(max_diff),
+        int(bool(apply_outlier_removal)), float(outlier_threshold), int(outlier_kernel), out_disp.data_ptr(),
+        out_depth.data_ptr() if want_depth else None, float(focal_length or 0.0), float(baseline or 0.0),
+        float(doffs or 0.0), float(eps), float(max_depth or 0.0), int(max_depth is not None), ws.data_ptr(),
+        nbytes, sptr)
+    _dsx.check(rc, "dsx_postprocess_full_device")
+    return out_disp, out_depth

@@ -10,7 +10,7 @@ each function restates the documented OpenCV semantics with numpy/scipy:
                           0 (newVal=0, postprocess.py:30). Pixels already equal to 0 never join
                           a region.
 * ``detect_outliers``   - normalised k x k box mean / mean of squares with BORDER_REFLECT_101
-                          (cv2.boxFilter default), float64 sums cast to float32.
+                          (cv2.boxFilter default): exact float64 window sums x 1/k^2 -> float32.
 * ``fill_holes``        - 'inpaint': Telea fast-marching inpainting; 'nearest': iterated
                           elliptical dilation (postprocess.py:106-116).
 * ``median_blur3``      - 3 x 3 median with BORDER_REPLICATE (cv2.medianBlur, ksize 3).
@@ -65,7 +65,13 @@ def filter_speckles(disparity, max_speckle_size=100, max_diff=1):
 
 
 def _box_mean(a: np.ndarray, k: int) -> np.ndarray:
-    return ndimage.uniform_filter(a.astype(np.float64), size=k, mode="mirror").astype(np.float32)
+    """cv2.boxFilter(a, -1, (k, k)) for float32: the k x k window sum (BORDER_REFLECT_101) taken
+    exactly in float64, times the scale 1/(k*k), rounded to float32.  The window sums of float32
+    disparities (multiples of 1/16) and of their float32 squares are exact in float64, so the
+    result does not depend on summation order (the GPU kernel gives the same bits)."""
+    a64 = np.asarray(a, np.float32).astype(np.float64)
+    s = ndimage.correlate(a64, np.ones((k, k)), mode="mirror")
+    return (s * (1.0 / (k * k))).astype(np.float32)
 
 
 def detect_outliers(disparity, threshold=3.0, kernel_size=5):

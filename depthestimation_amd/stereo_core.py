@@ -23,7 +23,7 @@ from typing import Dict, Optional, Tuple
 
 import numpy as np
 
-from .matcher import HipBlockMatcher, postprocess_fast_device, rectify_device
+from .matcher import HipBlockMatcher, postprocess_fast_device, postprocess_full_device, rectify_device
 from .postprocess import median_blur3, postprocess_disparity
 from .rectify import RectificationCache, rectify_images, to_grayscale_bgr
 
@@ -210,10 +210,11 @@ class StereoCore:
 
     def process_pair_device(self, left, right, stream=None):
         """Device-resident ``_process_pair`` (stereo_core.py:162-200) for rectified uint8 HIP
-        tensors: matcher -> crop -> 3x3 median -> depth, all in HBM (fast mode; SURVEY.md 8f
-        row F1).  Returns (disparity_px, depth_m or None) as float32 HIP tensors.  Without
-        fast_mode the post-processing runs on the host (GPU post-processing is row F2) and the
-        results are copied back to the device."""
+        tensors: matcher -> crop -> post-processing -> depth, all in HBM.  Fast mode: 3x3 median
+        (SURVEY.md 8f row F1); otherwise speckle filter + outlier removal + median (row F2).
+        Hole filling (Telea inpainting, off by default) has no device kernel: with
+        ``hole_filling`` set, that path post-processes on the host.  Returns float32 HIP tensors
+        (disparity_px, depth_m or None)."""
         import torch
         disp = self.compute_disparity_device(left, right, stream=stream)
         p = self.sgbm_params
@@ -221,13 +222,18 @@ class StereoCore:
         doffs, eps, max_depth = p.get('doffs', 0.0), p.get('min_disp', 5.0), p.get('max_depth')
         if self.fast_mode:
             return postprocess_fast_device(disp, p['num_disp'], f, B, doffs, eps, max_depth, stream=stream)
+        if not p.get('hole_filling', False):
+            return postprocess_full_device(disp, p['num_disp'], max_speckle_size=int(100 * self.downscale_factor),
+                                           max_diff=1.0, apply_outlier_removal=True, outlier_threshold=2.5,
+                                           outlier_kernel=5, focal_length=f, baseline=B, doffs=doffs, eps=eps,
+                                           max_depth=max_depth, stream=stream)
         if stream is not None:
             stream.synchronize()
         else:
             torch.cuda.synchronize(disp.device)
         d = postprocess_disparity(disp.cpu().numpy()[:, p['num_disp']:], max_speckle_size=int(100 * self.downscale_factor),
                                   max_diff=1.0, outlier_threshold=2.5, fill_method='inpaint',
-                                  apply_outlier_removal=True, apply_hole_filling=p.get('hole_filling', False))
+                                  apply_outlier_removal=True, apply_hole_filling=True)
         depth = None
         if f is not None and B is not None:
             depth = torch.from_numpy(self.disparity_to_depth(d, f, B, doffs, eps=eps, max_depth=max_depth)).to(disp.device)

@@ -124,6 +124,21 @@ int dsx_postprocess_fast_device(const void *d_disp, int32_t H, int32_t W, int64_
                                 double doffs, double eps, double max_depth, int32_t has_max_depth,
                                 void *hip_stream);
 
+/* Full post-processing on the device, replacing postprocess_disparity
+ * (postprocess.py:120-171) as StereoCore._process_pair calls it without fast mode
+ * (stereo_core.py:175-184) and with hole filling off (its default, stereo_core.py:38):
+ *   speckle filter (x16 int16, max_speckle_size, max_diff) -> optional box-statistics outlier removal
+ *   (kernel x kernel, threshold) -> 3x3 median -> optional depth (same scalars as
+ *   dsx_postprocess_fast_device).  Input cropped by `crop` columns first (stereo_core.py:168).
+ * d_workspace: >= dsx_postprocess_workspace_bytes(H, W, crop) bytes of device memory. Async. */
+size_t dsx_postprocess_workspace_bytes(int32_t H, int32_t W, int32_t crop);
+int dsx_postprocess_full_device(const void *d_disp, int32_t H, int32_t W, int64_t in_pitch, int32_t crop,
+                                int32_t max_speckle_size, double max_diff, int32_t apply_outlier_removal,
+                                double outlier_threshold, int32_t outlier_kernel, void *d_out_disp,
+                                void *d_out_depth, double focal_length, double baseline, double doffs, double eps,
+                                double max_depth, int32_t has_max_depth, void *d_workspace,
+                                size_t workspace_bytes, void *hip_stream);
+
 /* Per-frame rectification on the device, replacing cv2.cvtColor(BGR2GRAY)
  * + cv2.remap(INTER_LINEAR) of rectify.py:183-186 (cached-maps path) and stereo_core.py:155-159:
  * d_img: uint8 Hs x Ws x channels (channels 1 or 3, BGR), row stride `stride_bytes`;

@@ -172,3 +172,47 @@ def test_estimate_depth_device_calibrated_matches_host():
     torch.cuda.synchronize()
     np.testing.assert_array_equal(dd.cpu().numpy(), hd)
     np.testing.assert_array_equal(dz.cpu().numpy(), hz)
+
+
+def _noisy_disparity(H, W, seed):
+    rng = np.random.default_rng(seed)
+    d = np.full((H, W), 20.0, np.float32)
+    d[:, W // 2:] = 35.5
+    d += (rng.integers(-3, 4, (H, W)) / 16.0).astype(np.float32)           # sub-pixel noise
+    for _ in range(25):                                                    # speckles of 1..60 px
+        y, x, h, w = rng.integers(0, H - 8), rng.integers(0, W - 8), rng.integers(1, 8), rng.integers(1, 8)
+        d[y:y + h, x:x + w] = float(rng.integers(1, 60))
+    d[rng.random((H, W)) < 0.02] = -1.0                                    # invalid
+    d[rng.random((H, W)) < 0.01] = 0.0                                     # newVal pixels
+    d[rng.random((H, W)) < 0.005] = 90.0                                   # outliers
+    return d
+
+
+@pytest.mark.parametrize("crop,outl,maxsp", [(0, True, 50), (16, True, 100), (5, False, 20)])
+def test_postprocess_full_device_matches_host(crop, outl, maxsp):
+    """F2 kernels vs the host restatement of postprocess_disparity (hole filling off)."""
+    import torch
+    from depthestimation_amd.matcher import postprocess_full_device
+    from depthestimation_amd.postprocess import postprocess_disparity
+    d = _noisy_disparity(60, 140, crop + maxsp)
+    ref = postprocess_disparity(d[:, crop:], max_speckle_size=maxsp, max_diff=1.0, outlier_threshold=2.5,
+                                apply_outlier_removal=outl, apply_hole_filling=False)
+    got, z = postprocess_full_device(torch.from_numpy(d).cuda(), crop, max_speckle_size=maxsp, max_diff=1.0,
+                                     apply_outlier_removal=outl, outlier_threshold=2.5, focal_length=100.0,
+                                     baseline=0.3, doffs=0.0, eps=0.0)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(got.cpu().numpy(), ref)
+    np.testing.assert_array_equal(z.cpu().numpy(), StereoCore.disparity_to_depth(None, ref, 100.0, 0.3, 0.0, eps=0.0))
+
+
+def test_process_pair_device_default_mode_matches_host():
+    """The reference's default (non-fast) pipeline on the device equals the host pipeline."""
+    import torch
+    Lg, Rg, _ = stereo_pair(72, 260, 0, 64, seed=51)
+    core = StereoCore(fast_mode=False)
+    core.configure_sgbm(num_disp=64, block_size=5, focal_length=700.0, baseline=0.1)
+    hd, hz = core._process_pair(Lg, Rg)
+    dd, dz = core.process_pair_device(torch.from_numpy(Lg).cuda(), torch.from_numpy(Rg).cuda())
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(dd.cpu().numpy(), hd)
+    np.testing.assert_array_equal(dz.cpu().numpy(), hz)
