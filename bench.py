@@ -107,6 +107,7 @@ def main():
     ap.add_argument("--no-volume-roofline", action="store_true")
     ap.add_argument("--check", action="store_true", help="verify one frame against the C oracle")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline sample length")
+    ap.add_argument("--grid-blocks", type=int, default=0, help="force the persistent grid size (tuning)")
     args = ap.parse_args()
 
     import torch
@@ -143,7 +144,7 @@ def main():
 
     kw = dict(min_disp=0, num_disp=cfg["num_disp"], block_size=cfg["block_size"], cost=cfg["cost"],
               uniqueness_ratio=cfg["uniqueness_ratio"], disp12_max_diff=cfg["disp12_max_diff"], subpixel=True)
-    matcher = HipBlockMatcher(device=local, path=args.path, timing=True, **kw)
+    matcher = HipBlockMatcher(device=local, path=args.path, timing=True, grid_blocks=args.grid_blocks, **kw)
     stream = torch.cuda.current_stream(dev)
 
     def step(i):

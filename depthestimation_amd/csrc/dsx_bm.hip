@@ -28,6 +28,9 @@
 //   side 2 (volume) : tile copied to the [H][W][Dp] cost volume (north-star "K1")
 #include "dsx_internal.h"
 
+#include <cstdio>
+#include <cstdlib>
+
 namespace dsx {
 
 typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
@@ -652,10 +655,12 @@ static hipError_t launch_bm2_side(const Bm2Args &a, hipStream_t st) {
         int cus = 0;
         e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
         if (e != hipSuccess) return e;
-        // the occupancy API over-reports by one block per CU on gfx950 / ROCm 7.2 (measured with
-        // the DSX_TIMELINE census: 9 of 10 reported 1-wave blocks were co-resident), and a
-        // persistent grid that does not fit runs a second generation
-        blocks_per_cu[dev] = nb > 1 ? nb - 1 : 1;
+        // one block per resident slot: the DSX_TIMELINE census showed all 12 reported blocks of
+        // the C2 kernel co-resident (3072 on 256 CUs) and 12/CU beat 11/CU by 5% (C2, C4) while
+        // 13/CU ran a second generation.  DSX_BLOCKS_PER_CU_ADJ (e.g. -1) adjusts for tuning.
+        const char *adj = getenv("DSX_BLOCKS_PER_CU_ADJ");
+        const int nbr = nb + (adj ? atoi(adj) : 0);
+        blocks_per_cu[dev] = nbr > 1 ? nbr : 1;
         num_cu[dev] = cus > 0 ? cus : 1;
     }
     const long T = (long)a.strip_count * a.H;
@@ -663,6 +668,9 @@ static hipError_t launch_bm2_side(const Bm2Args &a, hipStream_t st) {
     if (a.grid_override > 0) grid = a.grid_override;
     if (grid > T) grid = T;
     if (grid < 1) grid = 1;
+    if (getenv("DSX_VERBOSE"))
+        fprintf(stderr, "[dsx] bm2<R=%d,SSD=%d,NW=%d,SIDE=%d> grid %ld (%d/CU) smem %d\n", R, (int)SSD, NW, SIDE, grid,
+                blocks_per_cu[dev], G::SMEM);
     hipLaunchKernelGGL((bm2<R, SSD, NW, SIDE>), dim3((unsigned)grid), dim3(G::NT), G::SMEM, st, a);
     return hipGetLastError();
 }
