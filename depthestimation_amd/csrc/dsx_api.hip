@@ -94,7 +94,8 @@ struct dsx_handle {
     uint8_t *dL = nullptr, *dR = nullptr;
     int16_t *dFixed = nullptr;
     float *dFloat = nullptr;
-    int16_t *dRmap = nullptr;
+    uint32_t *lrKeys = nullptr;  // LR check: right-view winner keys per pixel (atomicMin target)
+    int16_t *dStar = nullptr;    // LR check: left winners (or -1) for lr_fixup
     void *vol = nullptr;
     size_t vol_bytes = 0;
     // timing
@@ -112,12 +113,14 @@ void free_buffers(dsx_handle *h) {
     (void)hipFree(h->dR);
     (void)hipFree(h->dFixed);
     (void)hipFree(h->dFloat);
-    (void)hipFree(h->dRmap);
+    (void)hipFree(h->lrKeys);
+    (void)hipFree(h->dStar);
     (void)hipFree(h->vol);
     h->dL = h->dR = nullptr;
     h->dFixed = nullptr;
     h->dFloat = nullptr;
-    h->dRmap = nullptr;
+    h->lrKeys = nullptr;
+    h->dStar = nullptr;
     h->vol = nullptr;
     h->vol_bytes = 0;
     h->cH = h->cW = h->cDp = h->cCostBytes = 0;
@@ -134,7 +137,10 @@ int ensure_buffers(dsx_handle *h, int H, int W, bool host_staging) {
         DSX_HIP(hipMalloc(&h->dFixed, n * 2));
         DSX_HIP(hipMalloc(&h->dFloat, n * 4));
     }
-    if (h->p.disp12_max_diff >= 0 && h->p.path == DSX_PATH_FUSED && !h->dRmap) DSX_HIP(hipMalloc(&h->dRmap, n * 2));
+    if (h->p.disp12_max_diff >= 0 && h->p.path == DSX_PATH_FUSED && !h->lrKeys) {
+        DSX_HIP(hipMalloc(&h->lrKeys, n * 4));
+        DSX_HIP(hipMalloc(&h->dStar, n * 2));
+    }
 
     if (h->p.path == DSX_PATH_VOLUME && !h->vol) {
         h->vol_bytes = n * h->g.Dp * cbytes;
@@ -244,26 +250,33 @@ int run(dsx_handle *h, const void *dL, const void *dR, int H, int W, int64_t str
     const int radius = h->p.block_size / 2;
     const bool ssd = h->p.cost == DSX_COST_SSD;
     if (h->p.path == DSX_PATH_FUSED) {
-        if (h->p.disp12_max_diff >= 0) {
-            int rc = run_right_pass(h, dL, dR, H, W, stride, h->dRmap, st);
-            if (rc) return rc;
-        }
+        const bool lr = h->p.disp12_max_diff >= 0;
         dsx::Bm2Args a = base_args(h, H, W, stride);
         a.side = dsx::SIDE_LEFT;
         a.ref = static_cast<const uint8_t *>(dL);
         a.src = static_cast<const uint8_t *>(dR);
-        a.dRmap = h->dRmap;
         a.out_fixed = static_cast<int16_t *>(outFixed);
         a.out_float = static_cast<float *>(outFloat);
-        // only strips meeting the valid band [m + D - 1, W - 1 + m] need a search (stereo_core.py:168 crops the rest)
-        const int xlo = std::max(0, h->p.min_disp + h->p.num_disp - 1);
-        const int xhi = std::min(W - 1, W - 1 + h->p.min_disp);
-        if (xlo > xhi) {
-            a.strip_begin = 0;
-            a.strip_count = 0;
+        if (lr) {
+            // the left pass also builds the right-view winners (every strip: a right pixel's
+            // diagonal starts left of the valid band); lr_fixup applies the check afterwards
+            DSX_HIP(hipMemsetAsync(h->lrKeys, 0xFF, (size_t)H * W * 4, st));
+            a.side = dsx::SIDE_LEFT_LR;
+            a.lr_keys = h->lrKeys;
+            a.dstar = h->dStar;
+            a.kshift = ssd ? h->g.DB : 16;
         } else {
-            a.strip_begin = xlo / dsx::kStripWidth;
-            a.strip_count = xhi / dsx::kStripWidth + 1 - a.strip_begin;
+            // only strips meeting the valid band [m + D - 1, W - 1 + m] need a search
+            // (stereo_core.py:168 crops the rest)
+            const int xlo = std::max(0, h->p.min_disp + h->p.num_disp - 1);
+            const int xhi = std::min(W - 1, W - 1 + h->p.min_disp);
+            if (xlo > xhi) {
+                a.strip_begin = 0;
+                a.strip_count = 0;
+            } else {
+                a.strip_begin = xlo / dsx::kStripWidth;
+                a.strip_count = xhi / dsx::kStripWidth + 1 - a.strip_begin;
+            }
         }
         uint64_t *tl = nullptr;
         const char *tlpath = getenv("DSX_TIMELINE");
@@ -271,6 +284,10 @@ int run(dsx_handle *h, const void *dL, const void *dR, int H, int W, int64_t str
         if (tl) DSX_HIP(hipMemsetAsync(tl, 0, 12 * 8 * 65536, st));
         a.timeline = tl;
         DSX_LAUNCH(h, "bm_pass_left", st, dsx::launch_bm2(radius, ssd, h->g.NW, a, st));
+        if (lr)
+            DSX_LAUNCH(h, "lr_fixup", st,
+                       dsx::launch_lr_fixup(h->dStar, h->lrKeys, H, W, h->p.min_disp, h->p.disp12_max_diff, a.kshift,
+                                            a.out_fixed, a.out_float, st));
         if (tl) {
             std::vector<uint64_t> host(12 * 65536);
             DSX_HIP(hipStreamSynchronize(st));
@@ -573,7 +590,7 @@ int dsx_workspace_bytes(dsx_handle *h, int64_t *bytes) {
     const int64_t n = (int64_t)h->cH * h->cW;
     int64_t b = 0;
     if (h->dL) b += n * (1 + 1 + 2 + 4);
-    if (h->dRmap) b += n * 2;
+    if (h->lrKeys) b += n * 6;
     b += (int64_t)h->vol_bytes;
     *bytes = b;
     return DSX_OK;

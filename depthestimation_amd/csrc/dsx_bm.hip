@@ -26,6 +26,8 @@
 //   side 0 (left)   : full epilogue -> int16 x16 + float disparity
 //   side 1 (right)  : argmin only   -> right-view winners dR (LR check input)
 //   side 2 (volume) : tile copied to the [H][W][Dp] cost volume (north-star "K1")
+//   side 3 (left+LR): side 0 plus right-view winners built along the tile's cost diagonals
+//                     (atomicMin across strips), checked afterwards by lr_fixup
 #include "dsx_internal.h"
 
 #include <cstdio>
@@ -60,8 +62,7 @@ struct Geo {
     static constexpr int NB = DSL / 8;        // 8-disparity blocks per epilogue lane
     static constexpr int REFB = rnd16(2 * (NC + 8));  // reference row as u16 pairs (broadcast reads)
     static constexpr int SLOT = SROW + REFB;
-    static constexpr int DRN = TX + Dp;  // staged dR values per row (LR check)
-    static constexpr int SMEM0 = 4 * SLOT + TX * PITCH + rnd16(2 * DRN * 2);
+    static constexpr int SMEM0 = 4 * SLOT + TX * PITCH;
     static constexpr int SMEM = SMEM0 > (2 * R + 1) * SLOT ? SMEM0 : (2 * R + 1) * SLOT;
 };
 
@@ -130,7 +131,6 @@ __device__ __forceinline__ void bm2_segment(const Bm2Args &a, uint8_t *smem, int
     constexpr int side = SIDE;
     typedef typename std::conditional<SSD, uint32_t, u16x2>::type acc_t;
     uint8_t *tile = smem + 4 * SLOT;
-    int16_t *dRs = reinterpret_cast<int16_t *>(smem + 4 * SLOT + TX * PITCH);  // 2 x G::DRN staged dR rows
 
     const int tid = threadIdx.x;
     const int wv = tid >> 6, ln = tid & 63;
@@ -142,7 +142,6 @@ __device__ __forceinline__ void bm2_segment(const Bm2Args &a, uint8_t *smem, int
     //                               right j = d + c,      pos = PB + j  (pos = x' + m + d)
     const int PB = side == 1 ? (x0 - R + m) : (x0 - R - m + NC - 1);
     const int sgn = side == 1 ? 1 : -1;
-    const int xr0 = x0 - m - (D - 1);  // first right-view column the LR check can reference
 
     // ---- raw row loads (registers) and their LDS stores ----
     // FAST: w0 = dword of 4 search bytes, w1 = the 5th byte; SLOW: w0..w3 = finished S words
@@ -217,23 +216,6 @@ __device__ __forceinline__ void bm2_segment(const Bm2Args &a, uint8_t *smem, int
             }
         }
         if (tid < NJ4) *reinterpret_cast<uint4 *>(smem + sl * SLOT + 16 * tid) = make_uint4(w0, w1, w2, w3);
-    };
-    // right-view winners of row r (LR check), staged next to the tile
-    constexpr int DRQ = (G::DRN + NT - 1) / NT;
-    auto ld_dr = [&](int r, uint32_t(&v)[DRQ]) __attribute__((always_inline)) {
-        const int16_t *row = a.dRmap + (long)clampi2(r, 0, H - 1) * W;
-#pragma unroll
-        for (int q = 0; q < DRQ; ++q) {
-            const int j = tid + q * NT;
-            v[q] = j < G::DRN ? (uint16_t)row[clampi2(xr0 + j, 0, W - 1)] : 0u;
-        }
-    };
-    auto st_dr = [&](int buf, const uint32_t(&v)[DRQ]) __attribute__((always_inline)) {
-#pragma unroll
-        for (int q = 0; q < DRQ; ++q) {
-            const int j = tid + q * NT;
-            if (j < G::DRN) dRs[buf * G::DRN + j] = (int16_t)v[q];
-        }
     };
     // reference pixels of slot sl, columns [c0, c0+8): one broadcast 16-B LDS read (u16 pairs)
     auto ref_chunk = [&](int sl, int c0, uint32_t(&rw)[4]) __attribute__((always_inline)) {
@@ -332,12 +314,6 @@ __device__ __forceinline__ void bm2_segment(const Bm2Args &a, uint8_t *smem, int
         if constexpr (SSD) *reinterpret_cast<uint32_t *>(tile + k * PITCH + d * 4) = padv;
         else *reinterpret_cast<uint16_t *>(tile + k * PITCH + d * 2) = (uint16_t)padv;
     }
-    // stage the first row's dR segment (left pass with LR check)
-    if (side == 0 && lr_on) {
-        uint32_t v[DRQ];
-        ld_dr(yb, v);
-        st_dr(yb & 1, v);
-    }
     block_sync<NW>();
 
     const bool edge = side == 1 && (x0 + m < 0 || x0 + TX - 1 + m + Dp - 1 > W - 1);
@@ -353,11 +329,9 @@ __device__ __forceinline__ void bm2_segment(const Bm2Args &a, uint8_t *smem, int
         const bool more = y + 1 < ye;
         // prefetch the next step's entering / leaving rows (+ its dR segment); lands during this step
         uint32_t pn0 = 0, pn1 = 0, pn2 = 0, pn3 = 0, pnr = 0, po0 = 0, po1 = 0, po2 = 0, po3 = 0, por = 0;
-        uint32_t pd[DRQ];
         if (more) {
             ld(y + 1 + R, pn0, pn1, pn2, pn3, pnr);
             ld(y - R, po0, po1, po2, po3, por);
-            if (side == 0 && lr_on) ld_dr(y + 1, pd);
         }
         if (y > yb) {
 #pragma unroll
@@ -394,7 +368,55 @@ __device__ __forceinline__ void bm2_segment(const Bm2Args &a, uint8_t *smem, int
             acc_t acc = cs[0];
 #pragma unroll
             for (int c = 1; c <= 2 * R; ++c) acc += cs[c];
-            if (lane_writes) {
+            if constexpr (side == 3) {
+                // Right-view winners along the tile's diagonals: C_R(xr, d) = C(xr + m + d, d), so
+                // right pixel xr collects keys (C << s | d) from (x, d) with x - m - d = xr.  Each
+                // lane keeps the running key minimum of the diagonal through its slot(s); moving to
+                // pixel k+1 a diagonal moves one disparity up (SAD: odd slot <- even slot, even slot
+                // <- odd slot of lane-1).  One DPP wave_ror:1 does that move and hands the diagonal
+                // leaving the wave's top disparity to lane 0, from where a wave_shr:1 FIFO (E)
+                // collects it; after the row every partial minimum is combined across strips with a
+                // global atomicMin.  Keys of disparities >= D (Dp padding) are forced to ~0 through
+                // the byte-permute selector (selector byte 13 = 0xFF).
+                const int ks = a.kshift;
+                const uint32_t selE = d0 < D ? 0x05040100u : 0x0D0D0D0Du;
+                const uint32_t selO = d0 + 1 < D ? 0x07060100u : 0x0D0D0D0Du;
+                const uint32_t dmE = d0 < D ? (uint32_t)d0 : 0xFFFFFFFFu;
+                const bool lane0 = ln == 0;
+                uint32_t Ae = 0xFFFFFFFFu, Ao = 0xFFFFFFFFu, E = 0xFFFFFFFFu;
+#pragma unroll
+                for (int k = 0; k < TX; ++k) {
+                    if (k > 0) acc = acc + cs[k + 2 * R] - cs[k - 1];
+                    if (lane_writes) {
+                        if constexpr (SSD) *reinterpret_cast<uint32_t *>(tb + k * PITCH) = acc;
+                        else *reinterpret_cast<uint32_t *>(tb + k * PITCH) = as1(acc);
+                    }
+                    if (x0 + k < W) {
+                        if constexpr (SSD) {
+                            Ae = umin2(Ae, (acc << ks) | dmE);
+                        } else {  // (C << 16) | d by byte permute
+                            Ae = umin2(Ae, __builtin_amdgcn_perm(as1(acc), (uint32_t)d0, selE));
+                            Ao = umin2(Ao, __builtin_amdgcn_perm(as1(acc), (uint32_t)(d0 + 1), selO));
+                        }
+                    }
+                    if (k < TX - 1) {
+                        const uint32_t top = SSD ? Ae : Ao;
+                        const uint32_t F = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)top, 0x13C, 0xF, 0xF, false);  // wave_ror:1
+                        E = (uint32_t)__builtin_amdgcn_update_dpp((int)F, (int)E, 0x138, 0xF, 0xF, false);        // wave_shr:1, lane 0 <- F
+                        if constexpr (!SSD) Ao = Ae;
+                        Ae = lane0 ? 0xFFFFFFFFu : F;
+                    }
+                }
+                uint32_t *krow = a.lr_keys + (long)y * W;
+                const int dtop = (wv + 1) * G::LDW - 1;            // disparity of the wave's top slot
+                const int xe = x0 + (TX - 2 - ln) - m - dtop;       // E lane j: exit of pixel TX-2-j
+                if (ln < TX - 1 && E != 0xFFFFFFFFu && xe >= 0 && xe < W) atomicMin(krow + xe, E);
+                const int xa = x0 + TX - 1 - m - d0;
+                if (Ae != 0xFFFFFFFFu && xa >= 0 && xa < W) atomicMin(krow + xa, Ae);
+                if constexpr (!SSD) {
+                    if (Ao != 0xFFFFFFFFu && xa - 1 >= 0 && xa - 1 < W) atomicMin(krow + xa - 1, Ao);
+                }
+            } else if (lane_writes) {
 #pragma unroll
                 for (int k = 0; k < TX; ++k) {
                     if (k > 0) acc = acc + cs[k + 2 * R] - cs[k - 1];
@@ -525,12 +547,8 @@ __device__ __forceinline__ void bm2_segment(const Bm2Args &a, uint8_t *smem, int
                     f += div_trunc_small((cm - cp) * 16 + den, 2 * den);
                     if (a.float_mode == 1) pf = (float)(m + b) + (float)(cm - cp) / (float)(2 * den);
                 }
-                if (lr_on && valid) {
-                    const int dr = dRs[(y & 1) * G::DRN + (x - m - b - xr0)];
-                    const int df = dr - b;
-                    if (df > a.lr || df < -a.lr) valid = false;
-                }
                 if (h == 0 && x < W) {
+                    if (lr_on) a.dstar[o] = valid ? (int16_t)b : (int16_t)-1;  // LR check: lr_fixup
                     const int16_t fx = valid ? (int16_t)(m * 16 + f) : (int16_t)((m - 1) * 16);
                     if (a.out_fixed) a.out_fixed[o] = fx;
                     if (a.out_float) a.out_float[o] = a.float_mode == 0 ? (float)fx * 0.0625f : (valid ? pf : (float)(m - 1));
@@ -541,7 +559,6 @@ __device__ __forceinline__ void bm2_segment(const Bm2Args &a, uint8_t *smem, int
         if (more) {
             st(par ^ 2, pn0, pn1, pn2, pn3, pnr);
             st((par ^ 2) + 1, po0, po1, po2, po3, por);
-            if (side == 0 && lr_on) st_dr((y + 1) & 1, pd);
         }
         DSX_STAMP(6);
         block_sync<NW>();
@@ -566,7 +583,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(3))) vo
 #endif
 
     // ---- left pass: columns of strips that lie entirely in the invalid band ----
-    if (side == 0 && (a.out_fixed || a.out_float)) {
+    if ((side == 0 || side == 3) && (a.out_fixed || a.out_float)) {
         const int xa = a.strip_begin * TX, xb = min(W, (a.strip_begin + a.strip_count) * TX);
         const int nin = xa + (W - xb);
         const long total = (long)nin * H;
@@ -597,7 +614,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(3))) vo
         lin0 = b * T / NG;
         lin1 = (b + 1) * T / NG;
     }
-    const bool lr_on = side == 0 && a.lr >= 0 && a.dRmap != nullptr;
+    constexpr bool lr_on = SIDE == 3;  // left pass that also builds the right-view winners
     for (long it = lin0; it < lin1;) {
         const int s = a.strip_begin + (int)(it / H);
         const int yb = (int)(it % H);
@@ -680,6 +697,7 @@ static hipError_t launch_bm2_one(const Bm2Args &a, hipStream_t st) {
     switch (a.side) {
         case 0: return launch_bm2_side<R, SSD, NW, 0>(a, st);
         case 1: return launch_bm2_side<R, SSD, NW, 1>(a, st);
+        case 3: return launch_bm2_side<R, SSD, NW, 3>(a, st);
         default: return launch_bm2_side<R, SSD, NW, 2>(a, st);
     }
 }

@@ -5,7 +5,7 @@
 
 namespace dsx {
 
-enum Side : int { SIDE_LEFT = 0, SIDE_RIGHT = 1, SIDE_VOLUME = 2 };
+enum Side : int { SIDE_LEFT = 0, SIDE_RIGHT = 1, SIDE_VOLUME = 2, SIDE_LEFT_LR = 3 };
 
 constexpr int kVolThreads = 256;    // K2 (volume WTA) block size
 
@@ -25,12 +25,14 @@ struct Bm2Args {
     int H, W;
     int m;               // min_disp
     int D;               // num_disp (padded internally to the kernel's Dp)
-    int side;            // 0 left (full epilogue), 1 right (dR map), 2 volume (K1 store)
+    int side;            // 0 left (full epilogue), 1 right (dR map), 2 volume (K1 store), 3 left + LR keys
     int uniq, lr, subpix, float_mode;
     uint32_t padv;       // cost stored for disparities outside [0, D) / outside the image
     int strip_begin, strip_count;  // 32-column strips forming the work space
     int grid_override;   // >0: force the persistent grid size (tests)
-    const int16_t *dRmap;  // right-view winners (left pass with LR)
+    uint32_t *lr_keys;     // left pass with LR: per-pixel right-view winner keys (C << kshift | d),
+    int kshift;            //   filled by atomicMin (memset to ~0 first)
+    int16_t *dstar;        // left pass with LR: winning d (or -1) for lr_fixup
     int16_t *out_fixed;    // left pass outputs (either may be null)
     float *out_float;
     int16_t *out_dR;       // right pass output
@@ -66,6 +68,9 @@ __device__ __forceinline__ int div_trunc_small(int num, int den2) {
 // nw = waves per block: SAD Dp = 128*nw (nw in {1,2,4}), SSD Dp = 64*nw (nw in {1,2,4,8}).
 hipError_t launch_bm2(int radius, bool ssd, int nw, const Bm2Args &a, hipStream_t st);
 hipError_t launch_volume_wta(int TX, bool ssd, const VolArgs &a, hipStream_t st);
+// LR check after the left pass: invalidate x where |dR(x - m - d*) - d*| > lr.
+hipError_t launch_lr_fixup(const int16_t *dstar, const uint32_t *keys, int H, int W, int m, int lr, int kshift,
+                           int16_t *out_fixed, float *out_float, hipStream_t st);
 
 size_t volume_smem_bytes(int TX, bool ssd, int Dp, int TPP, int W);
 

@@ -14,6 +14,8 @@
 //                  via right-view winners built with LDS ds_min_u32 scatters.
 #include "dsx_internal.h"
 
+#include <algorithm>
+
 #include <type_traits>
 
 namespace dsx {
@@ -188,6 +190,37 @@ __global__ __launch_bounds__(kVolThreads) void vol_wta(VolArgs a) {
         if (a.out_fixed) a.out_fixed[o] = fx;
         if (a.out_float) a.out_float[o] = a.float_mode == 0 ? (float)fx * 0.0625f : (valid ? rowF[x] : (float)(m - 1));
     }
+}
+
+// ---------------------------------------------------------------------------------------
+// lr_fixup: the left-right check of the fused path (stereo_core.py:69 disp12MaxDiff) once the
+// left pass has built the right-view winners by atomicMin over its cost diagonals.
+// ---------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void lr_fixup(const int16_t *__restrict__ dstar, const uint32_t *__restrict__ keys,
+                                               int H, int W, int m, int lr, int kshift, int16_t *out_fixed,
+                                               float *out_float) {
+    const int64_t n = (int64_t)H * W;
+    const uint32_t mask = (1u << kshift) - 1u;
+    for (int64_t p = (int64_t)blockIdx.x * 256 + threadIdx.x; p < n; p += (int64_t)gridDim.x * 256) {
+        const int b = dstar[p];
+        if (b < 0) continue;
+        const int x = (int)(p % W);
+        const int xr = x - m - b;  // in [0, W-1] for every valid-band pixel
+        const int dr = (int)(keys[p - x + xr] & mask);
+        const int df = dr - b;
+        if (df > lr || df < -lr) {
+            if (out_fixed) out_fixed[p] = (int16_t)((m - 1) * 16);
+            if (out_float) out_float[p] = (float)(m - 1);
+        }
+    }
+}
+
+hipError_t launch_lr_fixup(const int16_t *dstar, const uint32_t *keys, int H, int W, int m, int lr, int kshift,
+                           int16_t *out_fixed, float *out_float, hipStream_t st) {
+    const int64_t n = (int64_t)H * W;
+    const int grid = (int)std::min<int64_t>((n + 255) / 256, 8192);
+    hipLaunchKernelGGL(lr_fixup, dim3(grid), dim3(256), 0, st, dstar, keys, H, W, m, lr, kshift, out_fixed, out_float);
+    return hipGetLastError();
 }
 
 // ---------------------------------------------------------------------------------------
