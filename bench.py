@@ -108,6 +108,8 @@ def main():
     ap.add_argument("--check", action="store_true", help="verify one frame against the C oracle")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline sample length")
     ap.add_argument("--grid-blocks", type=int, default=0, help="force the persistent grid size (tuning)")
+    ap.add_argument("--batch", type=int, default=1, help="frame pairs per GPU per step (one launch)")
+    ap.add_argument("--no-batched", action="store_true", help="skip the secondary batched measurement")
     args = ap.parse_args()
 
     import torch
@@ -130,17 +132,23 @@ def main():
     calib = sharding.broadcast_calibration(calibration_params() if rank == 0 else None, device=dev)
     assert calib["image_width"] == 2964, "calibration broadcast failed"
 
-    # frame-sharded synthetic stream: global frame g = rank + ws * i
-    frames = []
-    host_first = None
-    for i in range(args.frames):
+    # frame-sharded synthetic stream: global frame g = rank + ws * i; a step is one launch over
+    # `batch` resident frame pairs (batch 1: one compute_device call per step)
+    B = max(1, args.batch)
+    nres = max(args.frames, B)
+    hostL, hostR = [], []
+    for i in range(nres):
         g = rank + ws * i
         L, R, _ = stereo_pair(H, W, 0, cfg["num_disp"], seed=1234 + g)
-        if i == 0:
-            host_first = (L, R)
-        frames.append((torch.from_numpy(L).to(dev), torch.from_numpy(R).to(dev)))
-    out_fixed = torch.empty((H, W), dtype=torch.int16, device=dev)
-    out_float = torch.empty((H, W), dtype=torch.float32, device=dev)
+        hostL.append(L)
+        hostR.append(R)
+    host_first = (hostL[0], hostR[0])
+    allL = torch.from_numpy(np.stack(hostL)).to(dev)
+    allR = torch.from_numpy(np.stack(hostR)).to(dev)
+    groups = [(allL[i:i + B], allR[i:i + B]) for i in range(0, nres - B + 1, B)]
+    frames = [(allL[i], allR[i]) for i in range(nres)]
+    out_fixed = torch.empty((B, H, W), dtype=torch.int16, device=dev)
+    out_float = torch.empty((B, H, W), dtype=torch.float32, device=dev)
 
     kw = dict(min_disp=0, num_disp=cfg["num_disp"], block_size=cfg["block_size"], cost=cfg["cost"],
               uniqueness_ratio=cfg["uniqueness_ratio"], disp12_max_diff=cfg["disp12_max_diff"], subpixel=True)
@@ -148,8 +156,12 @@ def main():
     stream = torch.cuda.current_stream(dev)
 
     def step(i):
-        fl, fr = frames[i % len(frames)]
-        matcher.compute_device(fl, fr, out_fixed=out_fixed, out_float=out_float, stream=stream)
+        if B == 1:
+            fl, fr = frames[i % len(frames)]
+            matcher.compute_device(fl, fr, out_fixed=out_fixed[0], out_float=out_float[0], stream=stream)
+        else:
+            gl, gr = groups[i % len(groups)]
+            matcher.compute_batch_device(gl, gr, out_fixed=out_fixed, out_float=out_float, stream=stream)
 
     for i in range(args.warmup):
         step(i)
@@ -176,17 +188,17 @@ def main():
         ref = CRef()(host_first[0], host_first[1], nthreads=16, **kw)
         step(0)
         torch.cuda.synchronize(dev)
-        assert np.array_equal(out_fixed.cpu().numpy(), ref["fixed"]), "bench frame differs from oracle"
+        assert np.array_equal(out_fixed[0].cpu().numpy(), ref["fixed"]), "bench frame differs from oracle"
 
     result = None
     if rank == 0:
-        px_total = H * W * args.steps * ws
+        px_total = H * W * B * args.steps * ws
         value = px_total / elapsed / 1e6
         ab = algorithmic_bytes(cfg)
         # dominant kernel of this path (largest total time)
         dom = max(ktimes.items(), key=lambda kv: kv[1][0] * kv[1][1])
         dom_name, (dom_ms, dom_n) = dom
-        per_launch_bytes = ab["frame"]
+        per_launch_bytes = ab["frame"] * (B if dom_name == "bm_pass_left" else 1)  # one launch covers B frames
         achieved = per_launch_bytes / (dom_ms * 1e-3) / 1e9
         roofline = {
             "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -211,23 +223,43 @@ def main():
             "config": {"workload": cfg["desc"], "H": H, "W": W, "num_disp": cfg["num_disp"],
                        "block_size": cfg["block_size"], "cost": cfg["cost"],
                        "uniqueness_ratio": cfg["uniqueness_ratio"], "disp12_max_diff": cfg["disp12_max_diff"],
-                       "subpixel": True, "path": args.path, "frames_per_step_per_gpu": 1,
+                       "subpixel": True, "path": args.path, "frames_per_step_per_gpu": B,
                        "parallelism": f"frame-sharded x{ws} (RCCL calibration broadcast, no per-frame collectives)"},
             "roofline": roofline,
         }
+
+        if B == 1 and args.path == "fused" and not args.no_batched:
+            # secondary figure: the same workload with 4 frame pairs per launch (video streams)
+            Bb = 4
+            gL = allL[:Bb] if allL.shape[0] >= Bb else allL.repeat(Bb, 1, 1)[:Bb]
+            gR = allR[:Bb] if allR.shape[0] >= Bb else allR.repeat(Bb, 1, 1)[:Bb]
+            bf = torch.empty((Bb, H, W), dtype=torch.int16, device=dev)
+            bfl = torch.empty((Bb, H, W), dtype=torch.float32, device=dev)
+            for _ in range(3):
+                matcher.compute_batch_device(gL, gR, out_fixed=bf, out_float=bfl, stream=stream)
+            torch.cuda.synchronize(dev)
+            nb = 20
+            t1 = time.perf_counter()
+            for _ in range(nb):
+                matcher.compute_batch_device(gL, gR, out_fixed=bf, out_float=bfl, stream=stream)
+            torch.cuda.synchronize(dev)
+            bt = time.perf_counter() - t1
+            result["batched"] = {"frames_per_launch": Bb, "value": round(H * W * Bb * nb / bt / 1e6, 1),
+                                 "unit": "Mpix/s", "ms_per_frame": round(bt / (nb * Bb) * 1e3, 5),
+                                 "note": "secondary: dsx_compute_batch_device over 4 resident pairs per launch"}
 
         if not args.no_volume_roofline and args.path == "fused":
             vm = HipBlockMatcher(device=local, path="volume", timing=True, **kw)
             for i in range(5):
                 fl, fr = frames[i % len(frames)]
-                vm.compute_device(fl, fr, out_fixed=out_fixed, out_float=out_float, stream=stream)
+                vm.compute_device(fl, fr, out_fixed=out_fixed[0], out_float=out_float[0], stream=stream)
             torch.cuda.synchronize(dev)
             vm.reset_times()
             t1 = time.perf_counter()
             nv = 20
             for i in range(nv):
                 fl, fr = frames[i % len(frames)]
-                vm.compute_device(fl, fr, out_fixed=out_fixed, out_float=out_float, stream=stream)
+                vm.compute_device(fl, fr, out_fixed=out_fixed[0], out_float=out_float[0], stream=stream)
             torch.cuda.synchronize(dev)
             vt = time.perf_counter() - t1
             kt = vm.kernel_times()

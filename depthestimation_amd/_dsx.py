@@ -27,7 +27,7 @@ PATH = {"fused": 0, "volume": 1}
 # Every symbol include/dsx.h declares (checked by tests/test_abi.py against the header).
 EXPORTS = (
     "dsx_version", "dsx_device_count", "dsx_default_params", "dsx_check_params", "dsx_create",
-    "dsx_set_params", "dsx_compute_host", "dsx_compute_device", "dsx_right_map_device",
+    "dsx_set_params", "dsx_compute_host", "dsx_compute_device", "dsx_compute_batch_device", "dsx_right_map_device",
     "dsx_postprocess_fast_device", "dsx_postprocess_workspace_bytes", "dsx_postprocess_full_device",
     "dsx_rectify_device",
     "dsx_kernel_times", "dsx_reset_times", "dsx_workspace_bytes", "dsx_destroy", "dsx_last_error",
@@ -67,6 +67,7 @@ def _bind(lib):
         "dsx_set_params": (ctypes.c_int, [vp, P]),
         "dsx_compute_host": (ctypes.c_int, [vp, vp, vp, i32, i32, i64, vp, vp]),
         "dsx_compute_device": (ctypes.c_int, [vp, vp, vp, i32, i32, i64, vp, vp, vp]),
+        "dsx_compute_batch_device": (ctypes.c_int, [vp, i32, vp, vp, i64, i32, i32, i64, vp, vp, vp]),
         "dsx_right_map_device": (ctypes.c_int, [vp, vp, vp, i32, i32, i64, vp, vp]),
         "dsx_postprocess_workspace_bytes": (ctypes.c_size_t, [i32, i32, i32]),
         "dsx_postprocess_full_device": (ctypes.c_int, [vp, i32, i32, i64, i32, i32, ctypes.c_double, i32,

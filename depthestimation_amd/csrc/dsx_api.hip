@@ -91,6 +91,7 @@ struct dsx_handle {
     hipStream_t stream = nullptr;  // for dsx_compute_host
     // buffer cache keyed by (H, W, geometry); single entry like RectificationCache (rectify.py:49-50)
     int cH = 0, cW = 0, cDp = 0, cCostBytes = 0;
+    int lrFrames = 0;  // frames the LR buffers hold
     uint8_t *dL = nullptr, *dR = nullptr;
     int16_t *dFixed = nullptr;
     float *dFloat = nullptr;
@@ -124,9 +125,10 @@ void free_buffers(dsx_handle *h) {
     h->vol = nullptr;
     h->vol_bytes = 0;
     h->cH = h->cW = h->cDp = h->cCostBytes = 0;
+    h->lrFrames = 0;
 }
 
-int ensure_buffers(dsx_handle *h, int H, int W, bool host_staging) {
+int ensure_buffers(dsx_handle *h, int H, int W, bool host_staging, int nframes = 1) {
     const int cbytes = h->p.cost == DSX_COST_SSD ? 4 : 2;
     if (h->cH != H || h->cW != W || h->cDp != h->g.Dp || h->cCostBytes != cbytes) free_buffers(h);
     const size_t n = (size_t)H * W;
@@ -137,9 +139,16 @@ int ensure_buffers(dsx_handle *h, int H, int W, bool host_staging) {
         DSX_HIP(hipMalloc(&h->dFixed, n * 2));
         DSX_HIP(hipMalloc(&h->dFloat, n * 4));
     }
-    if (h->p.disp12_max_diff >= 0 && h->p.path == DSX_PATH_FUSED && !h->lrKeys) {
-        DSX_HIP(hipMalloc(&h->lrKeys, n * 4));
-        DSX_HIP(hipMalloc(&h->dStar, n * 2));
+    if (h->p.disp12_max_diff >= 0 && h->p.path == DSX_PATH_FUSED && h->lrFrames < nframes) {
+        (void)hipFree(h->lrKeys);
+        (void)hipFree(h->dStar);
+        h->lrKeys = nullptr;
+        h->dStar = nullptr;
+        h->lrFrames = 0;
+        DSX_HIP(hipMalloc(&h->lrKeys, n * nframes * 4));
+        DSX_HIP(hipMalloc(&h->dStar, n * nframes * 2));
+        DSX_HIP(hipMemset(h->lrKeys, 0xFF, n * nframes * 4));  // lr_fixup restores ~0 after every frame
+        h->lrFrames = nframes;
     }
 
     if (h->p.path == DSX_PATH_VOLUME && !h->vol) {
@@ -215,6 +224,8 @@ dsx::Bm2Args base_args(dsx_handle *h, int H, int W, int64_t stride) {
     a.strip_begin = 0;
     a.strip_count = (W + dsx::kStripWidth - 1) / dsx::kStripWidth;
     a.grid_override = h->p.grid_blocks;
+    a.nframes = 1;
+    a.frame_stride = 0;
     return a;
 }
 
@@ -245,8 +256,9 @@ int run_right_pass(dsx_handle *h, const void *dL, const void *dR, int H, int W, 
     return DSX_OK;
 }
 
+// nframes frames: inputs frame_stride bytes apart, outputs (and LR buffers) H * W elements apart
 int run(dsx_handle *h, const void *dL, const void *dR, int H, int W, int64_t stride, void *outFixed, void *outFloat,
-        hipStream_t st) {
+        hipStream_t st, int nframes = 1, int64_t frame_stride = 0) {
     const int radius = h->p.block_size / 2;
     const bool ssd = h->p.cost == DSX_COST_SSD;
     if (h->p.path == DSX_PATH_FUSED) {
@@ -257,10 +269,11 @@ int run(dsx_handle *h, const void *dL, const void *dR, int H, int W, int64_t str
         a.src = static_cast<const uint8_t *>(dR);
         a.out_fixed = static_cast<int16_t *>(outFixed);
         a.out_float = static_cast<float *>(outFloat);
+        a.nframes = nframes;
+        a.frame_stride = frame_stride;
         if (lr) {
             // the left pass also builds the right-view winners (every strip: a right pixel's
             // diagonal starts left of the valid band); lr_fixup applies the check afterwards
-            DSX_HIP(hipMemsetAsync(h->lrKeys, 0xFF, (size_t)H * W * 4, st));
             a.side = dsx::SIDE_LEFT_LR;
             a.lr_keys = h->lrKeys;
             a.dstar = h->dStar;
@@ -286,7 +299,7 @@ int run(dsx_handle *h, const void *dL, const void *dR, int H, int W, int64_t str
         DSX_LAUNCH(h, "bm_pass_left", st, dsx::launch_bm2(radius, ssd, h->g.NW, a, st));
         if (lr)
             DSX_LAUNCH(h, "lr_fixup", st,
-                       dsx::launch_lr_fixup(h->dStar, h->lrKeys, H, W, h->p.min_disp, h->p.disp12_max_diff, a.kshift,
+                       dsx::launch_lr_fixup(h->dStar, h->lrKeys, H * nframes, W, h->p.min_disp, h->p.disp12_max_diff, a.kshift,
                                             a.out_fixed, a.out_float, st));
         if (tl) {
             std::vector<uint64_t> host(12 * 65536);
@@ -300,30 +313,34 @@ int run(dsx_handle *h, const void *dL, const void *dR, int H, int W, int64_t str
             (void)hipFree(tl);
         }
     } else {
-        dsx::Bm2Args a = base_args(h, H, W, stride);
-        a.side = dsx::SIDE_VOLUME;
-        a.ref = static_cast<const uint8_t *>(dL);
-        a.src = static_cast<const uint8_t *>(dR);
-        a.vol = h->vol;
-        DSX_LAUNCH(h, "cost_volume", st, dsx::launch_bm2(radius, ssd, h->g.NW, a, st));
-        dsx::VolArgs v{};
-        v.vol = h->vol;
-        v.H = H;
-        v.W = W;
-        v.m = h->p.min_disp;
-        v.D = h->p.num_disp;
-        v.Dp = h->g.Dp;
-        v.DB = h->g.DB;
-        v.TPP = h->g.TPP;
-        v.uniq = h->p.uniqueness_ratio;
-        v.lr = h->p.disp12_max_diff;
-        v.subpix = h->p.subpixel;
-        v.float_mode = h->p.float_mode;
-        v.out_fixed = static_cast<int16_t *>(outFixed);
-        v.out_float = static_cast<float *>(outFloat);
-        if (dsx::volume_smem_bytes(h->g.TX, ssd, h->g.Dp, h->g.TPP, W) > 160 * 1024)
-            return fail(DSX_EINVAL, "image too wide for the volume path's row kernel");
-        DSX_LAUNCH(h, "volume_wta", st, dsx::launch_volume_wta(h->g.TX, ssd, v, st));
+        // volume path: one K1 + K2 pair per frame (the volume buffer holds one frame)
+        for (int f = 0; f < nframes; ++f) {
+            const size_t fo = (size_t)f * H * W;
+            dsx::Bm2Args a = base_args(h, H, W, stride);
+            a.side = dsx::SIDE_VOLUME;
+            a.ref = static_cast<const uint8_t *>(dL) + f * frame_stride;
+            a.src = static_cast<const uint8_t *>(dR) + f * frame_stride;
+            a.vol = h->vol;
+            DSX_LAUNCH(h, "cost_volume", st, dsx::launch_bm2(radius, ssd, h->g.NW, a, st));
+            dsx::VolArgs v{};
+            v.vol = h->vol;
+            v.H = H;
+            v.W = W;
+            v.m = h->p.min_disp;
+            v.D = h->p.num_disp;
+            v.Dp = h->g.Dp;
+            v.DB = h->g.DB;
+            v.TPP = h->g.TPP;
+            v.uniq = h->p.uniqueness_ratio;
+            v.lr = h->p.disp12_max_diff;
+            v.subpix = h->p.subpixel;
+            v.float_mode = h->p.float_mode;
+            v.out_fixed = outFixed ? static_cast<int16_t *>(outFixed) + fo : nullptr;
+            v.out_float = outFloat ? static_cast<float *>(outFloat) + fo : nullptr;
+            if (dsx::volume_smem_bytes(h->g.TX, ssd, h->g.Dp, h->g.TPP, W) > 160 * 1024)
+                return fail(DSX_EINVAL, "image too wide for the volume path's row kernel");
+            DSX_LAUNCH(h, "volume_wta", st, dsx::launch_volume_wta(h->g.TX, ssd, v, st));
+        }
     }
     return DSX_OK;
 }
@@ -515,6 +532,25 @@ int dsx_rectify_device(const void *d_img, int32_t Hs, int32_t Ws, int64_t stride
     return DSX_OK;
 }
 
+int dsx_compute_batch_device(dsx_handle *h, int32_t nframes, const void *dL, const void *dR, int64_t frame_stride_bytes,
+                             int32_t H, int32_t W, int64_t stride_bytes, void *d_out_fixed, void *d_out_float,
+                             void *hip_stream) {
+    g_err.clear();
+    if (!h) return fail(DSX_EINVAL, "handle is NULL");
+    if (!dL || !dR) return fail(DSX_EINVAL, "input pointers are NULL");
+    if (!d_out_fixed && !d_out_float) return fail(DSX_EINVAL, "at least one output is required");
+    if (nframes < 1) return fail(DSX_EINVAL, "nframes must be >= 1");
+    int rc = check_shape(H, W, stride_bytes);
+    if (rc) return rc;
+    if (nframes > 1 && frame_stride_bytes < (int64_t)(H - 1) * stride_bytes + W)
+        return fail(DSX_EINVAL, "frame_stride_bytes smaller than one frame");
+    DSX_HIP(hipSetDevice(h->device));
+    rc = ensure_buffers(h, H, W, false, nframes);
+    if (rc) return rc;
+    return run(h, dL, dR, H, W, stride_bytes, d_out_fixed, d_out_float, static_cast<hipStream_t>(hip_stream), nframes,
+               frame_stride_bytes);
+}
+
 int dsx_right_map_device(dsx_handle *h, const void *dL, const void *dR, int32_t H, int32_t W, int64_t stride_bytes,
                          void *d_out_dR, void *hip_stream) {
     g_err.clear();
@@ -590,7 +626,7 @@ int dsx_workspace_bytes(dsx_handle *h, int64_t *bytes) {
     const int64_t n = (int64_t)h->cH * h->cW;
     int64_t b = 0;
     if (h->dL) b += n * (1 + 1 + 2 + 4);
-    if (h->lrKeys) b += n * 6;
+    if (h->lrKeys) b += n * 6 * h->lrFrames;
     b += (int64_t)h->vol_bytes;
     *bytes = b;
     return DSX_OK;

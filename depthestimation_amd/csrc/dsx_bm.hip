@@ -119,7 +119,8 @@ typedef const __attribute__((address_space(4))) uint32_t cu32;
 // byte loads. All per-row state is in plain registers (no structs / arrays with runtime
 // indices, which hipcc would demote to scratch).
 template <int R, bool SSD, int NW, int SIDE, bool FAST>
-__device__ __forceinline__ void bm2_segment(const Bm2Args &a, uint8_t *smem, int x0, int yb, int ye, bool lr_on
+__device__ __forceinline__ void bm2_segment(const Bm2Args &a, uint8_t *smem, int x0, int yb, int ye, long fin, long fout,
+                                            bool lr_on
 #ifdef DSX_STAMPS
                                             , uint64_t (&ph)[8], uint64_t &t_prev, uint64_t &nsteps
 #endif
@@ -148,8 +149,8 @@ __device__ __forceinline__ void bm2_segment(const Bm2Args &a, uint8_t *smem, int
     constexpr int NC4 = (NC + 3) / 4;
     auto ld = [&](int r, uint32_t &w0, uint32_t &w1, uint32_t &w2, uint32_t &w3, uint32_t &rf) __attribute__((always_inline)) {
         const int yy = clampi2(r, 0, H - 1);
-        const uint8_t *srow = a.src + (long)yy * stride;
-        const uint8_t *rrow = a.ref + (long)yy * stride;
+        const uint8_t *srow = a.src + fin + (long)yy * stride;
+        const uint8_t *rrow = a.ref + fin + (long)yy * stride;
         if constexpr (FAST) {
             rf = tid < NC4 ? *reinterpret_cast<const uint32_t *>(rrow + x0 - R + 4 * tid) : 0u;
         } else {
@@ -407,7 +408,7 @@ __device__ __forceinline__ void bm2_segment(const Bm2Args &a, uint8_t *smem, int
                         Ae = lane0 ? 0xFFFFFFFFu : F;
                     }
                 }
-                uint32_t *krow = a.lr_keys + (long)y * W;
+                uint32_t *krow = a.lr_keys + fout + (long)y * W;
                 const int dtop = (wv + 1) * G::LDW - 1;            // disparity of the wave's top slot
                 const int xe = x0 + (TX - 2 - ln) - m - dtop;       // E lane j: exit of pixel TX-2-j
                 if (ln < TX - 1 && E != 0xFFFFFFFFu && xe >= 0 && xe < W) atomicMin(krow + xe, E);
@@ -451,7 +452,7 @@ __device__ __forceinline__ void bm2_segment(const Bm2Args &a, uint8_t *smem, int
                 const int x = x0 + k;
                 if (x < W) {
                     const uint4 v = *reinterpret_cast<const uint4 *>(tile + k * PITCH + off);
-                    *reinterpret_cast<uint4 *>(reinterpret_cast<uint8_t *>(a.vol) + ((size_t)y * W + x) * (Dp * CB) + off) = v;
+                    *reinterpret_cast<uint4 *>(reinterpret_cast<uint8_t *>(a.vol) + ((size_t)fout + (size_t)y * W + x) * (Dp * CB) + off) = v;
                 }
             }
         } else {
@@ -499,7 +500,7 @@ __device__ __forceinline__ void bm2_segment(const Bm2Args &a, uint8_t *smem, int
                 dl = (uint32_t)(h * DSL + 8 * bsel + e);
             }
             const int b = (int)gmin<TPP>(dl);
-            const long o = (long)y * W + x;
+            const long o = fout + (long)y * W + x;
             if constexpr (side == 1) {
                 if (h == 0 && x < W) a.out_dR[o] = cb == padv ? (int16_t)-1 : (int16_t)b;
             } else {
@@ -586,10 +587,11 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(3))) vo
     if ((side == 0 || side == 3) && (a.out_fixed || a.out_float)) {
         const int xa = a.strip_begin * TX, xb = min(W, (a.strip_begin + a.strip_count) * TX);
         const int nin = xa + (W - xb);
-        const long total = (long)nin * H;
+        const long total = (long)nin * H * a.nframes;  // frames are H-row slabs of one tall output
         const int16_t fi = (int16_t)((m - 1) * 16);
         for (long q = (long)blockIdx.x * NT + tid; q < total; q += (long)gridDim.x * NT) {
-            const int y = (int)(q / nin), c = (int)(q - (long)y * nin);
+            const long y = q / nin;
+            const int c = (int)(q - y * nin);
             const int x = c < xa ? c : xb + (c - xa);
             const long o = (long)y * W + x;
             if (a.out_fixed) a.out_fixed[o] = fi;
@@ -597,10 +599,10 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(3))) vo
         }
     }
 
-    // ---- work partition: with at least one block per strip, every block owns ONE contiguous
-    // run of rows of ONE strip (balanced to +-1 block per strip); otherwise an even split of
-    // the linearised (strip, row) space.
-    const int NS = a.strip_count;
+    // ---- work partition over the (frame, strip, row) space: with at least one block per
+    // (frame, strip), every block owns ONE contiguous run of rows of ONE strip of one frame
+    // (balanced to +-1 block per strip); otherwise an even split of the linearised space.
+    const int NS = a.strip_count * a.nframes;
     const long NG = gridDim.x, b = blockIdx.x;
     long lin0, lin1;
     if (NG >= NS && NS > 0) {
@@ -616,7 +618,10 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(3))) vo
     }
     constexpr bool lr_on = SIDE == 3;  // left pass that also builds the right-view winners
     for (long it = lin0; it < lin1;) {
-        const int s = a.strip_begin + (int)(it / H);
+        const int sidx = (int)(it / H);
+        const int f = sidx / a.strip_count;
+        const int s = a.strip_begin + (sidx - f * a.strip_count);
+        const long fin = (long)f * a.frame_stride, fout = (long)f * H * W;
         const int yb = (int)(it % H);
         const int ye = (int)min((long)H, (long)yb + (lin1 - it));
         it += ye - yb;
@@ -626,13 +631,13 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(3))) vo
         const bool fast = (side == 1 ? (PB >= 0 && PB + 4 * NJ4 <= W - 1) : (PB - 4 * NJ4 >= 0 && PB <= W - 1)) &&
                           x0 - R >= 0 && x0 - R + 4 * ((NC + 3) / 4) - 1 <= W - 1;
         if (fast)
-            bm2_segment<R, SSD, NW, SIDE, true>(a, smem, x0, yb, ye, lr_on
+            bm2_segment<R, SSD, NW, SIDE, true>(a, smem, x0, yb, ye, fin, fout, lr_on
 #ifdef DSX_STAMPS
                                                 , ph, t_prev, nsteps
 #endif
             );
         else
-            bm2_segment<R, SSD, NW, SIDE, false>(a, smem, x0, yb, ye, lr_on
+            bm2_segment<R, SSD, NW, SIDE, false>(a, smem, x0, yb, ye, fin, fout, lr_on
 #ifdef DSX_STAMPS
                                                  , ph, t_prev, nsteps
 #endif
@@ -680,7 +685,7 @@ static hipError_t launch_bm2_side(const Bm2Args &a, hipStream_t st) {
         blocks_per_cu[dev] = nbr > 1 ? nbr : 1;
         num_cu[dev] = cus > 0 ? cus : 1;
     }
-    const long T = (long)a.strip_count * a.H;
+    const long T = (long)a.strip_count * a.nframes * a.H;
     long grid = (long)blocks_per_cu[dev] * num_cu[dev];
     if (a.grid_override > 0) grid = a.grid_override;
     if (grid > T) grid = T;

@@ -22,6 +22,8 @@ struct Bm2Args {
     const uint8_t *ref;  // reference image (L for left/volume passes, R for the right pass)
     const uint8_t *src;  // searched image
     int64_t stride;      // row stride of both images in bytes
+    int nframes;         // frames in this launch (>= 1); frame f's inputs start f * frame_stride bytes
+    int64_t frame_stride;  // in, its outputs / LR buffers f * H * W elements in
     int H, W;
     int m;               // min_disp
     int D;               // num_disp (padded internally to the kernel's Dp)
@@ -68,8 +70,8 @@ __device__ __forceinline__ int div_trunc_small(int num, int den2) {
 // nw = waves per block: SAD Dp = 128*nw (nw in {1,2,4}), SSD Dp = 64*nw (nw in {1,2,4,8}).
 hipError_t launch_bm2(int radius, bool ssd, int nw, const Bm2Args &a, hipStream_t st);
 hipError_t launch_volume_wta(int TX, bool ssd, const VolArgs &a, hipStream_t st);
-// LR check after the left pass: invalidate x where |dR(x - m - d*) - d*| > lr.
-hipError_t launch_lr_fixup(const int16_t *dstar, const uint32_t *keys, int H, int W, int m, int lr, int kshift,
+// LR check after the left pass: invalidate x where |dR(x - m - d*) - d*| > lr; resets the keys.
+hipError_t launch_lr_fixup(const int16_t *dstar, uint32_t *keys, int H, int W, int m, int lr, int kshift,
                            int16_t *out_fixed, float *out_float, hipStream_t st);
 
 size_t volume_smem_bytes(int TX, bool ssd, int Dp, int TPP, int W);

@@ -145,6 +145,19 @@ class HipBlockMatcher:
         rc = _dsx.lib().dsx_compute_device(self._handle(), lp, rp, H, W, st, _ptr(out_fixed), _ptr(out_float), sptr)
         _dsx.check(rc, "dsx_compute_device")
 
+    def compute_batch_device(self, left, right, out_fixed=None, out_float=None, stream=None):
+        """One launch over N frame pairs: ``left``/``right`` uint8 HIP tensors N x H x W (unit
+        column stride, equal strides); outputs contiguous N x H x W.  Equals N compute_device calls."""
+        if left.dim() != 3 or left.shape != right.shape or left.stride() != right.stride():
+            raise ValueError("left and right must be N x H x W tensors of the same shape and strides")
+        if str(left.dtype) != "torch.uint8" or left.stride(2) != 1 or not left.is_cuda or not right.is_cuda:
+            raise ValueError("inputs must be uint8 device tensors with unit column stride")
+        N, H, W = left.shape
+        sptr = None if stream is None else (stream if isinstance(stream, int) else stream.cuda_stream)
+        rc = _dsx.lib().dsx_compute_batch_device(self._handle(), N, left.data_ptr(), right.data_ptr(), left.stride(0),
+                                                 H, W, left.stride(1), _ptr(out_fixed), _ptr(out_float), sptr)
+        _dsx.check(rc, "dsx_compute_batch_device")
+
     def right_map_device(self, left, right, out_dR, stream=None):
         H, W = left.shape
         sptr = None if stream is None else (stream if isinstance(stream, int) else stream.cuda_stream)

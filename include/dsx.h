@@ -104,6 +104,15 @@ int dsx_compute_device(dsx_handle *h, const void *dL, const void *dR, int32_t H,
                        int64_t stride_bytes, void *d_out_fixed, void *d_out_float,
                        void *hip_stream);
 
+/* Batched asynchronous compute of `nframes` frame pairs in ONE launch (video streams,
+ * StereoDepthEstimatorVideo.py:69-147 frames handed over in groups): frame f's inputs start at
+ * dL + f * frame_stride_bytes (same for dR); outputs are contiguous [nframes][H][W].  Same
+ * results as nframes calls of dsx_compute_device; the persistent grid spreads the
+ * (frame, strip, row) work, which amortises per-launch and per-run costs for small frames. */
+int dsx_compute_batch_device(dsx_handle *h, int32_t nframes, const void *dL, const void *dR, int64_t frame_stride_bytes,
+                             int32_t H, int32_t W, int64_t stride_bytes, void *d_out_fixed, void *d_out_float,
+                             void *hip_stream);
+
 /* Right-view winner map only (the LR check's dR, int16 H x W, -1 where the search range is
  * empty). Exposed for parity tests of the right pass. Async on hip_stream. */
 int dsx_right_map_device(dsx_handle *h, const void *dL, const void *dR, int32_t H, int32_t W,

@@ -155,3 +155,26 @@ def test_golden_fixtures(torch_dev, golden, path):
     np.testing.assert_array_equal(fl, z["fixed"].astype(np.float32) / np.float32(16))
     _, par = _run(z["L"], z["R"], path=path, float_mode="parabola", **kw)
     assert np.max(np.abs(par - z["parabola"])) <= FLOAT_TOL
+
+
+@pytest.mark.parametrize("path,cost,bs,D,u,lr", [("fused", "sad", 5, 64, 10, 1), ("fused", "sad", 9, 128, 0, -1),
+                                                 ("fused", "ssd", 7, 96, 10, 0), ("volume", "sad", 3, 64, 10, 1)])
+def test_batch_equals_single(torch_dev, path, cost, bs, D, u, lr):
+    """dsx_compute_batch_device over N frames == N dsx_compute_device calls (and the oracle)."""
+    torch = torch_dev
+    from depthestimation_amd.matcher import HipBlockMatcher
+    N, H, W = 3, 41, 230
+    pairs = [stereo_pair(H, W, 2, D, seed=70 + i) for i in range(N)]
+    Lb = torch.from_numpy(np.stack([p[0] for p in pairs])).cuda()
+    Rb = torch.from_numpy(np.stack([p[1] for p in pairs])).cuda()
+    m = HipBlockMatcher(min_disp=2, num_disp=D, block_size=bs, cost=cost, uniqueness_ratio=u, disp12_max_diff=lr,
+                        path=path)
+    of = torch.empty((N, H, W), dtype=torch.int16, device="cuda")
+    ff = torch.empty((N, H, W), dtype=torch.float32, device="cuda")
+    m.compute_batch_device(Lb, Rb, out_fixed=of, out_float=ff)
+    torch.cuda.synchronize()
+    for i, (L, R, _) in enumerate(pairs):
+        ref = stereo_bm(L, R, 2, D, bs, cost, u, lr, True)
+        np.testing.assert_array_equal(of[i].cpu().numpy(), ref["fixed"])
+        np.testing.assert_array_equal(ff[i].cpu().numpy(), ref["disp"])
+    m.close()
