@@ -224,6 +224,18 @@ dsx::Bm2Args base_args(dsx_handle *h, int H, int W, int64_t stride) {
     a.strip_begin = 0;
     a.strip_count = (W + dsx::kStripWidth - 1) / dsx::kStripWidth;
     a.grid_override = h->p.grid_blocks;
+    {
+        // Balance (measured on C2-C5, profiles/README.md r01d): co-resident waves drop their issue
+        // priority as they pass 50 / 80 / 95 % of their rows, and strips on the clamped-load
+        // path count 11/8 of a fast strip.  DSX_PRIO=0 / DSX_PRIO_T / DSX_SLOW_W8 override.
+        const char *pe = getenv("DSX_PRIO");
+        a.prio = pe ? atoi(pe) : 1;
+        a.pt1 = 128, a.pt2 = 205, a.pt3 = 243;
+        const char *pt = getenv("DSX_PRIO_T");
+        if (pt) sscanf(pt, "%d,%d,%d", &a.pt1, &a.pt2, &a.pt3);
+        const char *sw = getenv("DSX_SLOW_W8");
+        a.slow_w8 = sw ? atoi(sw) : 11;
+    }
     a.nframes = 1;
     a.frame_stride = 0;
     return a;
@@ -544,6 +556,8 @@ int dsx_compute_batch_device(dsx_handle *h, int32_t nframes, const void *dL, con
     if (rc) return rc;
     if (nframes > 1 && frame_stride_bytes < (int64_t)(H - 1) * stride_bytes + W)
         return fail(DSX_EINVAL, "frame_stride_bytes smaller than one frame");
+    if ((int64_t)nframes * H * W > ((int64_t)1 << 31) - 1)
+        return fail(DSX_EINVAL, "nframes * H * W must stay below 2^31 pixels per launch");
     DSX_HIP(hipSetDevice(h->device));
     rc = ensure_buffers(h, H, W, false, nframes);
     if (rc) return rc;

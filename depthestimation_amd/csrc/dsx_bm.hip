@@ -120,7 +120,7 @@ typedef const __attribute__((address_space(4))) uint32_t cu32;
 // indices, which hipcc would demote to scratch).
 template <int R, bool SSD, int NW, int SIDE, bool FAST>
 __device__ __forceinline__ void bm2_segment(const Bm2Args &a, uint8_t *smem, int x0, int yb, int ye, long fin, long fout,
-                                            bool lr_on
+                                            bool lr_on, int done0, const int (&pe)[3], int &qcur
 #ifdef DSX_STAMPS
                                             , uint64_t (&ph)[8], uint64_t &t_prev, uint64_t &nsteps
 #endif
@@ -147,39 +147,35 @@ __device__ __forceinline__ void bm2_segment(const Bm2Args &a, uint8_t *smem, int
     // ---- raw row loads (registers) and their LDS stores ----
     // FAST: w0 = dword of 4 search bytes, w1 = the 5th byte; SLOW: w0..w3 = finished S words
     constexpr int NC4 = (NC + 3) / 4;
+    // Branch-free: every lane loads (positions clamped into the row), so no load sits under an
+    // exec branch and the compiler never drains vmcnt inside the prefetch; st() stores only the
+    // lanes that own staged words.
     auto ld = [&](int r, uint32_t &w0, uint32_t &w1, uint32_t &w2, uint32_t &w3, uint32_t &rf) __attribute__((always_inline)) {
         const int yy = clampi2(r, 0, H - 1);
         const uint8_t *srow = a.src + fin + (long)yy * stride;
         const uint8_t *rrow = a.ref + fin + (long)yy * stride;
+        const int tr = min(tid, NC4 - 1);
         if constexpr (FAST) {
-            rf = tid < NC4 ? *reinterpret_cast<const uint32_t *>(rrow + x0 - R + 4 * tid) : 0u;
+            rf = *reinterpret_cast<const uint32_t *>(rrow + x0 - R + 4 * tr);
         } else {
             uint32_t v = 0;
-            if (tid < NC4) {
 #pragma unroll
-                for (int q = 0; q < 4; ++q) v |= (uint32_t)rrow[clampi2(x0 - R + 4 * tid + q, 0, W - 1)] << (8 * q);
-            }
+            for (int q = 0; q < 4; ++q) v |= (uint32_t)rrow[clampi2(x0 - R + 4 * tr + q, 0, W - 1)] << (8 * q);
             rf = v;
         }
         if constexpr (FAST) {
-            w0 = 0;
-            w1 = 0;
-            if (tid < NJ4) {
-                const uint8_t *p = side == 1 ? srow + PB + 4 * tid : srow + PB - 4 * tid - 3;
-                w0 = *reinterpret_cast<const uint32_t *>(p);
-                w1 = side == 1 ? p[4] : p[-1];
-            }
+            const int tj = min(tid, NJ4 - 1);
+            const uint8_t *p = side == 1 ? srow + PB + 4 * tj : srow + PB - 4 * tj - 3;
+            w0 = *reinterpret_cast<const uint32_t *>(p);
+            w1 = side == 1 ? p[4] : p[-1];
         } else {
             uint32_t v[4];
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
-                const int j = 4 * tid + q;
-                uint32_t t = 0;
-                if (j < NJ) {
-                    const int pp = PB + sgn * j;
-                    t = srow[clampi2(pp, 0, W - 1)];
-                    if constexpr (!SSD) t |= (uint32_t)srow[clampi2(pp + sgn, 0, W - 1)] << 16;
-                }
+                const int j = min(4 * tid + q, NJ - 1);
+                const int pp = PB + sgn * j;
+                uint32_t t = srow[clampi2(pp, 0, W - 1)];
+                if constexpr (!SSD) t |= (uint32_t)srow[clampi2(pp + sgn, 0, W - 1)] << 16;
                 v[q] = t;
             }
             w0 = v[0];
@@ -326,6 +322,22 @@ __device__ __forceinline__ void bm2_segment(const Bm2Args &a, uint8_t *smem, int
         ++nsteps;
 #endif
         DSX_STAMP(0);
+        if (a.prio) {
+            // issue priority by progress quartile: waves that are behind (the younger ones on a
+            // SIMD, which lose age arbitration) take the VALU first, so co-resident waves finish
+            // together instead of leaving the last one alone on its SIMD
+            const int dn = done0 + (y - yb);
+            const int q = (dn >= pe[0]) + (dn >= pe[1]) + (dn >= pe[2]);
+            if (q != qcur) {
+                qcur = q;
+                switch (q) {
+                    case 0: __builtin_amdgcn_s_setprio(3); break;
+                    case 1: __builtin_amdgcn_s_setprio(2); break;
+                    case 2: __builtin_amdgcn_s_setprio(1); break;
+                    default: __builtin_amdgcn_s_setprio(0); break;
+                }
+            }
+        }
         const int par = (y & 1) * 2;  // slots {par, par+1} = {new row y+R, old row y-R-1}
         const bool more = y + 1 < ye;
         // prefetch the next step's entering / leaving rows (+ its dR segment); lands during this step
@@ -587,11 +599,11 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(3))) vo
     if ((side == 0 || side == 3) && (a.out_fixed || a.out_float)) {
         const int xa = a.strip_begin * TX, xb = min(W, (a.strip_begin + a.strip_count) * TX);
         const int nin = xa + (W - xb);
-        const long total = (long)nin * H * a.nframes;  // frames are H-row slabs of one tall output
+        const int total = nin * H * a.nframes;  // frames are H-row slabs of one tall output (< 2^31)
         const int16_t fi = (int16_t)((m - 1) * 16);
-        for (long q = (long)blockIdx.x * NT + tid; q < total; q += (long)gridDim.x * NT) {
-            const long y = q / nin;
-            const int c = (int)(q - y * nin);
+        for (int q = blockIdx.x * NT + tid; q < total; q += gridDim.x * NT) {
+            const int y = q / nin;
+            const int c = q - y * nin;
             const int x = c < xa ? c : xb + (c - xa);
             const long o = (long)y * W + x;
             if (a.out_fixed) a.out_fixed[o] = fi;
@@ -600,30 +612,75 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(3))) vo
     }
 
     // ---- work partition over the (frame, strip, row) space: with at least one block per
-    // (frame, strip), every block owns ONE contiguous run of rows of ONE strip of one frame
-    // (balanced to +-1 block per strip); otherwise an even split of the linearised space.
+    // (frame, strip), every block owns ONE contiguous run of rows of ONE strip of one frame;
+    // otherwise an even split of the linearised space.  Strips on the clamped-load path (image
+    // edges) weigh slow_w8/8 of a fast strip, so they get proportionally more blocks.
     const int NS = a.strip_count * a.nframes;
-    const long NG = gridDim.x, b = blockIdx.x;
-    long lin0, lin1;
+    const int NG = gridDim.x, b = blockIdx.x;
+    int lin0, lin1;  // (frame, strip, row) units: nframes * H * W < 2^31 (host check)
     if (NG >= NS && NS > 0) {
-        const int s = (int)(b * NS / NG);
-        const long bs0 = ((long)s * NG + NS - 1) / NS, bs1 = ((long)(s + 1) * NG + NS - 1) / NS;
-        const long j = b - bs0, cnt = bs1 - bs0;
-        lin0 = (long)s * H + j * H / cnt;
-        lin1 = (long)s * H + (j + 1) * H / cnt;
+        const int S = a.strip_count;
+        // fast strips: x0 in [XL, XU] (the `fast` test below, solved for x0)
+        constexpr int NJ4c = (NJ + 3) / 4, NC4c = (NC + 3) / 4;
+        int XL, XU;
+        if (side == 1) {
+            XL = max(R - m, R);
+            XU = min(W - 1 - 4 * NJ4c + R - m, W - 1 + R - 4 * NC4c + 1);
+        } else {
+            XL = max(4 * NJ4c + R + m - NC + 1, R);
+            XU = min(W - 1 + R + m - NC + 1, W - 1 + R - 4 * NC4c + 1);
+        }
+        const int sb = a.strip_begin;
+        const int slo = clampi2((XL + TX - 1 >= 0 ? (XL + TX - 1) / TX : -((-(XL + TX - 1) + TX - 1) / TX)) - sb, 0, S);
+        const int shi = clampi2((XU >= 0 ? XU / TX : -((-XU + TX - 1) / TX)) - sb + 1, slo, S);  // fast: [slo, shi)
+        int w8 = a.slow_w8;
+        if (w8 < 8 || NG * 8 < NS * w8 + 8 * NS) w8 = 8;  // every strip keeps >= 1 block
+        const int ex = w8 - 8;
+        auto Pf = [&](int s) -> long { return 8L * s + (long)ex * (min(s, slo) + max(0, s - shi)); };
+        const long Uf = Pf(S), U = Uf * a.nframes;
+        auto P = [&](int g) -> long { const int f = g / S; return f * Uf + Pf(g - f * S); };
+        // start(g) = ceil(P(g) * NG / U): double quotient + exact integer fix-up (no 64-bit
+        // integer division, which is a long SALU sequence on gfx950)
+        auto start = [&](int g) -> int {
+            const long num = P(g) * NG;
+            long q = (long)__builtin_ceil((double)num / (double)U);
+            if (q * U < num) ++q;
+            if (q > 0 && (q - 1) * U >= num) --q;
+            return (int)q;
+        };
+        int lo = 0, hi = NS - 1;  // largest g with start(g) <= b
+        while (lo < hi) {
+            const int mid = (lo + hi + 1) >> 1;
+            if (start(mid) <= b) lo = mid;
+            else hi = mid - 1;
+        }
+        const int s = lo;
+        const int bs0 = start(s), bs1 = start(s + 1);
+        const int j = b - bs0, cnt = bs1 - bs0;
+        lin0 = s * H + j * H / cnt;
+        lin1 = s * H + (j + 1) * H / cnt;
     } else {
         const long T = (long)NS * H;
-        lin0 = b * T / NG;
-        lin1 = (b + 1) * T / NG;
+        lin0 = (int)(b * T / NG);
+        lin1 = (int)((b + 1) * T / NG);
     }
     constexpr bool lr_on = SIDE == 3;  // left pass that also builds the right-view winners
-    for (long it = lin0; it < lin1;) {
-        const int sidx = (int)(it / H);
+    int qcur = -1;
+    int pe[3];  // rows done at which the priority drops (progress bands pt1..pt3 of 256)
+    {
+        const int tot = lin1 - lin0;
+        pe[0] = (a.pt1 * tot + 255) >> 8;
+        pe[1] = (a.pt2 * tot + 255) >> 8;
+        pe[2] = (a.pt3 * tot + 255) >> 8;
+    }
+    for (int it = lin0; it < lin1;) {
+        const int sidx = it / H;
         const int f = sidx / a.strip_count;
         const int s = a.strip_begin + (sidx - f * a.strip_count);
         const long fin = (long)f * a.frame_stride, fout = (long)f * H * W;
-        const int yb = (int)(it % H);
-        const int ye = (int)min((long)H, (long)yb + (lin1 - it));
+        const int yb = it - sidx * H;
+        const int ye = min(H, yb + (lin1 - it));
+        const int done0 = it - lin0;
         it += ye - yb;
         const int x0 = s * TX;
         const int PB = side == 1 ? (x0 - R + m) : (x0 - R - m + NC - 1);
@@ -631,13 +688,13 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(3))) vo
         const bool fast = (side == 1 ? (PB >= 0 && PB + 4 * NJ4 <= W - 1) : (PB - 4 * NJ4 >= 0 && PB <= W - 1)) &&
                           x0 - R >= 0 && x0 - R + 4 * ((NC + 3) / 4) - 1 <= W - 1;
         if (fast)
-            bm2_segment<R, SSD, NW, SIDE, true>(a, smem, x0, yb, ye, fin, fout, lr_on
+            bm2_segment<R, SSD, NW, SIDE, true>(a, smem, x0, yb, ye, fin, fout, lr_on, done0, pe, qcur
 #ifdef DSX_STAMPS
                                                 , ph, t_prev, nsteps
 #endif
             );
         else
-            bm2_segment<R, SSD, NW, SIDE, false>(a, smem, x0, yb, ye, fin, fout, lr_on
+            bm2_segment<R, SSD, NW, SIDE, false>(a, smem, x0, yb, ye, fin, fout, lr_on, done0, pe, qcur
 #ifdef DSX_STAMPS
                                                  , ph, t_prev, nsteps
 #endif

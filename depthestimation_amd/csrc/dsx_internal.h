@@ -32,6 +32,9 @@ struct Bm2Args {
     uint32_t padv;       // cost stored for disparities outside [0, D) / outside the image
     int strip_begin, strip_count;  // 32-column strips forming the work space
     int grid_override;   // >0: force the persistent grid size (tests)
+    int prio;            // 1: waves raise their issue priority while behind (progress bands below)
+    int pt1, pt2, pt3;   // progress band edges in 1/256 of a block's rows (priority 3, 2, 1, 0)
+    int slow_w8;         // work weight of a strip on the clamped-load path, in 1/8 of a fast strip
     uint32_t *lr_keys;     // left pass with LR: per-pixel right-view winner keys (C << kshift | d),
     int kshift;            //   filled by atomicMin (memset to ~0 first)
     int16_t *dstar;        // left pass with LR: winning d (or -1) for lr_fixup

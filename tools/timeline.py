@@ -52,3 +52,13 @@ if ext.size >= 12 * 65536:
         names = ["update", "prefetch-issue", "horizontal", "barrier1", "epilogue", "store-row", "barrier2"]
         tot = ps[:, :7].astype(np.float64).sum(0) / steps.sum()
         print("cycles per row-step (s_memtime):", {n: round(v, 1) for n, v in zip(names, tot)}, "sum", round(tot.sum(), 1))
+# duration by strip (block b owns strip b * NS / NG in the one-strip-per-block regime)
+NS = (W + 31) // 32
+dur = en - st
+bs_ = np.arange(len(t))
+strip = bs_ * NS // len(t)
+per = [dur[strip == s].mean() for s in range(NS)]
+print("mean block duration per strip (us):", " ".join(f"{v:.0f}" for v in per))
+print("slowest 10 blocks (block, strip, dur, start):", [(int(b), int(strip[b]), round(float(dur[b]), 1), round(float(st[b]), 1)) for b in np.argsort(-dur)[:10]])
+print("duration by CU-slot rank within CU:")
+order = np.lexsort((st, key))
