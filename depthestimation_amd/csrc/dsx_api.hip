@@ -235,6 +235,8 @@ dsx::Bm2Args base_args(dsx_handle *h, int H, int W, int64_t stride) {
         if (pt) sscanf(pt, "%d,%d,%d", &a.pt1, &a.pt2, &a.pt3);
         const char *sw = getenv("DSX_SLOW_W8");
         a.slow_w8 = sw ? atoi(sw) : 11;
+        const char *va = getenv("DSX_VARIANT");
+        a.variant = va ? atoi(va) : 0;
     }
     a.nframes = 1;
     a.frame_stride = 0;

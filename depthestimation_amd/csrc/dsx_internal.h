@@ -34,6 +34,7 @@ struct Bm2Args {
     int grid_override;   // >0: force the persistent grid size (tests)
     int prio;            // 1: waves raise their issue priority while behind (progress bands below)
     int pt1, pt2, pt3;   // progress band edges in 1/256 of a block's rows (priority 3, 2, 1, 0)
+    int variant;         // experiment bits (DSX_VARIANT env), 0 = production
     int slow_w8;         // work weight of a strip on the clamped-load path, in 1/8 of a fast strip
     uint32_t *lr_keys;     // left pass with LR: per-pixel right-view winner keys (C << kshift | d),
     int kshift;            //   filled by atomicMin (memset to ~0 first)

@@ -14,6 +14,8 @@
 //                  via right-view winners built with LDS ds_min_u32 scatters.
 #include "dsx_internal.h"
 
+#include <cstdlib>
+
 #include <algorithm>
 
 #include <type_traits>
@@ -64,7 +66,7 @@ __device__ __forceinline__ uint32_t slice_cost(const uint4 (&v)[NV], int j) {
     }
 }
 
-template <bool SSD, bool UNIQ, bool LR>
+template <bool SSD, bool UNIQ, bool LR, int RING>
 __global__ __launch_bounds__(kVolThreads) void vol_wta(VolArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     using CT = cost_t<SSD>;
@@ -75,6 +77,10 @@ __global__ __launch_bounds__(kVolThreads) void vol_wta(VolArgs a) {
     const int XC = kVolThreads / TPP;  // pixels per chunk
     const int y = blockIdx.x;
     constexpr bool lr = LR;
+    // row segment [xa, xb) of this block (gridDim.y segments per row; 1 with the LR check, whose
+    // right-view winners need the whole row)
+    const int XSg = ((W + gridDim.y - 1) / gridDim.y + XC - 1) / XC * XC;
+    const int xa = blockIdx.y * XSg, xb = min(W, xa + XSg);
     const int k = tid / TPP, s = tid - (tid / TPP) * TPP;
     const int dbase = s * TX;
     const uint32_t dmask = (1u << DB) - 1u;
@@ -95,7 +101,7 @@ __global__ __launch_bounds__(kVolThreads) void vol_wta(VolArgs a) {
     // unconditional loads (clamped pixel): no branch around them, so the compiler keeps partial
     // vmcnt waits and the ring really has two chunks in flight
     auto load = [&](int xc0, uint4(&v)[NV]) __attribute__((always_inline)) {
-        const int x = min(xc0 + k, W - 1);
+        const int x = min(xc0 + k, xb - 1);
         const u32x4 *p = reinterpret_cast<const u32x4 *>(vrow + (size_t)x * Dp + dbase);
 #pragma unroll
         for (int i = 0; i < NV; ++i) {
@@ -104,9 +110,9 @@ __global__ __launch_bounds__(kVolThreads) void vol_wta(VolArgs a) {
         }
     };
     auto process = [&](int xc0, const uint4(&cur)[NV]) __attribute__((always_inline)) {
-        if (xc0 >= W) return;
+        if (xc0 >= xb) return;
         const int x = xc0 + k;
-        const bool inb = x < W;
+        const bool inb = x < xb;
         if (a.subpix) {
 #pragma unroll
             for (int i = 0; i < NV; ++i) scratch[i] = cur[i];
@@ -160,20 +166,19 @@ __global__ __launch_bounds__(kVolThreads) void vol_wta(VolArgs a) {
         }
         if (a.subpix) __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront", "local");  // reads before next writes
     };
-    // 3-deep register ring: two chunks in flight while one is reduced
-    uint4 b0[NV], b1[NV], b2[NV];
-    load(0, b0);
-    load(XC, b1);
-    for (int xc0 = 0; xc0 < W; xc0 += 3 * XC) {
-        load(xc0 + 2 * XC, b2);
-        process(xc0, b0);
-        load(xc0 + 3 * XC, b0);
-        process(xc0 + XC, b1);
-        load(xc0 + 4 * XC, b1);
-        process(xc0 + 2 * XC, b2);
+    // RING-deep register ring: RING-1 chunks in flight while one is reduced
+    uint4 rb[RING][NV];
+#pragma unroll
+    for (int i = 0; i < RING - 1; ++i) load(xa + i * XC, rb[i]);
+    for (int xc0 = xa; xc0 < xb; xc0 += RING * XC) {
+#pragma unroll
+        for (int i = 0; i < RING; ++i) {
+            load(xc0 + (i + RING - 1) * XC, rb[(i + RING - 1) % RING]);
+            process(xc0 + i * XC, rb[i]);
+        }
     }
     __syncthreads();
-    for (int x = tid; x < W; x += kVolThreads) {
+    for (int x = xa + tid; x < xb; x += kVolThreads) {
         int16_t fx = rowFixed[x];
         bool valid = true;
         if (lr) {
@@ -233,20 +238,32 @@ size_t volume_smem_bytes(int TX, bool ssd, int Dp, int TPP, int W) {
     return (size_t)kVolThreads * (ssd ? 64 : 32) + (size_t)round16(W * 4) * 2 + (size_t)W * 4;
 }
 
-template <bool SSD, bool UNIQ, bool LR>
-static hipError_t launch_vol_one(const VolArgs &a, hipStream_t st) {
+template <bool SSD, bool UNIQ, bool LR, int RING>
+static hipError_t launch_vol_ring(const VolArgs &a, hipStream_t st) {
     const size_t smem = volume_smem_bytes(16, SSD, a.Dp, a.TPP, a.W);
     static bool attr_done[64] = {};
     int dev = 0;
     (void)hipGetDevice(&dev);
     if (dev < 0 || dev >= 64 || !attr_done[dev]) {
-        hipError_t e = hipFuncSetAttribute((const void *)vol_wta<SSD, UNIQ, LR>,
+        hipError_t e = hipFuncSetAttribute((const void *)vol_wta<SSD, UNIQ, LR, RING>,
                                            hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         if (e != hipSuccess) return e;
         if (dev >= 0 && dev < 64) attr_done[dev] = true;
     }
-    hipLaunchKernelGGL((vol_wta<SSD, UNIQ, LR>), dim3(a.H), dim3(kVolThreads), smem, st, a);
+    // 4 row segments per row without the LR check: 4x the blocks for 1080 rows on 256 CUs
+    // (C2 K2 161 -> 150 us, C5 843 -> 785 us; DSX_K2_SEG overrides)
+    static const int seg = [] {
+        const char *e = getenv("DSX_K2_SEG");
+        return e ? atoi(e) : 4;
+    }();
+    const int nseg = LR ? 1 : (seg > 1 ? seg : 1);
+    hipLaunchKernelGGL((vol_wta<SSD, UNIQ, LR, RING>), dim3(a.H, nseg), dim3(kVolThreads), smem, st, a);
     return hipGetLastError();
+}
+
+template <bool SSD, bool UNIQ, bool LR>
+static hipError_t launch_vol_one(const VolArgs &a, hipStream_t st) {
+    return launch_vol_ring<SSD, UNIQ, LR, 3>(a, st);
 }
 
 template <bool SSD>
