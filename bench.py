@@ -110,6 +110,7 @@ def main():
     ap.add_argument("--grid-blocks", type=int, default=0, help="force the persistent grid size (tuning)")
     ap.add_argument("--batch", type=int, default=1, help="frame pairs per GPU per step (one launch)")
     ap.add_argument("--no-batched", action="store_true", help="skip the secondary batched measurement")
+    ap.add_argument("--no-e2e", action="store_true", help="skip the PCIe-inclusive host-buffer measurement")
     args = ap.parse_args()
 
     import torch
@@ -274,6 +275,23 @@ def main():
                                     "hbm_bytes_per_launch")}
             result["roofline_volume"] = rv
             vm.close()
+
+        if not args.no_e2e and ws == 1 and args.path == "fused":
+            # secondary, never `value`: host numpy frames -> pinned -> H2D -> matcher -> D2H, two
+            # workers (streams) on this GPU via multigpu.MultiDeviceStereo (SURVEY 8e end-to-end)
+            from depthestimation_amd.multigpu import MultiDeviceStereo
+            run = MultiDeviceStereo(devices=[local], streams_per_device=2, **kw)
+            ne = 64
+            src = [(hostL[i % nres], hostR[i % nres]) for i in range(ne)]
+            for _ in run.map(iter(src[:4])):
+                pass
+            t1 = time.perf_counter()
+            n_done = sum(1 for _ in run.map(iter(src)))
+            et = time.perf_counter() - t1
+            result["e2e_host"] = {"value": round(H * W * n_done / et / 1e6, 1), "unit": "Mpix/s", "frames": n_done,
+                                  "ms_per_frame": round(et / n_done * 1e3, 4),
+                                  "note": "secondary, PCIe-inclusive: host uint8 pairs in, int16 x16 out, 2 worker "
+                                          "streams on one GPU (multigpu.MultiDeviceStereo)"}
 
         if not args.no_cpu_baseline and ws == 1:
             L, R = host_first

@@ -8,8 +8,11 @@ The re-application of ``configure_sgbm`` to already-scaled parameters at the sta
 ``estimate_depth`` (StereoDepthEstimatorVideo.py:78; num_disp, focal_length and doffs get
 downscale_factor squared) is kept, so results match the reference's.
 
-Multi-GPU: pass ``rank``/``world_size`` (or let them come from the torch.distributed env)
-to process only frames i with i % world_size == rank; see ``sharding.py``.
+Multi-GPU, two forms: pass ``rank``/``world_size`` (or let them come from the
+torch.distributed env) to process only frames i with i % world_size == rank in one process per
+GPU (``sharding.py``); or pass ``devices=[0, 1, ...]`` to drive several GPUs from this one
+process (``multigpu.MultiDeviceStereo``: frame i on devices[i % N], one StereoCore per worker,
+results yielded in frame order).
 """
 from __future__ import annotations
 
@@ -25,7 +28,7 @@ from .threaded_stereo import ThreadedStereoCapture
 class StereoDepthEstimatorVideo:
     def __init__(self, left_source=None, right_source=None, downscale_factor=1.0, visualize_live=False,
                  saving_path=None, fast_mode=False, use_threading=True, target_fps=30, drop_frames=False,
-                 visualize_gray=False, rank=None, world_size=None) -> None:
+                 visualize_gray=False, rank=None, world_size=None, devices=None) -> None:
         self.left_source = left_source
         self.right_source = right_source
         self.downscale_factor = downscale_factor
@@ -40,6 +43,7 @@ class StereoDepthEstimatorVideo:
         env = DistEnv.from_env()
         self.rank = env.rank if rank is None else int(rank)
         self.world_size = env.world_size if world_size is None else int(world_size)
+        self.devices = None if devices is None else [int(d) for d in devices]
         self.core = StereoCore(downscale_factor=downscale_factor, fast_mode=fast_mode)
         if self.world_size > 1:
             self.core.configure_sgbm(device=env.local_rank if rank is None else self.core.sgbm_params['device'])
@@ -70,11 +74,39 @@ class StereoDepthEstimatorVideo:
         self.core.configure_sgbm(**self.core.get_sgbm_params())
         if self.visualize_live:
             warnings.warn("visualize_live: no GUI in this build; frames are only yielded", RuntimeWarning)
+        if self.devices:
+            yield from self._estimate_multi_device()
+            return
         frame_start_time = time.time()
         for i, (left_frame, right_frame) in enumerate(self._frames()):
             if i % self.world_size != self.rank:
                 continue
             _, depth_m = self.core.estimate_depth(left_frame, right_frame)
+            yield depth_m
+            if self._frame_interval > 0:
+                sleep_time = self._frame_interval - (time.time() - frame_start_time)
+                if sleep_time > 0:
+                    time.sleep(sleep_time)
+            frame_start_time = time.time()
+
+    def _estimate_multi_device(self):
+        """Single-process multi-GPU form: every worker owns a StereoCore with this facade's
+        (already re-scaled) parameters on its device; depth maps come back in frame order."""
+        from .multigpu import MultiDeviceStereo
+
+        params = dict(self.core.get_sgbm_params())
+        ds, fast = self.downscale_factor, self.fast_mode
+
+        def make(dev):
+            core = StereoCore(downscale_factor=ds, fast_mode=fast)
+            core.sgbm_params.update(params)
+            core.sgbm_params['device'] = dev
+            core._build_sgbm()
+            return lambda pair: core.estimate_depth(pair[0], pair[1])[1]
+
+        runner = MultiDeviceStereo(devices=self.devices, streams_per_device=1)
+        frame_start_time = time.time()
+        for depth_m in runner.map_fn(self._frames(), make):
             yield depth_m
             if self._frame_interval > 0:
                 sleep_time = self._frame_interval - (time.time() - frame_start_time)

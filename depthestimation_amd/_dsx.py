@@ -31,6 +31,7 @@ EXPORTS = (
     "dsx_postprocess_fast_device", "dsx_postprocess_workspace_bytes", "dsx_postprocess_full_device",
     "dsx_rectify_device",
     "dsx_kernel_times", "dsx_reset_times", "dsx_workspace_bytes", "dsx_destroy", "dsx_last_error",
+    "dsx_comm_init_all", "dsx_comm_size", "dsx_bcast", "dsx_comm_destroy",
 )
 
 
@@ -84,6 +85,10 @@ def _bind(lib):
         "dsx_workspace_bytes": (ctypes.c_int, [vp, ctypes.POINTER(ctypes.c_int64)]),
         "dsx_destroy": (ctypes.c_int, [vp]),
         "dsx_last_error": (ctypes.c_char_p, []),
+        "dsx_comm_init_all": (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(vp)]),
+        "dsx_comm_size": (ctypes.c_int, [vp, ctypes.POINTER(ctypes.c_int)]),
+        "dsx_bcast": (ctypes.c_int, [vp, ctypes.POINTER(vp), ctypes.c_size_t, ctypes.c_int]),
+        "dsx_comm_destroy": (ctypes.c_int, [vp]),
     }
     for name, (res, args) in sig.items():
         f = getattr(lib, name)

@@ -368,6 +368,11 @@ int check_shape(int H, int W, int64_t stride) {
 
 }  // namespace
 
+namespace dsx {
+// shared with dsx_comm.hip: one thread-local message behind dsx_last_error()
+int set_error(int code, const std::string &msg) { return fail(code, msg); }
+}  // namespace dsx
+
 extern "C" {
 
 int dsx_version(void) { return DSX_VERSION; }

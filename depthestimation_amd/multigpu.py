@@ -1,0 +1,250 @@
+"""Single-process multi-GPU frame sharding.
+
+The process-per-GPU form of the video path lives in ``sharding.py`` (torch.distributed, one
+rank per GPU, what ``bench.py --gpus N`` runs).  This module is the other form the survey
+describes: ONE process drives N GPUs from threads, the generalisation of
+``ThreadedStereoCapture`` (threaded_stereo.py:23,49-80) from one consumer to N.
+
+* ``DeviceComm``: one RCCL communicator per device (``dsx_comm_init_all``) and the one exchange
+  the path has - the calibration block broadcast from the root GPU (``dsx_bcast``).
+* ``MultiDeviceStereo``: worker threads, two per device, each with its own matcher handle and
+  HIP stream.  Frame i goes to worker i mod (2N), i.e. device i mod N, through a bounded queue;
+  a worker stages the pair into pinned host memory, copies it up, runs the matcher and copies
+  the result back on its stream, so one worker's copies overlap the other's kernels.  Results come back in frame order, as the
+  reference's generator yields them (StereoDepthEstimatorVideo.py:103).  ctypes drops the GIL
+  inside every C-ABI call, so the devices run concurrently.
+
+The product path never routes through a CPU implementation: without a HIP device every
+worker raises RuntimeError.
+"""
+from __future__ import annotations
+
+import ctypes
+import queue
+import threading
+from typing import Callable, Dict, Iterable, Iterator, List, Optional, Sequence, Tuple
+
+import numpy as np
+
+from . import _dsx
+from .matcher import HipBlockMatcher
+from .sharding import CALIB_LEN, pack_calibration, unpack_calibration
+
+
+class DeviceComm:
+    """RCCL communicators over ``devices`` of this process (C-ABI dsx_comm_*)."""
+
+    def __init__(self, devices: Sequence[int]):
+        self.devices = [int(d) for d in devices]
+        arr = (ctypes.c_int * len(self.devices))(*self.devices)
+        h = ctypes.c_void_p()
+        _dsx.check(_dsx.lib().dsx_comm_init_all(len(self.devices), arr, ctypes.byref(h)), "dsx_comm_init_all")
+        self._h = h
+
+    def size(self) -> int:
+        n = ctypes.c_int()
+        _dsx.check(_dsx.lib().dsx_comm_size(self._h, ctypes.byref(n)), "dsx_comm_size")
+        return n.value
+
+    def broadcast(self, tensors: List, root: int = 0) -> None:
+        """In-place broadcast of ``tensors[root]`` into every ``tensors[i]`` (one contiguous
+        device tensor per communicator device, same byte size)."""
+        if len(tensors) != len(self.devices):
+            raise ValueError("one tensor per communicator device is required")
+        nbytes = tensors[0].numel() * tensors[0].element_size()
+        for t, d in zip(tensors, self.devices):
+            if not t.is_cuda or t.device.index != d or not t.is_contiguous():
+                raise ValueError("tensors must be contiguous and live on the communicator's devices, in order")
+            if t.numel() * t.element_size() != nbytes:
+                raise ValueError("all tensors must have the same byte size")
+        ptrs = (ctypes.c_void_p * len(tensors))(*[t.data_ptr() for t in tensors])
+        _dsx.check(_dsx.lib().dsx_bcast(self._h, ptrs, nbytes, int(root)), "dsx_bcast")
+
+    def broadcast_calibration(self, params: Optional[Dict], root: int = 0) -> List[Dict]:
+        """Send the root's calibration block (sharding.pack_calibration, 45 float64) to every
+        device; returns the dict each device received (read back for verification)."""
+        import torch
+        vecs = []
+        for i, d in enumerate(self.devices):
+            v = pack_calibration(params or {}) if i == root else np.zeros(CALIB_LEN, np.float64)
+            vecs.append(torch.from_numpy(v).to(torch.device("cuda", d)))
+        self.broadcast(vecs, root)
+        return [unpack_calibration(v.cpu().numpy()) for v in vecs]
+
+    def close(self) -> None:
+        if getattr(self, "_h", None):
+            _dsx.lib().dsx_comm_destroy(self._h)
+            self._h = None
+
+    def __del__(self):  # pragma: no cover - GC timing
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+_STOP = object()
+
+
+def sharded_map(frames: Iterable, slots: Sequence[int], make_fn: Callable[[int], Callable],
+                queue_depth: int = 4) -> Iterator:
+    """Item i -> worker i mod len(slots) (worker w lives on device slots[w] and calls
+    ``make_fn(slots[w])`` once, in its own thread); results are yielded in item order.  A worker
+    error stops the producer and is re-raised in the consumer.  Pure host threading - the
+    devices only appear through ``make_fn``."""
+    N = len(slots)
+    inq = [queue.Queue(maxsize=max(1, int(queue_depth))) for _ in range(N)]
+    results: Dict[int, object] = {}
+    errors: List[BaseException] = []
+    cv = threading.Condition()
+    stop = threading.Event()
+
+    def worker(slot: int, dev: int):
+        try:
+            fn = make_fn(dev)
+            while True:
+                item = inq[slot].get()
+                if item is _STOP:
+                    return
+                i, payload = item
+                r = fn(payload)
+                with cv:
+                    results[i] = r
+                    cv.notify_all()
+        except BaseException as e:  # surfaced in the consumer
+            with cv:
+                errors.append(e)
+                cv.notify_all()
+            stop.set()
+
+    threads = [threading.Thread(target=worker, args=(s, d), daemon=True) for s, d in enumerate(slots)]
+    for t in threads:
+        t.start()
+    produced = [0]
+    done_producing = threading.Event()
+
+    def producer():
+        try:
+            for i, item in enumerate(frames):
+                while not stop.is_set():
+                    try:
+                        inq[i % N].put((i, item), timeout=0.1)
+                        break
+                    except queue.Full:
+                        continue
+                if stop.is_set():
+                    break
+                with cv:
+                    produced[0] = i + 1
+                    cv.notify_all()
+        except BaseException as e:
+            with cv:
+                errors.append(e)
+                cv.notify_all()
+            stop.set()
+        finally:
+            for q in inq:
+                while True:
+                    try:
+                        q.put(_STOP, timeout=0.1)
+                        break
+                    except queue.Full:
+                        if stop.is_set():
+                            try:
+                                q.get_nowait()
+                            except queue.Empty:
+                                pass
+            with cv:
+                done_producing.set()
+                cv.notify_all()
+
+    pt = threading.Thread(target=producer, daemon=True)
+    pt.start()
+    nxt = 0
+    try:
+        while True:
+            with cv:
+                while nxt not in results and not errors and not (done_producing.is_set() and nxt >= produced[0]):
+                    cv.wait(timeout=1.0)
+                if errors:
+                    raise errors[0]
+                if nxt in results:
+                    r = results.pop(nxt)
+                else:
+                    return
+            yield r
+            nxt += 1
+    finally:
+        stop.set()
+        pt.join(timeout=5.0)
+        for t in threads:
+            t.join(timeout=5.0)
+
+
+class MultiDeviceStereo:
+    """Frame-sharded matcher over several GPUs of one process (see module docstring).
+
+    ``map(frames)`` yields ``(fixed, float)`` per frame pair in order: int16 x16 disparity
+    (the cv2 StereoMatcher.compute contract, stereo_core.py:231) and its float32 /16 view.
+    ``map_fn(frames, make_fn)`` runs an arbitrary per-device function instead (e.g. a whole
+    ``StereoCore.estimate_depth`` on that device) with the same ordering and sharding.
+    """
+
+    def __init__(self, devices: Optional[Sequence[int]] = None, queue_depth: int = 4, streams_per_device: int = 2,
+                 **matcher_kw):
+        n = _dsx.device_count()
+        if n == 0:
+            raise RuntimeError("MultiDeviceStereo: no HIP device visible (the engine has no CPU fallback)")
+        self.devices = list(range(n)) if devices is None else [int(d) for d in devices]
+        if not self.devices:
+            raise ValueError("devices must not be empty")
+        self.queue_depth = max(1, int(queue_depth))
+        # workers: streams_per_device per GPU (one handle + stream each), so one worker's
+        # copies overlap another's kernels on the same GPU; frame i -> worker i mod len(slots)
+        spd = max(1, int(streams_per_device))
+        self.slots = [self.devices[k % len(self.devices)] for k in range(len(self.devices) * spd)]
+        self.matcher_kw = dict(matcher_kw)
+        self.matcher_kw.pop("device", None)
+
+    # -- generic sharded map ---------------------------------------------------------------
+    def map_fn(self, frames: Iterable, make_fn: Callable[[int], Callable]) -> Iterator:
+        """Apply ``make_fn(device)(item)`` to every item, item i on worker i mod len(slots)
+        (device i mod N), results in order.  ``make_fn`` runs inside the worker thread."""
+        return sharded_map(frames, self.slots, make_fn, self.queue_depth)
+
+    # -- the matcher over host frames (PCIe-inclusive) ----------------------------------------
+    def _make_matcher_fn(self, dev: int):
+        import torch
+        torch.cuda.set_device(dev)
+        m = HipBlockMatcher(device=dev, **self.matcher_kw)
+        stream = torch.cuda.Stream(device=dev)
+        state = {}
+
+        def fn(pair: Tuple[np.ndarray, np.ndarray]):
+            L, R = pair
+            L = np.ascontiguousarray(L, np.uint8)
+            R = np.ascontiguousarray(R, np.uint8)
+            if L.shape != R.shape or L.ndim != 2:
+                raise ValueError("left and right must be uint8 H x W arrays of the same size")
+            H, W = L.shape
+            if state.get("shape") != (H, W):
+                state["shape"] = (H, W)
+                state["hin"] = torch.empty((2, H, W), dtype=torch.uint8, pin_memory=True)
+                state["din"] = torch.empty((2, H, W), dtype=torch.uint8, device=dev)
+                state["dfx"] = torch.empty((H, W), dtype=torch.int16, device=dev)
+                state["hfx"] = torch.empty((H, W), dtype=torch.int16, pin_memory=True)
+            hin, din, dfx, hfx = state["hin"], state["din"], state["dfx"], state["hfx"]
+            hin[0].numpy()[...] = L
+            hin[1].numpy()[...] = R
+            with torch.cuda.stream(stream):
+                din.copy_(hin, non_blocking=True)
+                m.compute_device(din[0], din[1], out_fixed=dfx, stream=stream)
+                hfx.copy_(dfx, non_blocking=True)
+            stream.synchronize()
+            fixed = hfx.numpy().copy()
+            return fixed, fixed.astype(np.float32) / 16.0
+
+        return fn
+
+    def map(self, frames: Iterable[Tuple[np.ndarray, np.ndarray]]) -> Iterator[Tuple[np.ndarray, np.ndarray]]:
+        return self.map_fn(frames, self._make_matcher_fn)

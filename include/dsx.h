@@ -37,7 +37,7 @@ extern "C" {
 #define DSX_OK 0
 #define DSX_EINVAL (-1) /* bad argument (mirrors ValueError / cv2.error on bad input) */
 #define DSX_EHIP (-2)   /* HIP runtime error */
-#define DSX_ECOMM (-3)  /* reserved: collective error */
+#define DSX_ECOMM (-3)  /* RCCL (collective) error */
 #define DSX_ENOMEM (-4) /* device allocation failed */
 
 #define DSX_COST_SAD 0
@@ -173,6 +173,30 @@ int dsx_destroy(dsx_handle *h);
 
 /* Thread-local message of the last error on this thread ("" if none). */
 const char *dsx_last_error(void);
+
+/* ---- single-process multi-GPU collectives ----
+ * The frame-sharded video path (StereoDepthEstimatorVideo.py:69-147 fed by
+ * ThreadedStereoCapture, threaded_stereo.py:49-80) has one exchange: the calibration block
+ * (stereo_core.py:26-37 keys; optionally the rectification maps of rectify.py:49-73) sent
+ * once from the root GPU before the first frame.  A process driving several GPUs from
+ * threads creates one RCCL communicator per device (ncclCommInitAll) and broadcasts over
+ * xGMI.  RCCL is loaded lazily (dlopen), so these are the only entry points that need it. */
+typedef struct dsx_comm dsx_comm;
+
+/* One communicator per device in devs[0..ndev) (distinct, visible).  DSX_ECOMM if RCCL is
+ * unavailable or ncclCommInitAll fails. */
+int dsx_comm_init_all(int ndev, const int *devs, dsx_comm **out);
+
+/* Number of devices in the communicator. */
+int dsx_comm_size(dsx_comm *c, int *n);
+
+/* Broadcast `bytes` from dev_bufs[root] into dev_bufs[i] on every device i (device pointers
+ * in communicator order).  Synchronous: orders after prior work on each device, returns once
+ * every copy has landed. */
+int dsx_bcast(dsx_comm *c, void *const *dev_bufs, size_t bytes, int root);
+
+/* Destroy the communicators and their streams (NULL is a no-op). */
+int dsx_comm_destroy(dsx_comm *c);
 
 #ifdef __cplusplus
 }

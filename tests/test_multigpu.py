@@ -1,0 +1,162 @@
+"""Single-process multi-GPU sharding (depthestimation_amd/multigpu.py, SURVEY.md 8e row E1 and
+the dsx_comm_* entry points of 8b row B2).
+
+CPU tests cover the host machinery: frame i -> worker i mod len(slots), results in frame order,
+worker errors surfacing in the consumer, early consumer exit, and the C-ABI refusing devices it
+cannot see.  GPU tests (one MI355X on the test box) run the RCCL broadcast and the sharded
+matcher against the oracle; with more devices visible they use all of them."""
+from __future__ import annotations
+
+import random
+import threading
+import time
+
+import numpy as np
+import pytest
+
+from depthestimation_amd import _dsx
+from depthestimation_amd.multigpu import DeviceComm, MultiDeviceStereo, sharded_map
+
+
+def _slow_square(dev):
+    def f(x):
+        time.sleep(random.random() * 0.002)
+        return dev, threading.get_ident(), x * x
+    return f
+
+
+@pytest.mark.parametrize("slots", [[0], [0, 1], [0, 1, 2, 3, 0, 1, 2, 3]])
+def test_sharded_map_keeps_frame_order(slots):
+    out = list(sharded_map(range(64), slots, _slow_square, queue_depth=2))
+    assert [r[2] for r in out] == [i * i for i in range(64)]
+    # item i ran on worker i mod len(slots), i.e. device slots[i mod len(slots)]
+    assert [r[0] for r in out] == [slots[i % len(slots)] for i in range(64)]
+    # one thread per worker
+    tid_of = {}
+    for i, r in enumerate(out):
+        tid_of.setdefault(i % len(slots), set()).add(r[1])
+    assert all(len(v) == 1 for v in tid_of.values())
+
+
+def test_sharded_map_empty_input():
+    assert list(sharded_map([], [0, 1], _slow_square)) == []
+
+
+def test_sharded_map_worker_error_propagates():
+    def make(dev):
+        def f(x):
+            if x == 7:
+                raise ValueError("frame 7 is bad")
+            return x
+        return f
+    got = []
+    with pytest.raises(ValueError, match="frame 7"):
+        for r in sharded_map(range(100), [0, 1, 2], make):
+            got.append(r)
+    assert got == list(range(len(got))) and len(got) <= 7
+
+
+def test_sharded_map_setup_error_propagates():
+    def make(dev):
+        if dev == 1:
+            raise RuntimeError("no device 1")
+        return lambda x: x
+    with pytest.raises(RuntimeError, match="no device 1"):
+        list(sharded_map(range(10), [0, 1], make))
+
+
+def test_sharded_map_early_consumer_exit_does_not_hang():
+    gen = sharded_map(iter(range(10_000)), [0, 1], _slow_square, queue_depth=1)
+    first = [next(gen) for _ in range(5)]
+    gen.close()
+    assert [r[2] for r in first] == [0, 1, 4, 9, 16]
+
+
+def test_comm_rejects_invisible_devices(gpu_available):
+    if gpu_available:
+        pytest.skip("CPU-only check")
+    with pytest.raises(ValueError, match="not visible"):
+        DeviceComm([0])
+    with pytest.raises(ValueError):
+        DeviceComm([])
+
+
+def test_multi_device_stereo_needs_a_device(gpu_available):
+    if gpu_available:
+        pytest.skip("CPU-only check")
+    with pytest.raises(RuntimeError, match="no HIP device"):
+        MultiDeviceStereo(devices=[0])
+
+
+def test_comm_symbols_bound():
+    lib = _dsx.lib()
+    for n in ("dsx_comm_init_all", "dsx_comm_size", "dsx_bcast", "dsx_comm_destroy"):
+        assert hasattr(lib, n)
+    assert lib.dsx_comm_destroy(None) == 0
+
+
+# ---------------------------------------------------------------- GPU -------------------
+def _devices():
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    return list(range(torch.cuda.device_count()))
+
+
+@pytest.mark.gpu
+def test_comm_broadcast_calibration():
+    import torch
+    devs = _devices()
+    from bench import calibration_params
+    comm = DeviceComm(devs)
+    assert comm.size() == len(devs)
+    got = comm.broadcast_calibration(calibration_params(), root=0)
+    for g in got:
+        assert g["image_width"] == 2964 and abs(g["baseline"] - 0.193001) < 1e-12
+        np.testing.assert_array_equal(g["cam_matrix_L"], np.asarray(calibration_params()["cam_matrix_L"]))
+    # raw broadcast of a larger block (rectification-map sized) from the last device
+    ts = [torch.full((1 << 20,), float(i), device=torch.device("cuda", d)) for i, d in enumerate(devs)]
+    comm.broadcast(ts, root=len(devs) - 1)
+    for t in ts:
+        assert float(t.min()) == float(t.max()) == float(len(devs) - 1)
+    with pytest.raises(ValueError):
+        comm.broadcast(ts[:1] + ts[:1] if len(devs) > 1 else [], root=0)
+    comm.close()
+
+
+@pytest.mark.gpu
+def test_multi_device_stereo_matches_oracle():
+    from depthestimation_amd.synthetic import stereo_pair
+    from oracle.stereo_bm import stereo_bm
+    devs = _devices()
+    kw = dict(min_disp=0, num_disp=64, block_size=5, cost="sad", uniqueness_ratio=10, disp12_max_diff=1,
+              subpixel=True)
+    frames = [stereo_pair(40, 200, 0, 64, seed=100 + i)[:2] for i in range(9)]
+    run = MultiDeviceStereo(devices=devs, **kw)
+    out = list(run.map(iter(frames)))
+    assert len(out) == len(frames)
+    for (L, R), (fixed, flt) in zip(frames, out):
+        ref = stereo_bm(L, R, **kw)
+        np.testing.assert_array_equal(fixed, ref["fixed"])
+        np.testing.assert_array_equal(flt, ref["fixed"].astype(np.float32) / 16.0)
+
+
+@pytest.mark.gpu
+def test_video_estimator_devices_matches_single_device():
+    devs = _devices()
+    from depthestimation_amd import StereoDepthEstimatorVideo
+    from depthestimation_amd.synthetic import stereo_pair
+    frames = [stereo_pair(48, 160, 0, 32, seed=i) for i in range(5)]
+    Ls = [np.repeat(f[0][:, :, None], 3, 2) for f in frames]
+    Rs = [np.repeat(f[1][:, :, None], 3, 2) for f in frames]
+
+    def run(devices):
+        v = StereoDepthEstimatorVideo(list(Ls), list(Rs), fast_mode=True, target_fps=0, use_threading=False,
+                                      devices=devices)
+        v.configure_sgbm(num_disp=32, block_size=5, focal_length=100.0, baseline=0.1)
+        return list(v.estimate_depth())
+
+    a, b = run(None), run(devs)
+    assert len(a) == len(b) == 5
+    for x, y in zip(a, b):
+        np.testing.assert_array_equal(x, y)
