@@ -303,6 +303,11 @@ def main():
                           f"{dt_cpu:.1f} s on {threads} OpenMP threads; oracle/bm_ref.c -O3 -march=native "
                           f"(C restatement of the same contract; OpenCV absent)",
             }
+            # also one core (a shorter sample, whole frames)
+            v1, dt1, n1 = time_cpu_baseline(cfg, L, R, 1, args.cpu_seconds / 3, max_frames=1000)
+            result["cpu_baseline"]["single_core"] = {
+                "value": round(v1, 3), "unit": "Mpix/s", "cores": 1,
+                "sample": f"{n1} whole frames in {dt1:.1f} s on 1 thread", "host_cpus": os.cpu_count()}
         print(json.dumps(result), flush=True)
 
     matcher.close()
