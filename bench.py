@@ -111,6 +111,8 @@ def main():
     ap.add_argument("--batch", type=int, default=1, help="frame pairs per GPU per step (one launch)")
     ap.add_argument("--no-batched", action="store_true", help="skip the secondary batched measurement")
     ap.add_argument("--no-e2e", action="store_true", help="skip the PCIe-inclusive host-buffer measurement")
+    ap.add_argument("--sgm", default=None, choices=["sgbm_3way", "hh4", "sgbm", "hh"],
+                    help="SGM aggregation mode (SURVEY 8f F4; volume path + path passes); not the headline")
     args = ap.parse_args()
 
     import torch
@@ -153,7 +155,13 @@ def main():
 
     kw = dict(min_disp=0, num_disp=cfg["num_disp"], block_size=cfg["block_size"], cost=cfg["cost"],
               uniqueness_ratio=cfg["uniqueness_ratio"], disp12_max_diff=cfg["disp12_max_diff"], subpixel=True)
-    matcher = HipBlockMatcher(device=local, path=args.path, timing=True, grid_blocks=args.grid_blocks, **kw)
+    if args.sgm:
+        if cfg["cost"] != "sad":
+            raise SystemExit("--sgm needs a SAD config")
+        args.path = "volume"
+        args.no_batched = True
+    matcher = HipBlockMatcher(device=local, path=args.path, timing=True, grid_blocks=args.grid_blocks,
+                              aggregation=args.sgm, **kw)
     stream = torch.cuda.current_stream(dev)
 
     def step(i):
@@ -224,7 +232,7 @@ def main():
             "config": {"workload": cfg["desc"], "H": H, "W": W, "num_disp": cfg["num_disp"],
                        "block_size": cfg["block_size"], "cost": cfg["cost"],
                        "uniqueness_ratio": cfg["uniqueness_ratio"], "disp12_max_diff": cfg["disp12_max_diff"],
-                       "subpixel": True, "path": args.path, "frames_per_step_per_gpu": B,
+                       "subpixel": True, "path": args.path, "aggregation": args.sgm or "none", "frames_per_step_per_gpu": B,
                        "parallelism": f"frame-sharded x{ws} (RCCL calibration broadcast, no per-frame collectives)"},
             "roofline": roofline,
         }

@@ -23,6 +23,8 @@ DSX_ENOMEM = -4
 COST = {"sad": 0, "ssd": 1}
 FLOAT_MODE = {"fixed": 0, "parabola": 1}
 PATH = {"fused": 0, "volume": 1}
+# SGM path sets by the reference's sgbm_mode names (stereo_core.py:55-61), include/dsx.h DSX_AGG_*
+AGGREGATION = {None: 0, "none": 0, "sgbm_3way": 3, "hh4": 4, "sgbm": 5, "hh": 8}
 
 # Every symbol include/dsx.h declares (checked by tests/test_abi.py against the header).
 EXPORTS = (
@@ -48,7 +50,10 @@ class DsxParams(ctypes.Structure):
         ("path", ctypes.c_int32),
         ("timing", ctypes.c_int32),
         ("grid_blocks", ctypes.c_int32),
-        ("reserved", ctypes.c_int32 * 5),
+        ("aggregation", ctypes.c_int32),
+        ("p1", ctypes.c_int32),
+        ("p2", ctypes.c_int32),
+        ("reserved", ctypes.c_int32 * 2),
     ]
 
 
@@ -140,7 +145,7 @@ def default_params() -> DsxParams:
 
 def make_params(min_disp=0, num_disp=128, block_size=5, cost="sad", uniqueness_ratio=10,
                 disp12_max_diff=1, subpixel=True, float_mode="fixed", path="fused",
-                timing=False, grid_blocks=0) -> DsxParams:
+                timing=False, grid_blocks=0, aggregation=None, p1=0, p2=0) -> DsxParams:
     p = default_params()
     p.min_disp = int(min_disp)
     p.num_disp = int(num_disp)
@@ -159,6 +164,11 @@ def make_params(min_disp=0, num_disp=128, block_size=5, cost="sad", uniqueness_r
     p.path = PATH[path]
     p.timing = int(bool(timing))
     p.grid_blocks = int(grid_blocks)
+    if aggregation not in AGGREGATION:
+        raise ValueError(f"aggregation must be one of {[k for k in AGGREGATION if k]}")
+    p.aggregation = AGGREGATION[aggregation]
+    p.p1 = int(p1)
+    p.p2 = int(p2)
     return p
 
 

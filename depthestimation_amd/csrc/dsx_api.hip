@@ -70,6 +70,15 @@ int check(const dsx_params *p) {
     if (p->grid_blocks < 0) return fail(DSX_EINVAL, "grid_blocks must be >= 0");
     if (p->min_disp < -2047 || p->min_disp + p->num_disp > 2047)
         return fail(DSX_EINVAL, "min_disp/num_disp out of the int16 x16 fixed-point range");
+    if (p->aggregation != DSX_AGG_NONE) {
+        if (p->aggregation != DSX_AGG_SGBM_3WAY && p->aggregation != DSX_AGG_HH4 && p->aggregation != DSX_AGG_SGBM &&
+            p->aggregation != DSX_AGG_HH)
+            return fail(DSX_EINVAL, "aggregation must be 0, 3 (sgbm_3way), 4 (hh4), 5 (sgbm) or 8 (hh)");
+        if (p->cost != DSX_COST_SAD) return fail(DSX_EINVAL, "SGM aggregation runs on SAD block costs");
+        if (p->num_disp > 256) return fail(DSX_EINVAL, "SGM aggregation supports num_disp <= 256");
+        if (p->p1 > 65535 || p->p2 > 65535 || (p->p1 > 0 && p->p2 > 0 && p->p2 < p->p1))
+            return fail(DSX_EINVAL, "SGM penalties must satisfy 0 < P1 <= P2 <= 65535");
+    }
     dsx::Geometry g;
     if (!pick_geometry(p->num_disp, p->cost, g)) return fail(DSX_EINVAL, "num_disp too large");
     if (max_cost(*p) >= (1ull << (32 - g.DB)) - 1)
@@ -99,6 +108,7 @@ struct dsx_handle {
     int16_t *dStar = nullptr;    // LR check: left winners (or -1) for lr_fixup
     void *vol = nullptr;
     size_t vol_bytes = 0;
+    uint32_t *sgmS = nullptr;  // SGM path sums [H][W][Dp] u32
     // timing
     std::vector<std::string> knames;
     std::vector<double> ktotal;
@@ -117,6 +127,8 @@ void free_buffers(dsx_handle *h) {
     (void)hipFree(h->lrKeys);
     (void)hipFree(h->dStar);
     (void)hipFree(h->vol);
+    (void)hipFree(h->sgmS);
+    h->sgmS = nullptr;
     h->dL = h->dR = nullptr;
     h->dFixed = nullptr;
     h->dFloat = nullptr;
@@ -151,10 +163,11 @@ int ensure_buffers(dsx_handle *h, int H, int W, bool host_staging, int nframes =
         h->lrFrames = nframes;
     }
 
-    if (h->p.path == DSX_PATH_VOLUME && !h->vol) {
+    if ((h->p.path == DSX_PATH_VOLUME || h->p.aggregation) && !h->vol) {
         h->vol_bytes = n * h->g.Dp * cbytes;
         DSX_HIP(hipMalloc(&h->vol, h->vol_bytes));
     }
+    if (h->p.aggregation && !h->sgmS) DSX_HIP(hipMalloc(&h->sgmS, n * h->g.Dp * 4));
     h->cH = H;
     h->cW = W;
     h->cDp = h->g.Dp;
@@ -275,7 +288,7 @@ int run(dsx_handle *h, const void *dL, const void *dR, int H, int W, int64_t str
         hipStream_t st, int nframes = 1, int64_t frame_stride = 0) {
     const int radius = h->p.block_size / 2;
     const bool ssd = h->p.cost == DSX_COST_SSD;
-    if (h->p.path == DSX_PATH_FUSED) {
+    if (h->p.path == DSX_PATH_FUSED && !h->p.aggregation) {
         const bool lr = h->p.disp12_max_diff >= 0;
         dsx::Bm2Args a = base_args(h, H, W, stride);
         a.side = dsx::SIDE_LEFT;
@@ -336,8 +349,36 @@ int run(dsx_handle *h, const void *dL, const void *dR, int H, int W, int64_t str
             a.src = static_cast<const uint8_t *>(dR) + f * frame_stride;
             a.vol = h->vol;
             DSX_LAUNCH(h, "cost_volume", st, dsx::launch_bm2(radius, ssd, h->g.NW, a, st));
+            const bool agg = h->p.aggregation != DSX_AGG_NONE;
+            if (agg) {
+                // SGM: one pass per direction of the mode's path set (oracle/sgm.py DIRECTIONS)
+                static const int dirs[8][2] = {{1, 0}, {-1, 0}, {0, 1}, {0, -1}, {1, 1}, {-1, 1}, {1, -1}, {-1, -1}};
+                static const int set3[] = {0, 1, 2}, set4[] = {0, 1, 2, 3}, set5[] = {0, 1, 2, 4, 5},
+                                 set8[] = {0, 1, 2, 3, 4, 5, 6, 7};
+                const int *set = set3;
+                int nd = 3;
+                if (h->p.aggregation == DSX_AGG_HH4) set = set4, nd = 4;
+                if (h->p.aggregation == DSX_AGG_SGBM) set = set5, nd = 5;
+                if (h->p.aggregation == DSX_AGG_HH) set = set8, nd = 8;
+                const int bs2 = h->p.block_size * h->p.block_size;
+                dsx::SgmArgs sa{};
+                sa.C = static_cast<const uint16_t *>(h->vol);
+                sa.S = h->sgmS;
+                sa.H = H;
+                sa.W = W;
+                sa.D = h->p.num_disp;
+                sa.Dp = h->g.Dp;
+                sa.P1 = h->p.p1 > 0 ? h->p.p1 : 8 * bs2;
+                sa.P2 = h->p.p2 > 0 ? h->p.p2 : 32 * bs2;
+                sa.pads = (uint32_t)((1ull << (32 - h->g.DB)) - 1ull);
+                for (int i = 0; i < nd; ++i) {
+                    sa.dx = dirs[set[i]][0];
+                    sa.dy = dirs[set[i]][1];
+                    DSX_LAUNCH(h, "sgm_path", st, dsx::launch_sgm_path(sa, i == 0, st));
+                }
+            }
             dsx::VolArgs v{};
-            v.vol = h->vol;
+            v.vol = agg ? static_cast<const void *>(h->sgmS) : h->vol;
             v.H = H;
             v.W = W;
             v.m = h->p.min_disp;
@@ -351,9 +392,10 @@ int run(dsx_handle *h, const void *dL, const void *dR, int H, int W, int64_t str
             v.float_mode = h->p.float_mode;
             v.out_fixed = outFixed ? static_cast<int16_t *>(outFixed) + fo : nullptr;
             v.out_float = outFloat ? static_cast<float *>(outFloat) + fo : nullptr;
-            if (dsx::volume_smem_bytes(h->g.TX, ssd, h->g.Dp, h->g.TPP, W) > 160 * 1024)
+            const bool wide = ssd || agg;  // u32 costs: SSD block costs or SGM path sums
+            if (dsx::volume_smem_bytes(h->g.TX, wide, h->g.Dp, h->g.TPP, W) > 160 * 1024)
                 return fail(DSX_EINVAL, "image too wide for the volume path's row kernel");
-            DSX_LAUNCH(h, "volume_wta", st, dsx::launch_volume_wta(h->g.TX, ssd, v, st));
+            DSX_LAUNCH(h, "volume_wta", st, dsx::launch_volume_wta(h->g.TX, wide, v, st));
         }
     }
     return DSX_OK;

@@ -80,6 +80,17 @@ hipError_t launch_lr_fixup(const int16_t *dstar, uint32_t *keys, int H, int W, i
 
 size_t volume_smem_bytes(int TX, bool ssd, int Dp, int TPP, int W);
 
+// Semi-global aggregation (dsx_sgm.hip): one launch per path direction over the K1 volume.
+struct SgmArgs {
+    const uint16_t *C;  // [H][W][Dp] u16 SAD block costs (K1 output)
+    uint32_t *S;        // [H][W][Dp] u32 path sums (written by the first direction, then +=)
+    int H, W, D, Dp;
+    int dx, dy;         // step direction of the path
+    int P1, P2;
+    uint32_t pads;      // S value for disparities >= D (never wins in K2)
+};
+hipError_t launch_sgm_path(const SgmArgs &a, bool first, hipStream_t st);
+
 // Fast-mode epilogue (dsx_post.hip): crop + 3x3 median + optional depth.
 struct PostArgs {
     const float *disp;  // H x W float disparity, row pitch in_pitch elements

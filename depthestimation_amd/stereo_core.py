@@ -10,10 +10,13 @@ Keys added to ``sgbm_params`` (accepted by ``configure_sgbm`` like the reference
   'cost'     : 'sad' | 'ssd'          (block cost; north_star SAD/SSD)
   'subpixel' : bool                   (1/16-px parabola refinement, on by default)
   'device'   : int                    (HIP device of the matcher)
+  'aggregation': 'none' | 'sgm'       ('none', the default, is the north-star block matching;
+                                       'sgm' adds semi-global aggregation over the SAD costs with
+                                       the path set of 'sgbm_mode' and P1 = 8 bs^2, P2 = 32 bs^2 as
+                                       _build_sgbm derives them, stereo_core.py:51-61)
 Keys of the reference that have no block-matching meaning are kept, validated and reported
-but do not change the result: 'prefilter_cap', 'speckle_window_size', 'speckle_range',
-'sgbm_mode' (and the derived P1/P2, stereo_core.py:51-52) belong to OpenCV's semi-global
-aggregation, which the north-star path replaces with plain block matching (SURVEY.md 8a A5').
+but do not change the result: 'prefilter_cap', 'speckle_window_size', 'speckle_range', and
+'sgbm_mode' / P1 / P2 while 'aggregation' is 'none' (SURVEY.md 8a A5').
 
 There is no CPU fallback: without libdsx.so or a HIP device ``compute_disparity`` raises.
 """
@@ -66,6 +69,7 @@ class StereoCore:
             'cost': 'sad',
             'subpixel': True,
             'device': 0,
+            'aggregation': 'none',
         }
         self._build_sgbm()
         self.disparity_map = None
@@ -74,8 +78,10 @@ class StereoCore:
     # -- matcher -------------------------------------------------------------------------
     def _build_sgbm(self):
         """stereo_core.py:44-75 -> HipBlockMatcher. P1/P2 and the mode are recorded for
-        reporting (SGM aggregation is not part of the block-matching contract)."""
+        reporting and drive the optional SGM aggregation ('aggregation': 'sgm')."""
         p = self.sgbm_params
+        if p.get('aggregation', 'none') not in ('none', 'sgm'):
+            raise ValueError("Invalid parameter value for 'aggregation': expected 'none' or 'sgm'")
         self.P1 = 8 * p['block_size'] ** 2
         self.P2 = 32 * p['block_size'] ** 2
         self.mode = p.get('sgbm_mode', 'sgbm_3way') if p.get('sgbm_mode') in _SGBM_MODES else 'sgbm_3way'
@@ -89,6 +95,9 @@ class StereoCore:
             disp12_max_diff=p['disp12_max_diff'],
             subpixel=p['subpixel'],
             device=p['device'],
+            aggregation=self.mode if p.get('aggregation', 'none') == 'sgm' else None,
+            p1=self.P1,
+            p2=self.P2,
         )
         if old is not None:
             old.close()

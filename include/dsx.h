@@ -49,6 +49,15 @@ extern "C" {
 #define DSX_PATH_FUSED 0  /* cost computed in LDS, never written to HBM (default) */
 #define DSX_PATH_VOLUME 1 /* K1 writes the [H][W][D] cost volume to HBM, K2 reduces it */
 
+/* Semi-global aggregation over the SAD block costs: the path sets the
+ * reference selects with sgbm_mode (stereo_core.py:55-61).  With aggregation != 0 the volume
+ * path runs K1, one pass per direction into u32 path sums, then K2 on the sums. */
+#define DSX_AGG_NONE 0
+#define DSX_AGG_SGBM_3WAY 3 /* 'sgbm_3way': left->right, right->left, top->bottom          */
+#define DSX_AGG_HH4 4       /* 'hh4'      : the 3-way set plus bottom->top                   */
+#define DSX_AGG_SGBM 5      /* 'sgbm'     : the 3-way set plus the two top diagonals         */
+#define DSX_AGG_HH 8        /* 'hh'       : all 8 neighbours                                 */
+
 /* Matcher parameters. Field meaning follows StereoCore.sgbm_params
  * (depthlib/stereo_core.py:16-39) for the keys that exist there. */
 typedef struct dsx_params {
@@ -64,7 +73,10 @@ typedef struct dsx_params {
     int32_t timing;           /* 1 = record per-kernel HIP-event timings (dsx_kernel_times)   */
     int32_t grid_blocks;      /* 0 = one persistent block per resident slot; >0 forces the   */
                               /* persistent grid size (tests of the work partition)         */
-    int32_t reserved[5];
+    int32_t aggregation;      /* DSX_AGG_*: 0 = plain block matching (default); otherwise the */
+                              /* SGM path set of 'sgbm_mode' (stereo_core.py:55-61), SAD only */
+    int32_t p1, p2;           /* SGM penalties; <= 0 -> 8*bs^2 / 32*bs^2 (stereo_core.py:51-52) */
+    int32_t reserved[2];
 } dsx_params;
 
 typedef struct dsx_handle dsx_handle;

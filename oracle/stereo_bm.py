@@ -30,6 +30,7 @@ import numpy as np
 
 __all__ = [
     "cost_volume",
+    "wta_epilogue",
     "right_argmin",
     "stereo_bm",
     "bm_bruteforce",
@@ -108,6 +109,13 @@ def stereo_bm(L, R, min_disp: int = 0, num_disp: int = 64, block_size: int = 5,
     StereoCore.compute_disparity returns at stereo_core.py:232), parabola=float32 HxW,
     dstar=int32 HxW (-1 where invalid), dR=int32 HxW or None)."""
     C = cost_volume(L, R, min_disp, num_disp, block_size, cost)
+    return wta_epilogue(C, min_disp, uniqueness_ratio, disp12_max_diff, subpixel)
+
+
+def wta_epilogue(C, min_disp: int, uniqueness_ratio: int = 0, disp12_max_diff: int = -1, subpixel: bool = True):
+    """Per-pixel decision on any int64 cost volume C[y, x, d] (block costs, or SGM path sums
+    from ``oracle.sgm``): lowest-d WTA, uniqueness, LR check, sub-pixel, int16 x16 output -
+    the A5' epilogue described in the module docstring."""
     H, W, D = C.shape
     m = min_disp
     dstar = np.argmin(C, axis=2).astype(np.int64)
