@@ -178,3 +178,31 @@ def test_batch_equals_single(torch_dev, path, cost, bs, D, u, lr):
         np.testing.assert_array_equal(of[i].cpu().numpy(), ref["fixed"])
         np.testing.assert_array_equal(ff[i].cpu().numpy(), ref["disp"])
     m.close()
+
+
+@pytest.mark.parametrize("grid", [1, 7, 23, 61, 200, 999, 0])
+@pytest.mark.parametrize("w8,prio", [("8", "1"), ("11", "1"), ("16", "0")])
+def test_partition_covers_every_row(torch_dev, grid, w8, prio, monkeypatch):
+    """The persistent grid's (frame, strip, row) partition: tiny grids (even split of the
+    linearised space), grids near the strip count (uniform strips) and large grids (clamped-path
+    strips weighted w8/8), with and without the progress-banded priority - all bit-exact, LR on
+    (its right-view winners need every strip) and off, single frame and a 3-frame batch."""
+    torch = torch_dev
+    from depthestimation_amd.matcher import HipBlockMatcher
+    monkeypatch.setenv("DSX_SLOW_W8", w8)
+    monkeypatch.setenv("DSX_PRIO", prio)
+    H, W, D = 53, 700, 64
+    pairs = [stereo_pair(H, W, 0, D, seed=300 + i) for i in range(3)]
+    for lr in (-1, 1):
+        kw = dict(min_disp=0, num_disp=D, block_size=5, cost="sad", uniqueness_ratio=10, disp12_max_diff=lr)
+        m = HipBlockMatcher(grid_blocks=grid, **kw)
+        refs = [stereo_bm(L, R, subpixel=True, **kw)["fixed"] for L, R, _ in pairs]
+        np.testing.assert_array_equal(m.compute(pairs[0][0], pairs[0][1]), refs[0])
+        Lb = torch.from_numpy(np.stack([p[0] for p in pairs])).cuda()
+        Rb = torch.from_numpy(np.stack([p[1] for p in pairs])).cuda()
+        of = torch.empty((3, H, W), dtype=torch.int16, device="cuda")
+        m.compute_batch_device(Lb, Rb, out_fixed=of)
+        torch.cuda.synchronize()
+        for i in range(3):
+            np.testing.assert_array_equal(of[i].cpu().numpy(), refs[i])
+        m.close()
