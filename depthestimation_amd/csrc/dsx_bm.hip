@@ -41,6 +41,12 @@ __device__ __forceinline__ u16x2 as2(uint32_t v) { return __builtin_bit_cast(u16
 __device__ __forceinline__ uint32_t as1(u16x2 v) { return __builtin_bit_cast(uint32_t, v); }
 __device__ __forceinline__ int clampi2(int v, int lo, int hi) { return v < lo ? lo : (v > hi ? hi : v); }
 __device__ __forceinline__ uint32_t umin2(uint32_t a, uint32_t b) { return a < b ? a : b; }
+// a * b + c on 24-bit signed operands (|a|, |b| <= 255 here): one full-rate v_mad_i32_i24
+__device__ __forceinline__ int mad_i24(int a, int b, int c) {
+    int r;
+    asm("v_mad_i32_i24 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+}
 __host__ __device__ constexpr int rnd16(int v) { return (v + 15) & ~15; }
 
 template <int R, bool SSD, int NW>
@@ -294,7 +300,7 @@ __device__ __forceinline__ void bm2_segment(const Bm2Args &a, uint8_t *smem, int
                 if (c0 + c < NC) {
                     if constexpr (SSD) {
                         const int t = (int)refv(rw, c) - (int)sw[c];
-                        cs[c0 + c] += (uint32_t)(t * t);
+                        cs[c0 + c] += (uint32_t)__mul24(t, t);  // v_mul_i32_i24: |t| <= 255
                     } else {
                         const u16x2 Lp = refpk(rw, c), sv = as2(sw[c]);
                         cs[c0 + c] += __builtin_elementwise_max(Lp, sv) - __builtin_elementwise_min(Lp, sv);
@@ -361,7 +367,10 @@ __device__ __forceinline__ void bm2_segment(const Bm2Args &a, uint8_t *smem, int
                         if constexpr (SSD) {
                             const int tn = (int)refv(rn, c) - (int)sn[c];
                             const int to = (int)refv(ro, c) - (int)so[c];
-                            cs[c0 + c] += (uint32_t)(tn * tn) - (uint32_t)(to * to);
+                            const int nto = (int)so[c] - (int)refv(ro, c);
+                            // two v_mad_i32_i24 (cs + tn^2 + to * (-to)), not the 64-bit
+                            // v_mad_u64_u32 that plain int products lowered to
+                            cs[c0 + c] = (uint32_t)mad_i24(to, nto, mad_i24(tn, tn, (int)cs[c0 + c]));
                         } else {
                             const u16x2 Lnp = refpk(rn, c), Lop = refpk(ro, c);
                             const u16x2 vn = as2(sn[c]), vo = as2(so[c]);

@@ -248,3 +248,55 @@ class MultiDeviceStereo:
 
     def map(self, frames: Iterable[Tuple[np.ndarray, np.ndarray]]) -> Iterator[Tuple[np.ndarray, np.ndarray]]:
         return self.map_fn(frames, self._make_matcher_fn)
+
+
+class BandedStereo:
+    """One frame split into horizontal row bands over several GPUs, for latency on large frames
+    ("a single 4K frame can alternatively be row-banded with (block-1)/2 halo rows,
+    no exchange").  Band i computes output rows [y0, y1) from input rows [y0 - r, y1 + r) clipped
+    to the image, r = block_size // 2.  Every term of the A5' contract is row-local except the
+    vertical window, which the halo supplies, and the image's own top / bottom clamp coincides
+    with the sub-image's, so the stitched map equals the single-device result bit for bit.
+    ``devices`` may repeat a device (several bands on one GPU, e.g. for testing)."""
+
+    def __init__(self, devices: Optional[Sequence[int]] = None, **matcher_kw):
+        n = _dsx.device_count()
+        if n == 0:
+            raise RuntimeError("BandedStereo: no HIP device visible (the engine has no CPU fallback)")
+        self.devices = list(range(n)) if devices is None else [int(d) for d in devices]
+        if not self.devices:
+            raise ValueError("devices must not be empty")
+        self.matcher_kw = dict(matcher_kw)
+        self.matcher_kw.pop("device", None)
+        self.r = int(self.matcher_kw.get("block_size", 5)) // 2
+        self._m = [HipBlockMatcher(device=d, **self.matcher_kw) for d in self.devices]
+        from concurrent.futures import ThreadPoolExecutor
+        self._pool = ThreadPoolExecutor(max_workers=len(self.devices))
+
+    def bands(self, H: int) -> List[Tuple[int, int]]:
+        n = min(len(self.devices), H)
+        return [(H * i // n, H * (i + 1) // n) for i in range(n)]
+
+    def compute(self, left: np.ndarray, right: np.ndarray) -> np.ndarray:
+        """int16 x16 disparity of one frame (the cv2 StereoMatcher.compute contract)."""
+        L = np.ascontiguousarray(left, np.uint8)
+        R = np.ascontiguousarray(right, np.uint8)
+        if L.shape != R.shape or L.ndim != 2:
+            raise ValueError("left and right must be uint8 H x W arrays of the same size")
+        H, W = L.shape
+        out = np.empty((H, W), np.int16)
+
+        def band(i, y0, y1):
+            ys, ye = max(0, y0 - self.r), min(H, y1 + self.r)
+            part = self._m[i].compute(L[ys:ye], R[ys:ye])
+            out[y0:y1] = part[y0 - ys:y1 - ys]
+
+        futs = [self._pool.submit(band, i, y0, y1) for i, (y0, y1) in enumerate(self.bands(H))]
+        for f in futs:
+            f.result()
+        return out
+
+    def close(self) -> None:
+        self._pool.shutdown(wait=True)
+        for m in self._m:
+            m.close()
