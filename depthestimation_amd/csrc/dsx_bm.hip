@@ -32,6 +32,7 @@
 
 #include <cstdio>
 #include <cstdlib>
+#include <type_traits>
 
 namespace dsx {
 
@@ -406,29 +407,36 @@ __device__ __forceinline__ void bm2_segment(const Bm2Args &a, uint8_t *smem, int
                 const uint32_t dmE = d0 < D ? (uint32_t)d0 : 0xFFFFFFFFu;
                 const bool lane0 = ln == 0;
                 uint32_t Ae = 0xFFFFFFFFu, Ao = 0xFFFFFFFFu, E = 0xFFFFFFFFu;
+                // FULL: the strip lies inside the image and every lane owns real disparities
+                // (D == Dp), so the per-pixel bounds / lane checks drop out of the unrolled loop
+                auto diag_loop = [&](auto fullc) __attribute__((always_inline)) {
+                    constexpr bool FULL = decltype(fullc)::value;
 #pragma unroll
-                for (int k = 0; k < TX; ++k) {
-                    if (k > 0) acc = acc + cs[k + 2 * R] - cs[k - 1];
-                    if (lane_writes) {
-                        if constexpr (SSD) *reinterpret_cast<uint32_t *>(tb + k * PITCH) = acc;
-                        else *reinterpret_cast<uint32_t *>(tb + k * PITCH) = as1(acc);
-                    }
-                    if (x0 + k < W) {
-                        if constexpr (SSD) {
-                            Ae = umin2(Ae, (acc << ks) | dmE);
-                        } else {  // (C << 16) | d by byte permute
-                            Ae = umin2(Ae, __builtin_amdgcn_perm(as1(acc), (uint32_t)d0, selE));
-                            Ao = umin2(Ao, __builtin_amdgcn_perm(as1(acc), (uint32_t)(d0 + 1), selO));
+                    for (int k = 0; k < TX; ++k) {
+                        if (k > 0) acc = acc + cs[k + 2 * R] - cs[k - 1];
+                        if (FULL || lane_writes) {
+                            if constexpr (SSD) *reinterpret_cast<uint32_t *>(tb + k * PITCH) = acc;
+                            else *reinterpret_cast<uint32_t *>(tb + k * PITCH) = as1(acc);
+                        }
+                        if (FULL || x0 + k < W) {
+                            if constexpr (SSD) {
+                                Ae = umin2(Ae, (acc << ks) | dmE);
+                            } else {  // (C << 16) | d by byte permute
+                                Ae = umin2(Ae, __builtin_amdgcn_perm(as1(acc), (uint32_t)d0, selE));
+                                Ao = umin2(Ao, __builtin_amdgcn_perm(as1(acc), (uint32_t)(d0 + 1), selO));
+                            }
+                        }
+                        if (k < TX - 1) {
+                            const uint32_t top = SSD ? Ae : Ao;
+                            const uint32_t F = (uint32_t)__builtin_amdgcn_mov_dpp((int)top, 0x13C, 0xF, 0xF, false);  // wave_ror:1
+                            E = (uint32_t)__builtin_amdgcn_update_dpp((int)F, (int)E, 0x138, 0xF, 0xF, false);  // wave_shr:1, lane 0 <- F
+                            if constexpr (!SSD) Ao = Ae;
+                            Ae = lane0 ? 0xFFFFFFFFu : F;
                         }
                     }
-                    if (k < TX - 1) {
-                        const uint32_t top = SSD ? Ae : Ao;
-                        const uint32_t F = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)top, 0x13C, 0xF, 0xF, false);  // wave_ror:1
-                        E = (uint32_t)__builtin_amdgcn_update_dpp((int)F, (int)E, 0x138, 0xF, 0xF, false);        // wave_shr:1, lane 0 <- F
-                        if constexpr (!SSD) Ao = Ae;
-                        Ae = lane0 ? 0xFFFFFFFFu : F;
-                    }
-                }
+                };
+                if (x0 + TX <= W && D == Dp) diag_loop(std::true_type{});
+                else diag_loop(std::false_type{});
                 uint32_t *krow = a.lr_keys + fout + (long)y * W;
                 const int dtop = (wv + 1) * G::LDW - 1;            // disparity of the wave's top slot
                 const int xe = x0 + (TX - 2 - ln) - m - dtop;       // E lane j: exit of pixel TX-2-j
