@@ -159,7 +159,10 @@ int ensure_buffers(dsx_handle *h, int H, int W, bool host_staging, int nframes =
         h->lrFrames = 0;
         DSX_HIP(hipMalloc(&h->lrKeys, n * nframes * 4));
         DSX_HIP(hipMalloc(&h->dStar, n * nframes * 2));
-        DSX_HIP(hipMemset(h->lrKeys, 0xFF, n * nframes * 4));  // lr_fixup restores ~0 after every frame
+        // lr_fixup restores ~0 after every frame.  The handle's streams are non-blocking, so the
+        // fill must have landed before any later launch: wait for it here (allocation time only)
+        DSX_HIP(hipMemsetAsync(h->lrKeys, 0xFF, n * nframes * 4, nullptr));
+        DSX_HIP(hipStreamSynchronize(nullptr));
         h->lrFrames = nframes;
     }
 

@@ -32,6 +32,7 @@
 
 #include <cstdio>
 #include <cstdlib>
+#include <mutex>
 #include <type_traits>
 
 namespace dsx {
@@ -503,30 +504,69 @@ __device__ __forceinline__ void bm2_segment(const Bm2Args &a, uint8_t *smem, int
                     bs[i] = umin2(mm.x, mm.y);
                 }
             }
-            uint32_t lmin = bs[0];
-#pragma unroll
-            for (int i = 1; i < NB; ++i) lmin = umin2(lmin, bs[i]);
-            const uint32_t cb = gmin<TPP>(lmin);
-            int bsel = -1;
-#pragma unroll
-            for (int i = NB - 1; i >= 0; --i) bsel = bs[i] == cb ? i : bsel;
-            uint32_t dl = 0xFFFFu;
-            if (bsel >= 0) {
-                uint32_t c8[8];
-                if constexpr (SSD) {
-                    const uint4 v0 = *reinterpret_cast<const uint4 *>(px + 32 * bsel);
-                    const uint4 v1 = *reinterpret_cast<const uint4 *>(px + 32 * bsel + 16);
-                    c8[0] = v0.x; c8[1] = v0.y; c8[2] = v0.z; c8[3] = v0.w;
-                    c8[4] = v1.x; c8[5] = v1.y; c8[6] = v1.z; c8[7] = v1.w;
-                } else {
-                    const uint4 v = *reinterpret_cast<const uint4 *>(px + 16 * bsel);
-                    c8[0] = v.x & 0xFFFFu; c8[1] = v.x >> 16; c8[2] = v.y & 0xFFFFu; c8[3] = v.y >> 16;
-                    c8[4] = v.z & 0xFFFFu; c8[5] = v.z >> 16; c8[6] = v.w & 0xFFFFu; c8[7] = v.w >> 16;
+            // Two argmin forms, chosen per instantiation from measurements (r01e): the key tree
+            // wins on the LR pass (C3, C4) and 15x15 windows (C5); the compare/select scan keeps
+            // the SIDE 0 pass at <= 11x11 at 151 VGPRs (the key tree costs C2 +7 %).
+            constexpr bool KEYS = SIDE == 3 || R >= 6;
+            uint32_t cb, dl;
+            if constexpr (KEYS) {
+                // lowest-d argmin without compare/select scans: keys (cost << GB | global block) give
+                // the minimum and its lowest block in one min tree; the owning lane then keys the 8
+                // costs of that block (cost << 3 | e).  Costs < 2^24 (SSD) / 2^16 (SAD), GB <= 6.
+                constexpr int GB = Dp / 8 <= 16 ? 4 : (Dp / 8 <= 32 ? 5 : 6);
+                uint32_t kmin = 0xFFFFFFFFu;
+    #pragma unroll
+                for (int i = 0; i < NB; ++i) kmin = umin2(kmin, (bs[i] << GB) | (uint32_t)(h * NB + i));
+                kmin = gmin<TPP>(kmin);
+                cb = kmin >> GB;
+                const int gblk = (int)(kmin & ((1u << GB) - 1u));
+                dl = 0xFFFFu;
+                if (gblk / NB == h) {
+                    const int bsel = gblk - h * NB;
+                    uint32_t k8 = 0xFFFFFFFFu;
+                    if constexpr (SSD) {
+                        const uint4 v0 = *reinterpret_cast<const uint4 *>(px + 32 * bsel);
+                        const uint4 v1 = *reinterpret_cast<const uint4 *>(px + 32 * bsel + 16);
+                        const uint32_t c8[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
+    #pragma unroll
+                        for (int q = 0; q < 8; ++q) k8 = umin2(k8, (c8[q] << 3) | (uint32_t)q);
+                    } else {
+                        const uint4 v = *reinterpret_cast<const uint4 *>(px + 16 * bsel);
+                        const uint32_t w4[4] = {v.x, v.y, v.z, v.w};
+    #pragma unroll
+                        for (int q = 0; q < 4; ++q) {
+                            k8 = umin2(k8, ((w4[q] & 0xFFFFu) << 3) | (uint32_t)(2 * q));
+                            k8 = umin2(k8, ((w4[q] >> 16) << 3) | (uint32_t)(2 * q + 1));
+                        }
+                    }
+                    dl = (uint32_t)(h * DSL + 8 * bsel + (int)(k8 & 7u));
                 }
-                int e = 7;
-#pragma unroll
-                for (int q = 6; q >= 0; --q) e = c8[q] == cb ? q : e;
-                dl = (uint32_t)(h * DSL + 8 * bsel + e);
+            } else {
+                uint32_t lmin = bs[0];
+    #pragma unroll
+                for (int i = 1; i < NB; ++i) lmin = umin2(lmin, bs[i]);
+                cb = gmin<TPP>(lmin);
+                int bsel = -1;
+    #pragma unroll
+                for (int i = NB - 1; i >= 0; --i) bsel = bs[i] == cb ? i : bsel;
+                dl = 0xFFFFu;
+                if (bsel >= 0) {
+                    uint32_t c8[8];
+                    if constexpr (SSD) {
+                        const uint4 v0 = *reinterpret_cast<const uint4 *>(px + 32 * bsel);
+                        const uint4 v1 = *reinterpret_cast<const uint4 *>(px + 32 * bsel + 16);
+                        c8[0] = v0.x; c8[1] = v0.y; c8[2] = v0.z; c8[3] = v0.w;
+                        c8[4] = v1.x; c8[5] = v1.y; c8[6] = v1.z; c8[7] = v1.w;
+                    } else {
+                        const uint4 v = *reinterpret_cast<const uint4 *>(px + 16 * bsel);
+                        c8[0] = v.x & 0xFFFFu; c8[1] = v.x >> 16; c8[2] = v.y & 0xFFFFu; c8[3] = v.y >> 16;
+                        c8[4] = v.z & 0xFFFFu; c8[5] = v.z >> 16; c8[6] = v.w & 0xFFFFu; c8[7] = v.w >> 16;
+                    }
+                    int e = 7;
+    #pragma unroll
+                    for (int q = 6; q >= 0; --q) e = c8[q] == cb ? q : e;
+                    dl = (uint32_t)(h * DSL + 8 * bsel + e);
+                }
             }
             const int b = (int)gmin<TPP>(dl);
             const long o = fout + (long)y * W + x;
@@ -742,6 +782,8 @@ static hipError_t launch_bm2_side(const Bm2Args &a, hipStream_t st) {
     hipError_t e = hipGetDevice(&dev);
     if (e != hipSuccess) return e;
     if (dev < 0 || dev >= 64) return hipErrorInvalidDevice;
+    static std::mutex init_mu;  // first launch per device may come from several host threads
+    std::lock_guard<std::mutex> lock(init_mu);
     if (!blocks_per_cu[dev]) {
         e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, G::SMEM);
         if (e != hipSuccess) return e;
