@@ -199,6 +199,32 @@ def main():
         torch.cuda.synchronize(dev)
         assert np.array_equal(out_fixed[0].cpu().numpy(), ref["fixed"]), "bench frame differs from oracle"
 
+    # secondary, never `value`: host numpy frames -> pinned -> H2D -> matcher -> D2H of the int16 map,
+    # two worker streams per GPU (multigpu.MultiDeviceStereo), every rank on its own GPU and the
+    # whole-job rate over the slowest rank (SURVEY 8e / BASELINE.md: end-to-end scaling next to
+    # the device-resident `value`)
+    e2e = None
+    if not args.no_e2e and args.path == "fused" and not args.sgm:
+        from depthestimation_amd.multigpu import MultiDeviceStereo
+        run = MultiDeviceStereo(devices=[local], streams_per_device=2, **kw)
+        ne = 64
+        src = [(hostL[i % nres], hostR[i % nres]) for i in range(ne)]
+        for _ in run.map(iter(src[:4])):
+            pass
+        if ws > 1:
+            dist.barrier()
+        t1 = time.perf_counter()
+        n_done = sum(1 for _ in run.map(iter(src)))
+        et = time.perf_counter() - t1
+        if ws > 1:
+            t = torch.tensor([et], dtype=torch.float64, device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            et = float(t.item())
+        e2e = {"value": round(H * W * n_done * ws / et / 1e6, 1), "unit": "Mpix/s", "frames_per_gpu": n_done,
+               "ms_per_frame_per_gpu": round(et / n_done * 1e3, 4),
+               "note": "secondary, PCIe-inclusive: host uint8 pairs in, int16 x16 out, 2 worker streams per GPU "
+                       "(multigpu.MultiDeviceStereo), all ranks, max time over ranks"}
+
     result = None
     if rank == 0:
         px_total = H * W * B * args.steps * ws
@@ -284,22 +310,8 @@ def main():
             result["roofline_volume"] = rv
             vm.close()
 
-        if not args.no_e2e and ws == 1 and args.path == "fused":
-            # secondary, never `value`: host numpy frames -> pinned -> H2D -> matcher -> D2H, two
-            # workers (streams) on this GPU via multigpu.MultiDeviceStereo (SURVEY 8e end-to-end)
-            from depthestimation_amd.multigpu import MultiDeviceStereo
-            run = MultiDeviceStereo(devices=[local], streams_per_device=2, **kw)
-            ne = 64
-            src = [(hostL[i % nres], hostR[i % nres]) for i in range(ne)]
-            for _ in run.map(iter(src[:4])):
-                pass
-            t1 = time.perf_counter()
-            n_done = sum(1 for _ in run.map(iter(src)))
-            et = time.perf_counter() - t1
-            result["e2e_host"] = {"value": round(H * W * n_done / et / 1e6, 1), "unit": "Mpix/s", "frames": n_done,
-                                  "ms_per_frame": round(et / n_done * 1e3, 4),
-                                  "note": "secondary, PCIe-inclusive: host uint8 pairs in, int16 x16 out, 2 worker "
-                                          "streams on one GPU (multigpu.MultiDeviceStereo)"}
+        if e2e is not None:
+            result["e2e_host"] = e2e
 
         if not args.no_cpu_baseline and ws == 1:
             L, R = host_first

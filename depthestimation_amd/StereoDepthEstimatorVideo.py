@@ -19,6 +19,8 @@ from __future__ import annotations
 import time
 import warnings
 
+import numpy as np
+
 from .input import stereo_stream
 from .sharding import DistEnv
 from .stereo_core import StereoCore
@@ -98,11 +100,27 @@ class StereoDepthEstimatorVideo:
         ds, fast = self.downscale_factor, self.fast_mode
 
         def make(dev):
+            import torch
+            torch.cuda.set_device(dev)
             core = StereoCore(downscale_factor=ds, fast_mode=fast)
             core.sgbm_params.update(params)
             core.sgbm_params['device'] = dev
             core._build_sgbm()
-            return lambda pair: core.estimate_depth(pair[0], pair[1])[1]
+            if core.sgbm_params.get('hole_filling', False):  # Telea inpainting: host path
+                return lambda pair: core.estimate_depth(pair[0], pair[1])[1]
+            stream = torch.cuda.Stream(device=dev)
+
+            def run(pair):
+                # device pipeline (rectify/gray -> match -> post-process -> depth in HBM), equal
+                # bit for bit to the host path (tests/test_gpu_host_api.py)
+                with torch.cuda.stream(stream):
+                    tl = torch.from_numpy(np.ascontiguousarray(pair[0])).to(dev, non_blocking=True)
+                    tr = torch.from_numpy(np.ascontiguousarray(pair[1])).to(dev, non_blocking=True)
+                    _, depth = core.estimate_depth_device(tl, tr, stream=stream)
+                    out = None if depth is None else depth.cpu().numpy()
+                stream.synchronize()
+                return out
+            return run
 
         runner = MultiDeviceStereo(devices=self.devices, streams_per_device=1)
         frame_start_time = time.time()

@@ -261,8 +261,41 @@ class StereoCore:
         return Z
 
     def estimate_depth(self, left_source, right_source) -> Tuple[np.ndarray, Optional[np.ndarray]]:
-        """stereo_core.py:274-293."""
+        """stereo_core.py:274-293.  Host arrays in, host arrays out; the work runs on the
+        device pipeline (``estimate_depth_device``: rectify / gray, matcher, post-processing,
+        depth, all in HBM - bit-identical to the host steps, tests/test_gpu_host_api.py) unless
+        hole filling (Telea inpainting, host only) is on or the matcher was replaced."""
         if left_source is None or right_source is None:
             raise ValueError("Left and right sources must be set before estimating depth.")
+        if self._device_pipeline_ok(left_source, right_source):
+            import torch
+            dev = torch.device("cuda", int(self.sgbm_params.get('device', 0)))
+            tl = torch.from_numpy(np.ascontiguousarray(left_source)).to(dev)
+            tr = torch.from_numpy(np.ascontiguousarray(right_source)).to(dev)
+            d, z = self.estimate_depth_device(tl, tr)
+            self.left_rectified = self.left_rectified.cpu().numpy()
+            self.right_rectified = self.right_rectified.cpu().numpy()
+            self.disparity_map = d.cpu().numpy()
+            self.depth_map = None if z is None else z.cpu().numpy()
+            return self.disparity_map, self.depth_map
         self.left_rectified, self.right_rectified = self._prepare_rectified(left_source, right_source)
         return self._process_pair(self.left_rectified, self.right_rectified)
+
+    def _device_pipeline_ok(self, left, right) -> bool:
+        if self.sgbm_params.get('hole_filling', False) or 'compute_disparity' in self.__dict__:
+            return False
+        if not (isinstance(left, np.ndarray) and isinstance(right, np.ndarray)):
+            return False
+        if left.dtype != np.uint8 or right.dtype != np.uint8 or left.ndim not in (2, 3) or left.shape != right.shape:
+            return False
+        if left.ndim == 3 and left.shape[2] != 3:
+            return False
+        p = self.sgbm_params
+        if all(p.get(k) is not None for k in ('cam_matrix_L', 'cam_matrix_R', 'baseline', 'image_width', 'image_height')):
+            if tuple(left.shape[:2]) != (int(p['image_height']), int(p['image_width'])):
+                return False  # rectify_images' resize-on-mismatch path (rectify.py:92-105) is host-side
+        try:
+            import torch
+        except ImportError:  # pragma: no cover - torch is part of the image
+            return False
+        return torch.cuda.is_available()
