@@ -30,6 +30,16 @@
 //                     (atomicMin across strips), checked afterwards by lr_fixup
 #include "dsx_internal.h"
 
+// Register budget (waves per SIMD) the fused pass is compiled for, measured per cost (r01e): SAD at 4
+// waves spills in the row loop (C2 +45 %); SSD blocks of >= 4 waves (D > 128) gain at 4 despite init
+// spills (C3 392 -> 350 us); other SSD shapes were not measured and keep 3.
+#ifndef DSX_WPE
+#define DSX_WPE 3
+#endif
+#ifndef DSX_WPE_SSD
+#define DSX_WPE_SSD 4
+#endif
+
 #include <cstdio>
 #include <cstdlib>
 #include <mutex>
@@ -637,7 +647,7 @@ __device__ __forceinline__ void bm2_segment(const Bm2Args &a, uint8_t *smem, int
 }
 
 template <int R, bool SSD, int NW, int SIDE>
-__global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(3))) void bm2(Bm2Args a) {
+__global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu((SSD && NW >= 4) ? DSX_WPE_SSD : DSX_WPE))) void bm2(Bm2Args a) {
     using G = Geo<R, SSD, NW>;
     constexpr int TX = G::TX, NT = G::NT, NC = G::NC, NJ = G::NJ;
     constexpr int side = SIDE;

@@ -4,6 +4,6 @@
 set -e
 cd "$(dirname "$0")/../depthestimation_amd/csrc"
 for e in "$@"; do
-  make -s -j8 OBJ=build_e$e OUT=../exp FLAGS="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -Wall -Wno-unused-function -DDSX_EXP=$e" ../exp/libdsx.so >/dev/null
+  make -s -j8 OBJ=build_e$e OUT=../exp FLAGS="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -Wall -Wno-unused-function -DDSX_EXP=$e $EXTRA" ../exp/libdsx.so >/dev/null
   mv ../exp/libdsx.so ../exp/libdsx_e$e.so
 done
