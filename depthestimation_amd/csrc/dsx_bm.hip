@@ -597,18 +597,31 @@ __device__ __forceinline__ void bm2_segment(const Bm2Args &a, uint8_t *smem, int
                     for (int t = 0; t < 2; ++t) {
                         const int ib = t == 0 ? ib0 : ib1;
                         if (ib >= 0 && ib < NB && (t == 0 || ib1 != ib0)) {
+                            // one wide read of the block, selects instead of per-element branches
+                            uint32_t c8[8];
+                            if constexpr (SSD) {
+                                const uint4 v0 = *reinterpret_cast<const uint4 *>(px + 32 * ib);
+                                const uint4 v1 = *reinterpret_cast<const uint4 *>(px + 32 * ib + 16);
+                                c8[0] = v0.x; c8[1] = v0.y; c8[2] = v0.z; c8[3] = v0.w;
+                                c8[4] = v1.x; c8[5] = v1.y; c8[6] = v1.z; c8[7] = v1.w;
+                            } else {
+                                const uint4 v = *reinterpret_cast<const uint4 *>(px + 16 * ib);
+                                c8[0] = v.x & 0xFFFFu; c8[1] = v.x >> 16; c8[2] = v.y & 0xFFFFu; c8[3] = v.y >> 16;
+                                c8[4] = v.z & 0xFFFFu; c8[5] = v.z >> 16; c8[6] = v.w & 0xFFFFu; c8[7] = v.w >> 16;
+                            }
 #pragma unroll
                             for (int e = 0; e < 8; ++e) {
-                                uint32_t c;
-                                if constexpr (SSD) c = reinterpret_cast<const uint32_t *>(px)[8 * ib + e];
-                                else c = reinterpret_cast<const uint16_t *>(px)[8 * ib + e];
                                 const int dd = 8 * ib + e - rel;
-                                if (dd > 1 || dd < -1) nm = umin2(nm, c);
+                                nm = (dd > 1 || dd < -1) ? umin2(nm, c8[e]) : nm;
                             }
                         }
                     }
                     nm = gmin<TPP>(nm);
-                    if ((uint64_t)nm * (uint64_t)(100 - a.uniq) < (uint64_t)cb * 100u) valid = false;
+                    // real costs are < min(padv, 2^24) (SSD 15x15 max 14.6M); a larger minimum is
+                    // padding only, i.e. no competitor (the oracle's "no far d"), and the products
+                    // then fit 32 bits
+                    const uint32_t real_max = padv < (1u << 24) ? padv : (1u << 24);
+                    if (nm < real_max && nm * (uint32_t)(100 - a.uniq) < cb * 100u) valid = false;
                 }
                 int32_t f = b * 16;
                 float pf = (float)(m + b);

@@ -206,3 +206,16 @@ def test_partition_covers_every_row(torch_dev, grid, w8, prio, monkeypatch):
         for i in range(3):
             np.testing.assert_array_equal(of[i].cpu().numpy(), refs[i])
         m.close()
+
+
+@pytest.mark.parametrize("path", ["fused", "volume"])
+@pytest.mark.parametrize("cost", ["sad", "ssd"])
+@pytest.mark.parametrize("D", [1, 2, 3, 5])
+def test_tiny_disparity_ranges_with_uniqueness(torch_dev, path, cost, D):
+    """D <= 2 leaves no disparity with |d - d*| > 1: uniqueness must not fire on the padded
+    disparities (the oracle's 'no competitor'); D = 3, 5 have one or more real competitors."""
+    L, R, _ = stereo_pair(23, 70, 0, max(D, 1), seed=D + (7 if cost == "ssd" else 0))
+    for u in (1, 50, 99):
+        kw = dict(min_disp=0, num_disp=D, block_size=3, cost=cost, uniqueness_ratio=u, disp12_max_diff=1)
+        fixed, _ = _run(L, R, path=path, **kw)
+        np.testing.assert_array_equal(fixed, stereo_bm(L, R, subpixel=True, **kw)["fixed"])
