@@ -101,6 +101,7 @@ struct dsx_handle {
     // buffer cache keyed by (H, W, geometry); single entry like RectificationCache (rectify.py:49-50)
     int cH = 0, cW = 0, cDp = 0, cCostBytes = 0;
     int lrFrames = 0;  // frames the LR buffers hold
+    int lrParity = 0;  // which half of lrKeys the next frame's left pass fills
     uint8_t *dL = nullptr, *dR = nullptr;
     int16_t *dFixed = nullptr;
     float *dFloat = nullptr;
@@ -157,13 +158,14 @@ int ensure_buffers(dsx_handle *h, int H, int W, bool host_staging, int nframes =
         h->lrKeys = nullptr;
         h->dStar = nullptr;
         h->lrFrames = 0;
-        DSX_HIP(hipMalloc(&h->lrKeys, n * nframes * 4));
+        DSX_HIP(hipMalloc(&h->lrKeys, 2 * n * nframes * 4));  // two halves: this frame / next frame
         DSX_HIP(hipMalloc(&h->dStar, n * nframes * 2));
         // lr_fixup restores ~0 after every frame.  The handle's streams are non-blocking, so the
         // fill must have landed before any later launch: wait for it here (allocation time only)
-        DSX_HIP(hipMemsetAsync(h->lrKeys, 0xFF, n * nframes * 4, nullptr));
+        DSX_HIP(hipMemsetAsync(h->lrKeys, 0xFF, 2 * n * nframes * 4, nullptr));
         DSX_HIP(hipStreamSynchronize(nullptr));
         h->lrFrames = nframes;
+        h->lrParity = 0;
     }
 
     if ((h->p.path == DSX_PATH_VOLUME || h->p.aggregation) && !h->vol) {
@@ -305,7 +307,7 @@ int run(dsx_handle *h, const void *dL, const void *dR, int H, int W, int64_t str
             // the left pass also builds the right-view winners (every strip: a right pixel's
             // diagonal starts left of the valid band); lr_fixup applies the check afterwards
             a.side = dsx::SIDE_LEFT_LR;
-            a.lr_keys = h->lrKeys;
+            a.lr_keys = h->lrKeys + (size_t)h->lrParity * H * W * h->lrFrames;
             a.dstar = h->dStar;
             a.kshift = ssd ? h->g.DB : 16;
         } else {
@@ -329,8 +331,10 @@ int run(dsx_handle *h, const void *dL, const void *dR, int H, int W, int64_t str
         DSX_LAUNCH(h, "bm_pass_left", st, dsx::launch_bm2(radius, ssd, h->g.NW, a, st));
         if (lr)
             DSX_LAUNCH(h, "lr_fixup", st,
-                       dsx::launch_lr_fixup(h->dStar, h->lrKeys, H * nframes, W, h->p.min_disp, h->p.disp12_max_diff, a.kshift,
+                       dsx::launch_lr_fixup(h->dStar, a.lr_keys, h->lrKeys + (size_t)(h->lrParity ^ 1) * H * W * h->lrFrames,
+                                            H * nframes, W, h->p.min_disp, h->p.disp12_max_diff, a.kshift,
                                             a.out_fixed, a.out_float, st));
+        if (lr) h->lrParity ^= 1;
         if (tl) {
             std::vector<uint64_t> host(12 * 65536);
             DSX_HIP(hipStreamSynchronize(st));
@@ -692,7 +696,7 @@ int dsx_workspace_bytes(dsx_handle *h, int64_t *bytes) {
     const int64_t n = (int64_t)h->cH * h->cW;
     int64_t b = 0;
     if (h->dL) b += n * (1 + 1 + 2 + 4);
-    if (h->lrKeys) b += n * 6 * h->lrFrames;
+    if (h->lrKeys) b += n * 10 * h->lrFrames;
     b += (int64_t)h->vol_bytes;
     *bytes = b;
     return DSX_OK;

@@ -201,31 +201,30 @@ __global__ __launch_bounds__(kVolThreads) void vol_wta(VolArgs a) {
 // lr_fixup: the left-right check of the fused path (stereo_core.py:69 disp12MaxDiff) once the
 // left pass has built the right-view winners by atomicMin over its cost diagonals.
 // ---------------------------------------------------------------------------------------
-__global__ __launch_bounds__(1024) void lr_fixup(const int16_t *__restrict__ dstar, uint32_t *__restrict__ keys, int H,
-                                               int W, int m, int lr, int kshift, int16_t *out_fixed, float *out_float) {
-    // one block per row; afterwards the row's keys are reset to ~0 for the next frame (the
-    // buffer is initialised once at allocation), so no per-frame memset is needed
-    const int y = blockIdx.x;
+__global__ __launch_bounds__(256) void lr_fixup(const int16_t *__restrict__ dstar, const uint32_t *__restrict__ keys,
+                                              uint32_t *__restrict__ keys_next, int H, int W, int m, int lr, int kshift,
+                                              int16_t *out_fixed, float *out_float) {
+    // elementwise over H x W: the keys read here (this frame's buffer) are never written, and the
+    // other buffer (next frame's) is reset to ~0 - so no row-wide barrier is needed
     const uint32_t mask = (1u << kshift) - 1u;
-    const int16_t *drow = dstar + (int64_t)y * W;
-    uint32_t *krow = keys + (int64_t)y * W;
-    for (int x = threadIdx.x; x < W; x += 1024) {
-        const int b = drow[x];
-        if (b < 0) continue;
-        const int df = (int)(krow[x - m - b] & mask) - b;  // x - m - b in [0, W-1] for valid-band pixels
-        if (df > lr || df < -lr) {
-            const int64_t o = (int64_t)y * W + x;
-            if (out_fixed) out_fixed[o] = (int16_t)((m - 1) * 16);
-            if (out_float) out_float[o] = (float)(m - 1);
-        }
+    const int y = blockIdx.y;
+    const int x = blockIdx.x * blockDim.x + threadIdx.x;
+    if (x >= W) return;
+    const int64_t i = (int64_t)y * W + x;
+    keys_next[i] = 0xFFFFFFFFu;
+    const int b = dstar[i];
+    if (b < 0) return;
+    const int df = (int)(keys[i - m - b] & mask) - b;  // x - m - b in [0, W-1] for valid-band pixels
+    if (df > lr || df < -lr) {
+        if (out_fixed) out_fixed[i] = (int16_t)((m - 1) * 16);
+        if (out_float) out_float[i] = (float)(m - 1);
     }
-    __syncthreads();
-    for (int x = threadIdx.x; x < W; x += 1024) krow[x] = 0xFFFFFFFFu;
 }
 
-hipError_t launch_lr_fixup(const int16_t *dstar, uint32_t *keys, int H, int W, int m, int lr, int kshift,
-                           int16_t *out_fixed, float *out_float, hipStream_t st) {
-    hipLaunchKernelGGL(lr_fixup, dim3(H), dim3(1024), 0, st, dstar, keys, H, W, m, lr, kshift, out_fixed, out_float);
+hipError_t launch_lr_fixup(const int16_t *dstar, const uint32_t *keys, uint32_t *keys_next, int H, int W, int m,
+                           int lr, int kshift, int16_t *out_fixed, float *out_float, hipStream_t st) {
+    hipLaunchKernelGGL(lr_fixup, dim3((unsigned)((W + 255) / 256), (unsigned)H), dim3(256), 0, st, dstar, keys, keys_next,
+                       H, W, m, lr, kshift, out_fixed, out_float);
     return hipGetLastError();
 }
 
