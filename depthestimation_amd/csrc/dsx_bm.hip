@@ -53,6 +53,14 @@ __device__ __forceinline__ u16x2 as2(uint32_t v) { return __builtin_bit_cast(u16
 __device__ __forceinline__ uint32_t as1(u16x2 v) { return __builtin_bit_cast(uint32_t, v); }
 __device__ __forceinline__ int clampi2(int v, int lo, int hi) { return v < lo ? lo : (v > hi ? hi : v); }
 __device__ __forceinline__ uint32_t umin2(uint32_t a, uint32_t b) { return a < b ? a : b; }
+// Packed u16 pairs summed with 32-bit v_add_u32 / v_sub_u32, which issue in 2 cycles against 4 for
+// every v_pk_* op (tools/ubench3.hip).  Exact whenever no half carries or borrows: absolute
+// differences (max - min >= 0), column sums (<= 255 (2R+1)) plus one difference, box sums
+// (<= 57,375) plus one column sum, and results that are themselves non-negative sums.
+__device__ __forceinline__ u16x2 absdiff2(u16x2 a, u16x2 b) {
+    return as2(as1(__builtin_elementwise_max(a, b)) - as1(__builtin_elementwise_min(a, b)));
+}
+__device__ __forceinline__ u16x2 add_sub2(u16x2 a, u16x2 p, u16x2 q) { return as2(as1(a) + as1(p) - as1(q)); }
 // a * b + c on 24-bit signed operands (|a|, |b| <= 255 here): one full-rate v_mad_i32_i24
 __device__ __forceinline__ int mad_i24(int a, int b, int c) {
     int r;
@@ -315,7 +323,7 @@ __device__ __forceinline__ void bm2_segment(const Bm2Args &a, uint8_t *smem, int
                         cs[c0 + c] += (uint32_t)__mul24(t, t);  // v_mul_i32_i24: |t| <= 255
                     } else {
                         const u16x2 Lp = refpk(rw, c), sv = as2(sw[c]);
-                        cs[c0 + c] += __builtin_elementwise_max(Lp, sv) - __builtin_elementwise_min(Lp, sv);
+                        cs[c0 + c] = as2(as1(cs[c0 + c]) + as1(absdiff2(Lp, sv)));
                     }
                 }
             }
@@ -386,9 +394,7 @@ __device__ __forceinline__ void bm2_segment(const Bm2Args &a, uint8_t *smem, int
                         } else {
                             const u16x2 Lnp = refpk(rn, c), Lop = refpk(ro, c);
                             const u16x2 vn = as2(sn[c]), vo = as2(so[c]);
-                            cs[c0 + c] = cs[c0 + c] +
-                                         (__builtin_elementwise_max(Lnp, vn) - __builtin_elementwise_min(Lnp, vn)) -
-                                         (__builtin_elementwise_max(Lop, vo) - __builtin_elementwise_min(Lop, vo));
+                            cs[c0 + c] = add_sub2(cs[c0 + c], absdiff2(Lnp, vn), absdiff2(Lop, vo));
                         }
                     }
                 }
@@ -401,7 +407,10 @@ __device__ __forceinline__ void bm2_segment(const Bm2Args &a, uint8_t *smem, int
             uint8_t *tb = tile + d0 * CB;
             acc_t acc = cs[0];
 #pragma unroll
-            for (int c = 1; c <= 2 * R; ++c) acc += cs[c];
+            for (int c = 1; c <= 2 * R; ++c) {
+                if constexpr (SSD) acc += cs[c];
+                else acc = as2(as1(acc) + as1(cs[c]));
+            }
             if constexpr (side == 3) {
                 // Right-view winners along the tile's diagonals: C_R(xr, d) = C(xr + m + d, d), so
                 // right pixel xr collects keys (C << s | d) from (x, d) with x - m - d = xr.  Each
@@ -424,7 +433,10 @@ __device__ __forceinline__ void bm2_segment(const Bm2Args &a, uint8_t *smem, int
                     constexpr bool FULL = decltype(fullc)::value;
 #pragma unroll
                     for (int k = 0; k < TX; ++k) {
-                        if (k > 0) acc = acc + cs[k + 2 * R] - cs[k - 1];
+                        if (k > 0) {
+                            if constexpr (SSD) acc = acc + cs[k + 2 * R] - cs[k - 1];
+                            else acc = add_sub2(acc, cs[k + 2 * R], cs[k - 1]);
+                        }
                         if (FULL || lane_writes) {
                             if constexpr (SSD) *reinterpret_cast<uint32_t *>(tb + k * PITCH) = acc;
                             else *reinterpret_cast<uint32_t *>(tb + k * PITCH) = as1(acc);
@@ -460,7 +472,10 @@ __device__ __forceinline__ void bm2_segment(const Bm2Args &a, uint8_t *smem, int
             } else if (lane_writes) {
 #pragma unroll
                 for (int k = 0; k < TX; ++k) {
-                    if (k > 0) acc = acc + cs[k + 2 * R] - cs[k - 1];
+                    if (k > 0) {
+                        if constexpr (SSD) acc = acc + cs[k + 2 * R] - cs[k - 1];
+                        else acc = add_sub2(acc, cs[k + 2 * R], cs[k - 1]);
+                    }
                     if constexpr (SSD) *reinterpret_cast<uint32_t *>(tb + k * PITCH) = acc;
                     else *reinterpret_cast<uint32_t *>(tb + k * PITCH) = as1(acc);
                 }
