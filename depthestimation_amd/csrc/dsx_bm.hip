@@ -86,7 +86,8 @@ struct Geo {
     static constexpr int SROW = rnd16(NJ * 4 + 16);  // >= 16 * ceil(NJ / 4): whole-lane b128 stores
     static constexpr int MAXJ = (NJ + NT - 1) / NT;
     static constexpr int NB = DSL / 8;        // 8-disparity blocks per epilogue lane
-    static constexpr int REFB = rnd16(2 * (NC + 8));  // reference row as u16 pairs (broadcast reads)
+    // reference row (broadcast reads): u16 pairs for SAD, f32 for SSD
+    static constexpr int REFB = SSD ? rnd16(4 * (NC + 8)) : rnd16(2 * (NC + 8));
     static constexpr int SLOT = SROW + REFB;
     static constexpr int SMEM0 = 4 * SLOT + TX * PITCH;
     static constexpr int SMEM = SMEM0 > (2 * R + 1) * SLOT ? SMEM0 : (2 * R + 1) * SLOT;
@@ -156,7 +157,15 @@ __device__ __forceinline__ void bm2_segment(const Bm2Args &a, uint8_t *smem, int
                   PITCH = G::PITCH, NJ = G::NJ, SLOT = G::SLOT, NB = G::NB, NJ4 = (NJ + 3) / 4,
                   NCH = (NC + 7) / 8;
     constexpr int side = SIDE;
-    typedef typename std::conditional<SSD, uint32_t, u16x2>::type acc_t;
+    // FSS: SSD sums in f32.  Squared differences, column sums and (offset) box sums are integers
+    // below 2^24, so v_sub_f32 / v_fma_f32 / v_add_f32 (full rate, ~2 cycles) are exact and
+    // replace the quarter-rate v_mad_i32_i24.  Box sums carry a +2^23 offset: for box < 2^23
+    // (SSD R <= 5: 121 * 255^2 = 7.87M) the f32 value 2^23 + box has ulp 1 and its bit pattern is
+    // OFF + box, monotone as u32, so the tile and the LR keys take the raw bits (OFF's set bits
+    // lie above 23 + DB and leave the (C << DB | d) order intact); the epilogue subtracts OFF.
+    constexpr bool FSS = SSD && R <= 5 && (SIDE == 0 || SIDE == 3);
+    constexpr uint32_t OFF = FSS ? 0x4B000000u : 0u;
+    typedef typename std::conditional<FSS, float, typename std::conditional<SSD, uint32_t, u16x2>::type>::type acc_t;
     uint8_t *tile = smem + 4 * SLOT;
 
     const int tid = threadIdx.x;
@@ -202,6 +211,7 @@ __device__ __forceinline__ void bm2_segment(const Bm2Args &a, uint8_t *smem, int
                 const int pp = PB + sgn * j;
                 uint32_t t = srow[clampi2(pp, 0, W - 1)];
                 if constexpr (!SSD) t |= (uint32_t)srow[clampi2(pp + sgn, 0, W - 1)] << 16;
+                if constexpr (FSS) t = __float_as_uint((float)t);
                 v[q] = t;
             }
             w0 = v[0];
@@ -211,7 +221,11 @@ __device__ __forceinline__ void bm2_segment(const Bm2Args &a, uint8_t *smem, int
         }
     };
     auto st = [&](int sl, uint32_t w0, uint32_t w1, uint32_t w2, uint32_t w3, uint32_t rf) __attribute__((always_inline)) {
-        if (tid < NC4) {
+        if (FSS && tid < NC4) {
+            *reinterpret_cast<uint4 *>(smem + sl * SLOT + G::SROW + 16 * tid) =
+                make_uint4(__float_as_uint((float)(rf & 0xFFu)), __float_as_uint((float)((rf >> 8) & 0xFFu)),
+                           __float_as_uint((float)((rf >> 16) & 0xFFu)), __float_as_uint((float)(rf >> 24)));
+        } else if (tid < NC4) {
             const uint32_t r01 = __builtin_amdgcn_perm(0u, rf, 0x0C010C00u);  // {ref[4t], ref[4t+1]} as u16
             const uint32_t r23 = __builtin_amdgcn_perm(0u, rf, 0x0C030C02u);
             *reinterpret_cast<uint2 *>(smem + sl * SLOT + G::SROW + 8 * tid) = make_uint2(r01, r23);
@@ -221,6 +235,9 @@ __device__ __forceinline__ void bm2_segment(const Bm2Args &a, uint8_t *smem, int
             if constexpr (SSD) {
                 if (side == 1) {
                     w0 = dw & 0xFFu; w1 = (dw >> 8) & 0xFFu; w2 = (dw >> 16) & 0xFFu; w3 = dw >> 24;
+                } else if constexpr (FSS) {  // v_cvt_f32_ubyte{3,2,1,0}
+                    w0 = __float_as_uint((float)(dw >> 24)); w1 = __float_as_uint((float)((dw >> 16) & 0xFFu));
+                    w2 = __float_as_uint((float)((dw >> 8) & 0xFFu)); w3 = __float_as_uint((float)(dw & 0xFFu));
                 } else {
                     w0 = dw >> 24; w1 = (dw >> 16) & 0xFFu; w2 = (dw >> 8) & 0xFFu; w3 = dw & 0xFFu;
                 }
@@ -247,6 +264,13 @@ __device__ __forceinline__ void bm2_segment(const Bm2Args &a, uint8_t *smem, int
         rw[1] = v.y;
         rw[2] = v.z;
         rw[3] = v.w;
+    };
+    // FSS: 8 f32 reference pixels, two broadcast 16-B reads
+    auto ref_chunkf = [&](int sl, int c0, float(&rw)[8]) __attribute__((always_inline)) {
+        const uint4 v0 = *reinterpret_cast<const uint4 *>(smem + sl * SLOT + G::SROW + 4 * c0);
+        const uint4 v1 = *reinterpret_cast<const uint4 *>(smem + sl * SLOT + G::SROW + 4 * c0 + 16);
+        rw[0] = __uint_as_float(v0.x); rw[1] = __uint_as_float(v0.y); rw[2] = __uint_as_float(v0.z); rw[3] = __uint_as_float(v0.w);
+        rw[4] = __uint_as_float(v1.x); rw[5] = __uint_as_float(v1.y); rw[6] = __uint_as_float(v1.z); rw[7] = __uint_as_float(v1.w);
     };
     auto refpk = [](const uint32_t(&rw)[4], int c) __attribute__((always_inline)) -> u16x2 {
         const u16x2 v = as2(rw[c >> 1]);
@@ -313,12 +337,17 @@ __device__ __forceinline__ void bm2_segment(const Bm2Args &a, uint8_t *smem, int
         for (int q = 0; q < NCH; ++q) {
             const int c0 = 8 * q;
             uint32_t sw[8], rw[4];
+            float rf8[8];
             s_chunk(i, c0, sw);
-            ref_chunk(i, c0, rw);
+            if constexpr (FSS) ref_chunkf(i, c0, rf8);
+            else ref_chunk(i, c0, rw);
 #pragma unroll
             for (int c = 0; c < 8; ++c) {
                 if (c0 + c < NC) {
-                    if constexpr (SSD) {
+                    if constexpr (FSS) {
+                        const float t = rf8[c] - __uint_as_float(sw[c]);
+                        cs[c0 + c] = __builtin_fmaf(t, t, cs[c0 + c]);
+                    } else if constexpr (SSD) {
                         const int t = (int)refv(rw, c) - (int)sw[c];
                         cs[c0 + c] += (uint32_t)__mul24(t, t);  // v_mul_i32_i24: |t| <= 255
                     } else {
@@ -334,7 +363,7 @@ __device__ __forceinline__ void bm2_segment(const Bm2Args &a, uint8_t *smem, int
     // tile padding: disparities >= D never win
     for (int q = tid; q < TX * (Dp - D); q += NT) {
         const int k = q / (Dp - D), d = D + (q - k * (Dp - D));
-        if constexpr (SSD) *reinterpret_cast<uint32_t *>(tile + k * PITCH + d * 4) = padv;
+        if constexpr (SSD) *reinterpret_cast<uint32_t *>(tile + k * PITCH + d * 4) = padv + OFF;
         else *reinterpret_cast<uint16_t *>(tile + k * PITCH + d * 2) = (uint16_t)padv;
     }
     block_sync<NW>();
@@ -377,14 +406,25 @@ __device__ __forceinline__ void bm2_segment(const Bm2Args &a, uint8_t *smem, int
             for (int q = 0; q < NCH; ++q) {
                 const int c0 = 8 * q;
                 uint32_t sn[8], so[8], rn[4], ro[4];
-                ref_chunk(par, c0, rn);
-                ref_chunk(par + 1, c0, ro);
+                float rnf[8], rof[8];
+                if constexpr (FSS) {
+                    ref_chunkf(par, c0, rnf);
+                    ref_chunkf(par + 1, c0, rof);
+                } else {
+                    ref_chunk(par, c0, rn);
+                    ref_chunk(par + 1, c0, ro);
+                }
                 s_chunk(par, c0, sn);
                 s_chunk(par + 1, c0, so);
 #pragma unroll
                 for (int c = 0; c < 8; ++c) {
                     if (c0 + c < NC) {
-                        if constexpr (SSD) {
+                        if constexpr (FSS) {
+                            // cs + tn^2 - to^2: two v_sub_f32 + two v_fma_f32 (neg modifier)
+                            const float tn = rnf[c] - __uint_as_float(sn[c]);
+                            const float to = rof[c] - __uint_as_float(so[c]);
+                            cs[c0 + c] = __builtin_fmaf(-to, to, __builtin_fmaf(tn, tn, cs[c0 + c]));
+                        } else if constexpr (SSD) {
                             const int tn = (int)refv(rn, c) - (int)sn[c];
                             const int to = (int)refv(ro, c) - (int)so[c];
                             const int nto = (int)so[c] - (int)refv(ro, c);
@@ -405,7 +445,13 @@ __device__ __forceinline__ void bm2_segment(const Bm2Args &a, uint8_t *smem, int
         // ---- horizontal running box sum -> LDS tile (pixel k, disparity d0..) ----
         {
             uint8_t *tb = tile + d0 * CB;
+            auto abits = [](acc_t v) __attribute__((always_inline)) -> uint32_t {
+                if constexpr (FSS) return __float_as_uint(v);
+                else if constexpr (SSD) return v;
+                else return as1(v);
+            };
             acc_t acc = cs[0];
+            if constexpr (FSS) acc = 8388608.0f + cs[0];  // + 2^23 (see FSS)
 #pragma unroll
             for (int c = 1; c <= 2 * R; ++c) {
                 if constexpr (SSD) acc += cs[c];
@@ -434,16 +480,17 @@ __device__ __forceinline__ void bm2_segment(const Bm2Args &a, uint8_t *smem, int
 #pragma unroll
                     for (int k = 0; k < TX; ++k) {
                         if (k > 0) {
-                            if constexpr (SSD) acc = acc + cs[k + 2 * R] - cs[k - 1];
+                            if constexpr (FSS) acc = (acc - cs[k - 1]) + cs[k + 2 * R];  // stays in [2^23, 2^24)
+                            else if constexpr (SSD) acc = acc + cs[k + 2 * R] - cs[k - 1];
                             else acc = add_sub2(acc, cs[k + 2 * R], cs[k - 1]);
                         }
                         if (FULL || lane_writes) {
-                            if constexpr (SSD) *reinterpret_cast<uint32_t *>(tb + k * PITCH) = acc;
+                            if constexpr (SSD) *reinterpret_cast<uint32_t *>(tb + k * PITCH) = abits(acc);
                             else *reinterpret_cast<uint32_t *>(tb + k * PITCH) = as1(acc);
                         }
                         if (FULL || x0 + k < W) {
                             if constexpr (SSD) {
-                                Ae = umin2(Ae, (acc << ks) | dmE);
+                                Ae = umin2(Ae, (abits(acc) << ks) | dmE);
                             } else {  // (C << 16) | d by byte permute
                                 Ae = umin2(Ae, __builtin_amdgcn_perm(as1(acc), (uint32_t)d0, selE));
                                 Ao = umin2(Ao, __builtin_amdgcn_perm(as1(acc), (uint32_t)(d0 + 1), selO));
@@ -473,10 +520,11 @@ __device__ __forceinline__ void bm2_segment(const Bm2Args &a, uint8_t *smem, int
 #pragma unroll
                 for (int k = 0; k < TX; ++k) {
                     if (k > 0) {
-                        if constexpr (SSD) acc = acc + cs[k + 2 * R] - cs[k - 1];
+                        if constexpr (FSS) acc = (acc - cs[k - 1]) + cs[k + 2 * R];
+                        else if constexpr (SSD) acc = acc + cs[k + 2 * R] - cs[k - 1];
                         else acc = add_sub2(acc, cs[k + 2 * R], cs[k - 1]);
                     }
-                    if constexpr (SSD) *reinterpret_cast<uint32_t *>(tb + k * PITCH) = acc;
+                    if constexpr (SSD) *reinterpret_cast<uint32_t *>(tb + k * PITCH) = abits(acc);
                     else *reinterpret_cast<uint32_t *>(tb + k * PITCH) = as1(acc);
                 }
             }
@@ -521,7 +569,7 @@ __device__ __forceinline__ void bm2_segment(const Bm2Args &a, uint8_t *smem, int
                 if constexpr (SSD) {
                     const uint4 v0 = *reinterpret_cast<const uint4 *>(px + 32 * i);
                     const uint4 v1 = *reinterpret_cast<const uint4 *>(px + 32 * i + 16);
-                    bs[i] = umin2(umin2(umin2(v0.x, v0.y), umin2(v0.z, v0.w)), umin2(umin2(v1.x, v1.y), umin2(v1.z, v1.w)));
+                    bs[i] = umin2(umin2(umin2(v0.x, v0.y), umin2(v0.z, v0.w)), umin2(umin2(v1.x, v1.y), umin2(v1.z, v1.w))) - OFF;
                 } else {
                     const uint4 v = *reinterpret_cast<const uint4 *>(px + 16 * i);
                     const u16x2 mm = __builtin_elementwise_min(__builtin_elementwise_min(as2(v.x), as2(v.y)),
@@ -552,7 +600,8 @@ __device__ __forceinline__ void bm2_segment(const Bm2Args &a, uint8_t *smem, int
                     if constexpr (SSD) {
                         const uint4 v0 = *reinterpret_cast<const uint4 *>(px + 32 * bsel);
                         const uint4 v1 = *reinterpret_cast<const uint4 *>(px + 32 * bsel + 16);
-                        const uint32_t c8[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
+                        const uint32_t c8[8] = {v0.x - OFF, v0.y - OFF, v0.z - OFF, v0.w - OFF,
+                                                v1.x - OFF, v1.y - OFF, v1.z - OFF, v1.w - OFF};
     #pragma unroll
                         for (int q = 0; q < 8; ++q) k8 = umin2(k8, (c8[q] << 3) | (uint32_t)q);
                     } else {
@@ -580,8 +629,8 @@ __device__ __forceinline__ void bm2_segment(const Bm2Args &a, uint8_t *smem, int
                     if constexpr (SSD) {
                         const uint4 v0 = *reinterpret_cast<const uint4 *>(px + 32 * bsel);
                         const uint4 v1 = *reinterpret_cast<const uint4 *>(px + 32 * bsel + 16);
-                        c8[0] = v0.x; c8[1] = v0.y; c8[2] = v0.z; c8[3] = v0.w;
-                        c8[4] = v1.x; c8[5] = v1.y; c8[6] = v1.z; c8[7] = v1.w;
+                        c8[0] = v0.x - OFF; c8[1] = v0.y - OFF; c8[2] = v0.z - OFF; c8[3] = v0.w - OFF;
+                        c8[4] = v1.x - OFF; c8[5] = v1.y - OFF; c8[6] = v1.z - OFF; c8[7] = v1.w - OFF;
                     } else {
                         const uint4 v = *reinterpret_cast<const uint4 *>(px + 16 * bsel);
                         c8[0] = v.x & 0xFFFFu; c8[1] = v.x >> 16; c8[2] = v.y & 0xFFFFu; c8[3] = v.y >> 16;
@@ -617,8 +666,8 @@ __device__ __forceinline__ void bm2_segment(const Bm2Args &a, uint8_t *smem, int
                             if constexpr (SSD) {
                                 const uint4 v0 = *reinterpret_cast<const uint4 *>(px + 32 * ib);
                                 const uint4 v1 = *reinterpret_cast<const uint4 *>(px + 32 * ib + 16);
-                                c8[0] = v0.x; c8[1] = v0.y; c8[2] = v0.z; c8[3] = v0.w;
-                                c8[4] = v1.x; c8[5] = v1.y; c8[6] = v1.z; c8[7] = v1.w;
+                                c8[0] = v0.x - OFF; c8[1] = v0.y - OFF; c8[2] = v0.z - OFF; c8[3] = v0.w - OFF;
+                                c8[4] = v1.x - OFF; c8[5] = v1.y - OFF; c8[6] = v1.z - OFF; c8[7] = v1.w - OFF;
                             } else {
                                 const uint4 v = *reinterpret_cast<const uint4 *>(px + 16 * ib);
                                 c8[0] = v.x & 0xFFFFu; c8[1] = v.x >> 16; c8[2] = v.y & 0xFFFFu; c8[3] = v.y >> 16;
@@ -644,8 +693,8 @@ __device__ __forceinline__ void bm2_segment(const Bm2Args &a, uint8_t *smem, int
                     int32_t cm, cp;
                     const uint8_t *pk = tile + k * PITCH;
                     if constexpr (SSD) {
-                        cm = (int32_t)reinterpret_cast<const uint32_t *>(pk)[b - 1];
-                        cp = (int32_t)reinterpret_cast<const uint32_t *>(pk)[b + 1];
+                        cm = (int32_t)(reinterpret_cast<const uint32_t *>(pk)[b - 1] - OFF);
+                        cp = (int32_t)(reinterpret_cast<const uint32_t *>(pk)[b + 1] - OFF);
                     } else {
                         cm = reinterpret_cast<const uint16_t *>(pk)[b - 1];
                         cp = reinterpret_cast<const uint16_t *>(pk)[b + 1];

@@ -10,12 +10,17 @@ import torch  # noqa: E402
 from depthestimation_amd.matcher import HipBlockMatcher  # noqa: E402
 from depthestimation_amd.synthetic import stereo_pair  # noqa: E402
 
-H, W, D, bs = 1080, 1920, 128, 9
+from bench import CONFIGS  # noqa: E402
+
+# usage: python tools/timeline.py [grid] [config]   (config of bench.py, default c2)
 grid = int(sys.argv[1]) if len(sys.argv) > 1 else 0
+cfg = dict(CONFIGS[sys.argv[2] if len(sys.argv) > 2 else "c2"])
+H, W, D = cfg.pop("H"), cfg.pop("W"), cfg["num_disp"]
+cfg.pop("desc")
 L, R, _ = stereo_pair(H, W, 0, D, seed=1)
 tL, tR = torch.from_numpy(L).cuda(), torch.from_numpy(R).cuda()
 out = torch.empty((H, W), dtype=torch.int16, device="cuda")
-m = HipBlockMatcher(num_disp=D, block_size=bs, uniqueness_ratio=0, disp12_max_diff=-1, grid_blocks=grid)
+m = HipBlockMatcher(grid_blocks=grid, **cfg)
 for _ in range(3):
     m.compute_device(tL, tR, out_fixed=out)
 torch.cuda.synchronize()
