@@ -253,6 +253,11 @@ dsx::Bm2Args base_args(dsx_handle *h, int H, int W, int64_t stride) {
         if (pt) sscanf(pt, "%d,%d,%d", &a.pt1, &a.pt2, &a.pt3);
         const char *sw = getenv("DSX_SLOW_W8");
         a.slow_w8 = sw ? atoi(sw) : 11;
+        // age-level work weights (single frames; r01f A/B: C2 83.6 -> 81.7 us, C4 61.4 -> 59.9 us)
+        a.agew[0] = 78, a.agew[1] = 70, a.agew[2] = a.agew[3] = 64;
+        const char *aw = getenv("DSX_AGEW");
+        if (aw) sscanf(aw, "%d,%d,%d,%d", &a.agew[0], &a.agew[1], &a.agew[2], &a.agew[3]);
+        a.nlev = 0;  // set by the launcher from the residency it computes
         const char *va = getenv("DSX_VARIANT");
         a.variant = va ? atoi(va) : 0;
     }

@@ -40,10 +40,14 @@
 #define DSX_WPE_SSD 4
 #endif
 
+#include <algorithm>
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
 #include <mutex>
 #include <type_traits>
+#include <utility>
+#include <vector>
 
 namespace dsx {
 
@@ -401,7 +405,31 @@ __device__ __forceinline__ void bm2_segment(const Bm2Args &a, uint8_t *smem, int
             ld(y + 1 + R, pn0, pn1, pn2, pn3, pnr);
             ld(y - R, po0, po1, po2, po3, por);
         }
-        if (y > yb) {
+        if constexpr (FSS) {
+          if (y > yb) {
+            // chunks of 4 columns (one broadcast b128 of reference pixels per slot): half the
+            // transient registers of the 8-column chunks, which spilled at 4 waves / SIMD
+#pragma unroll
+            for (int q = 0; q < (NC + 3) / 4; ++q) {
+                const int c0 = 4 * q;
+                const uint4 rn = *reinterpret_cast<const uint4 *>(smem + par * SLOT + G::SROW + 4 * c0);
+                const uint4 ro = *reinterpret_cast<const uint4 *>(smem + (par + 1) * SLOT + G::SROW + 4 * c0);
+                const float rn4[4] = {__uint_as_float(rn.x), __uint_as_float(rn.y), __uint_as_float(rn.z), __uint_as_float(rn.w)};
+                const float ro4[4] = {__uint_as_float(ro.x), __uint_as_float(ro.y), __uint_as_float(ro.z), __uint_as_float(ro.w)};
+                const uint8_t *bn = smem + par * SLOT + d0 * 4, *bo = smem + (par + 1) * SLOT + d0 * 4;
+#pragma unroll
+                for (int c = 0; c < 4; ++c) {
+                    if (c0 + c < NC) {
+                        const float sn = *reinterpret_cast<const float *>(bn + (NC - 1 - c0 - c) * 4);
+                        const float so = *reinterpret_cast<const float *>(bo + (NC - 1 - c0 - c) * 4);
+                        // cs + tn^2 - to^2: two v_sub_f32 + two v_fma_f32 (neg modifier)
+                        const float tn = rn4[c] - sn, to = ro4[c] - so;
+                        cs[c0 + c] = __builtin_fmaf(-to, to, __builtin_fmaf(tn, tn, cs[c0 + c]));
+                    }
+                }
+            }
+          }
+        } else if (y > yb) {
 #pragma unroll
             for (int q = 0; q < NCH; ++q) {
                 const int c0 = 8 * q;
@@ -755,59 +783,9 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu((SSD &&
         }
     }
 
-    // ---- work partition over the (frame, strip, row) space: with at least one block per
-    // (frame, strip), every block owns ONE contiguous run of rows of ONE strip of one frame;
-    // otherwise an even split of the linearised space.  Strips on the clamped-load path (image
-    // edges) weigh slow_w8/8 of a fast strip, so they get proportionally more blocks.
-    const int NS = a.strip_count * a.nframes;
-    const int NG = gridDim.x, b = blockIdx.x;
-    int lin0, lin1;  // (frame, strip, row) units: nframes * H * W < 2^31 (host check)
-    if (NG >= NS && NS > 0) {
-        const int S = a.strip_count;
-        // fast strips: x0 in [XL, XU] (the `fast` test below, solved for x0)
-        constexpr int NJ4c = (NJ + 3) / 4, NC4c = (NC + 3) / 4;
-        int XL, XU;
-        if (side == 1) {
-            XL = max(R - m, R);
-            XU = min(W - 1 - 4 * NJ4c + R - m, W - 1 + R - 4 * NC4c + 1);
-        } else {
-            XL = max(4 * NJ4c + R + m - NC + 1, R);
-            XU = min(W - 1 + R + m - NC + 1, W - 1 + R - 4 * NC4c + 1);
-        }
-        const int sb = a.strip_begin;
-        const int slo = clampi2((XL + TX - 1 >= 0 ? (XL + TX - 1) / TX : -((-(XL + TX - 1) + TX - 1) / TX)) - sb, 0, S);
-        const int shi = clampi2((XU >= 0 ? XU / TX : -((-XU + TX - 1) / TX)) - sb + 1, slo, S);  // fast: [slo, shi)
-        int w8 = a.slow_w8;
-        if (w8 < 8 || NG * 8 < NS * w8 + 8 * NS) w8 = 8;  // every strip keeps >= 1 block
-        const int ex = w8 - 8;
-        auto Pf = [&](int s) -> long { return 8L * s + (long)ex * (min(s, slo) + max(0, s - shi)); };
-        const long Uf = Pf(S), U = Uf * a.nframes;
-        auto P = [&](int g) -> long { const int f = g / S; return f * Uf + Pf(g - f * S); };
-        // start(g) = ceil(P(g) * NG / U): double quotient + exact integer fix-up (no 64-bit
-        // integer division, which is a long SALU sequence on gfx950)
-        auto start = [&](int g) -> int {
-            const long num = P(g) * NG;
-            long q = (long)__builtin_ceil((double)num / (double)U);
-            if (q * U < num) ++q;
-            if (q > 0 && (q - 1) * U >= num) --q;
-            return (int)q;
-        };
-        int lo = 0, hi = NS - 1;  // largest g with start(g) <= b
-        while (lo < hi) {
-            const int mid = (lo + hi + 1) >> 1;
-            if (start(mid) <= b) lo = mid;
-            else hi = mid - 1;
-        }
-        const int s = lo;
-        const int bs0 = start(s), bs1 = start(s + 1);
-        const int j = b - bs0, cnt = bs1 - bs0;
-        lin0 = s * H + j * H / cnt;
-        lin1 = s * H + (j + 1) * H / cnt;
-    } else {
-        const long T = (long)NS * H;
-        lin0 = (int)(b * T / NG);
-        lin1 = (int)((b + 1) * T / NG);
-    }
+    // ---- work partition (host-computed, bm2_partition): block b owns linear (frame, strip, row)
+    // units [part[b], part[b+1]); nframes * H * W < 2^31 (host check)
+    const int lin0 = a.part[blockIdx.x], lin1 = a.part[blockIdx.x + 1];
     constexpr bool lr_on = SIDE == 3;  // left pass that also builds the right-view winners
     int qcur = -1;
     int pe[3];  // rows done at which the priority drops (progress bands pt1..pt3 of 256)
@@ -859,6 +837,95 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu((SSD &&
     }
 }
 
+
+// Work partition over the (frame, strip, row) space, computed on the host once per launch shape
+// and cached on the device (a per-block binary search with 64-bit / f64 arithmetic cost every
+// block microseconds at kernel start).  With at least one block per (frame, strip), every block
+// owns ONE contiguous run of rows of ONE strip of one frame; otherwise an even split of the
+// linearised space.  Strips on the clamped-load path (image edges) weigh slow_w8/8 of a fast
+// strip, so they get proportionally more blocks.  Fast strips are those with x0 in [XL, XU]
+// (bm2's `fast` test solved for x0).
+//
+// Block capacities by age level (DSX_AGEW, 1/64): with one block per resident slot, block b is
+// the (b * nlev / NG)-th block its CU received; co-resident waves on a SIMD issue by age, so a
+// level's blocks take work in proportion to its weight.  Q(b) = total weight of blocks < b; strip
+// g starts at the first block b with Q(b) * U >= P(g) * Qtot.  Every strip keeps >= 1 block while
+// 8 * NG * wmin >= U * wmax (else equal weights).
+static std::vector<int> bm2_partition(int NG, int S, int sb, int nframes, int H, int XL, int XU, int TX, int slow_w8,
+                                      int nlev, const int *agew) {
+    std::vector<int> part(NG + 1);
+    const int NS = S * nframes;
+    if (NG < NS || NS <= 0) {
+        const long T = (long)NS * H;
+        for (int b = 0; b <= NG; ++b) part[b] = (int)(b * T / NG);
+        return part;
+    }
+    auto fdiv = [](long x, long y) { return x >= 0 ? x / y : -((-x + y - 1) / y); };
+    const int slo = std::min(std::max((int)fdiv(XL + TX - 1, TX) - sb, 0), S);
+    const int shi = std::min(std::max((int)fdiv(XU, TX) - sb + 1, slo), S);  // fast strips: [slo, shi)
+    int w8 = slow_w8;
+    if (w8 < 8 || NG * 8 < NS * w8 + 8 * NS) w8 = 8;  // every strip keeps >= 1 block
+    const int ex = w8 - 8;
+    auto Pf = [&](int s) -> long { return 8L * s + (long)ex * (std::min(s, slo) + std::max(0, s - shi)); };
+    const long Uf = Pf(S), U = Uf * nframes;
+    auto P = [&](int g) -> long { const int f = g / S; return f * Uf + Pf(g - f * S); };
+    int nl = nlev > 1 ? std::min(nlev, 4) : 1;
+    {
+        int wmin = 1 << 30, wmax = 0;
+        for (int L = 0; L < nl; ++L) {
+            wmin = std::min(wmin, agew[L]);
+            wmax = std::max(wmax, agew[L]);
+        }
+        if (nl > 1 && (wmin < 1 || 8L * NG * wmin < U * wmax)) nl = 1;
+    }
+    std::vector<long> Q(NG + 1, 0);
+    for (int b = 0; b < NG; ++b) Q[b + 1] = Q[b] + (nl > 1 ? agew[(long)b * nl / NG] : 64);
+    const long Qtot = Q[NG];
+    std::vector<int> start(NS + 1);
+    int b = 0;
+    for (int g = 0; g <= NS; ++g) {
+        const long T = P(g) * Qtot;
+        while (b < NG && Q[b] * U < T) ++b;
+        start[g] = b;
+    }
+    for (int g = 0; g < NS; ++g) {
+        const long q0 = Q[start[g]], qd = Q[start[g + 1]] - q0;
+        for (int bb = start[g]; bb <= start[g + 1]; ++bb)
+            part[bb] = g * H + (int)((Q[bb] - q0) * H / qd);
+    }
+    part[NG] = NS * H;
+    return part;
+}
+
+// Device copies of partitions, one per launch shape (kept for the process lifetime: a launch in
+// flight on any stream may still read one).
+struct PartKey {
+    int dev, NG, S, sb, nframes, H, XL, XU, w8, nlev, w[4];
+    bool operator==(const PartKey &o) const { return memcmp(this, &o, sizeof(PartKey)) == 0; }
+};
+static hipError_t bm2_partition_dev(const PartKey &k, int TX, const int **out) {
+    static std::mutex mu;  // shared by every bm2 instantiation's launcher
+    static std::vector<std::pair<PartKey, int *>> cache;
+    std::lock_guard<std::mutex> lock(mu);
+    for (const auto &e : cache)
+        if (e.first == k) {
+            *out = e.second;
+            return hipSuccess;
+        }
+    const std::vector<int> part = bm2_partition(k.NG, k.S, k.sb, k.nframes, k.H, k.XL, k.XU, TX, k.w8, k.nlev, k.w);
+    int *d = nullptr;
+    hipError_t e = hipMalloc(&d, part.size() * sizeof(int));
+    if (e != hipSuccess) return e;
+    e = hipMemcpy(d, part.data(), part.size() * sizeof(int), hipMemcpyHostToDevice);
+    if (e != hipSuccess) {
+        (void)hipFree(d);
+        return e;
+    }
+    cache.emplace_back(k, d);
+    *out = d;
+    return hipSuccess;
+}
+
 template <int R, bool SSD, int NW, int SIDE>
 static hipError_t launch_bm2_side(const Bm2Args &a, hipStream_t st) {
     using G = Geo<R, SSD, NW>;
@@ -896,7 +963,33 @@ static hipError_t launch_bm2_side(const Bm2Args &a, hipStream_t st) {
     if (getenv("DSX_VERBOSE"))
         fprintf(stderr, "[dsx] bm2<R=%d,SSD=%d,NW=%d,SIDE=%d> grid %ld (%d/CU) smem %d\n", R, (int)SSD, NW, SIDE, grid,
                 blocks_per_cu[dev], G::SMEM);
-    hipLaunchKernelGGL((bm2<R, SSD, NW, SIDE>), dim3((unsigned)grid), dim3(G::NT), G::SMEM, st, a);
+    // age levels: with one block per resident slot, block b is the (b / num_cu)-th block its CU
+    // received, and co-resident waves of a SIMD differ in age (issue arbitration) by that rank
+    Bm2Args la = a;
+    la.nlev = 1;
+    if (grid == (long)blocks_per_cu[dev] * num_cu[dev] && a.nframes == 1) {  // batches: equal weights
+        const int lv = blocks_per_cu[dev] * NW / 4;
+        la.nlev = lv < 1 ? 1 : (lv > 4 ? 4 : lv);
+    }
+    {
+        constexpr int NJ4 = (G::NJ + 3) / 4, NC4 = (G::NC + 3) / 4, NC = G::NC;
+        const int W = a.W, m = a.m;
+        PartKey k;
+        memset(&k, 0, sizeof(k));
+        k.dev = dev, k.NG = (int)grid, k.S = a.strip_count, k.sb = a.strip_begin, k.nframes = a.nframes, k.H = a.H;
+        if (SIDE == 1) {
+            k.XL = std::max(R - m, R);
+            k.XU = std::min(W - 1 - 4 * NJ4 + R - m, W - 1 + R - 4 * NC4 + 1);
+        } else {
+            k.XL = std::max(4 * NJ4 + R + m - NC + 1, R);
+            k.XU = std::min(W - 1 + R + m - NC + 1, W - 1 + R - 4 * NC4 + 1);
+        }
+        k.w8 = a.slow_w8, k.nlev = la.nlev;
+        for (int i = 0; i < 4; ++i) k.w[i] = la.nlev > 1 ? a.agew[i] : 64;
+        e = bm2_partition_dev(k, G::TX, &la.part);
+        if (e != hipSuccess) return e;
+    }
+    hipLaunchKernelGGL((bm2<R, SSD, NW, SIDE>), dim3((unsigned)grid), dim3(G::NT), G::SMEM, st, la);
     return hipGetLastError();
 }
 

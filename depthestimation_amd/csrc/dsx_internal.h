@@ -36,6 +36,9 @@ struct Bm2Args {
     int pt1, pt2, pt3;   // progress band edges in 1/256 of a block's rows (priority 3, 2, 1, 0)
     int variant;         // experiment bits (DSX_VARIANT env), 0 = production
     int slow_w8;         // work weight of a strip on the clamped-load path, in 1/8 of a fast strip
+    int agew[4];         // work weight (1/64) of a block by co-residency age level (dispatch order)
+    int nlev;            // age levels (co-resident waves per SIMD, <= 4); <= 1: equal weights
+    const int *part;     // device: block b owns linear (frame, strip, row) units [part[b], part[b+1])
     uint32_t *lr_keys;     // left pass with LR: per-pixel right-view winner keys (C << kshift | d),
     int kshift;            //   filled by atomicMin (memset to ~0 first)
     int16_t *dstar;        // left pass with LR: winning d (or -1) for lr_fixup

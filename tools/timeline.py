@@ -65,5 +65,12 @@ strip = bs_ * NS // len(t)
 per = [dur[strip == s].mean() for s in range(NS)]
 print("mean block duration per strip (us):", " ".join(f"{v:.0f}" for v in per))
 print("slowest 10 blocks (block, strip, dur, start):", [(int(b), int(strip[b]), round(float(dur[b]), 1), round(float(st[b]), 1)) for b in np.argsort(-dur)[:10]])
-print("duration by CU-slot rank within CU:")
-order = np.lexsort((st, key))
+order = np.lexsort((bs_, key))  # blocks of each CU in dispatch (block id) order
+rank = np.empty(len(t), np.int64)
+ks, first = np.unique(key[order], return_index=True)
+for i, f in enumerate(first):
+    e = first[i + 1] if i + 1 < len(first) else len(order)
+    rank[order[f:e]] = np.arange(e - f)
+print("mean duration by CU-slot rank (us):", " ".join(f"{dur[rank == r].mean():.1f}" for r in range(rank.max() + 1)))
+print("mean duration by XCD (us):", " ".join(f"{dur[xcc == x].mean():.1f}" for x in range(8)))
+print("mean end by CU-slot rank (us):", " ".join(f"{en[rank == r].mean():.1f}" for r in range(rank.max() + 1)))
