@@ -3,11 +3,12 @@
 //
 // Work decomposition
 //   * One block = NW waves = Dp disparities. SAD lanes own a disparity PAIR (d0, d0+1) whose
-//     costs live in the two u16 halves of one VGPR (v_pk_{max,min,add,sub}_u16: two
-//     disparities per VALU op, SAD window sums <= 225*255 fit u16); SSD lanes own one
-//     disparity in u32.
+//     costs live in the two u16 halves of one VGPR (v_pk_{max,min}_u16 for the absolute
+//     differences, carry-free full-rate v_add/sub_u32 for the sums; SAD window sums <= 225*255
+//     fit u16); SSD lanes own one disparity, summed exactly in f32 (FSS below) or u32.
 //   * The image is cut into vertical strips of TX = 32 output columns.  The (strip, row)
-//     space is split evenly over a persistent grid (blocks = resident capacity), each block
+//     space is split over a persistent grid (blocks = resident capacity; host-computed
+//     partition, bm2_partition), each block
 //     sweeping down contiguous rows of a strip with running column sums (2 absolute
 //     differences per column per row: the entering and the leaving row), so there is no
 //     tail generation and no per-tile re-initialisation except at segment starts.

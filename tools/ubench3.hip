@@ -51,6 +51,31 @@ DEF3(k_min3_u32, "v_min3_u32")
 DEF3(k_perm_b32, "v_perm_b32")
 DEF3(k_pk_mad_u16, "v_pk_mad_u16")
 DEF3(k_mad_u32_u24, "v_mad_u32_u24")
+DEF3(k_msad_u8, "v_msad_u8")
+
+// 64-bit accumulator forms: INS d[2], s0[2], s1, d[2] (quad SAD) or d[2], s0[2], s1[2] (packed f32)
+#define DEFQ(NAME, INS, TAIL)                                                                      \
+  __global__ void NAME(uint32_t *out, uint32_t seed) {                                             \
+    uint64_t a0 = seed + threadIdx.x, a1 = a0 + 1, a2 = a0 + 2, a3 = a0 + 3, a4 = a0 + 4,          \
+             a5 = a0 + 5, a6 = a0 + 6, a7 = a0 + 7, b = seed * 3ull + 1;                           \
+    uint32_t c = seed ^ 0x1234;                                                                    \
+    for (int i = 0; i < N_OUTER; ++i) {                                                            \
+      asm volatile(INS " %0, %8, " TAIL(0) "\n\t" INS " %1, %8, " TAIL(1) "\n\t" INS " %2, %8, " TAIL(2) "\n\t" \
+                   INS " %3, %8, " TAIL(3) "\n\t" INS " %4, %8, " TAIL(4) "\n\t" INS " %5, %8, " TAIL(5) "\n\t" \
+                   INS " %6, %8, " TAIL(6) "\n\t" INS " %7, %8, " TAIL(7) "\n\t" INS " %0, %8, " TAIL(0) "\n\t" \
+                   INS " %1, %8, " TAIL(1) "\n\t" INS " %2, %8, " TAIL(2) "\n\t" INS " %3, %8, " TAIL(3) "\n\t" \
+                   INS " %4, %8, " TAIL(4) "\n\t" INS " %5, %8, " TAIL(5) "\n\t" INS " %6, %8, " TAIL(6) "\n\t" \
+                   INS " %7, %8, " TAIL(7)                                                         \
+                   : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(a4), "+v"(a5), "+v"(a6), "+v"(a7) : "v"(b), "v"(c)); \
+    }                                                                                              \
+    out[blockIdx.x * blockDim.x + threadIdx.x] = (uint32_t)(a0 + a1 + a2 + a3 + a4 + a5 + a6 + a7); \
+  }
+#define TQ(i) "%9, %" #i
+#define TP(i) "%" #i
+DEFQ(k_qsad, "v_qsad_pk_u16_u8", TQ)
+DEFQ(k_mqsad, "v_mqsad_pk_u16_u8", TQ)
+DEFQ(k_pk_add_f32, "v_pk_add_f32", TP)
+DEFQ(k_pk_mul_f32, "v_pk_mul_f32", TP)
 
 template <typename K>
 float time_kernel(K k, uint32_t *buf, int blocks, int threads) {
@@ -74,7 +99,9 @@ int main() {
     {"v_pk_min_u16", k_pk_min_u16}, {"v_add_f32", k_add_f32}, {"v_sub_f32_e64", k_sub_f32_e64abs},
     {"v_pk_add_f16", k_pk_add_f16}, {"v_pk_max_f16", k_pk_max_f16}, {"v_max_f32", k_max_f32},
     {"v_fma_f32", k_fma_f32}, {"v_sad_u8", k_sad_u8}, {"v_add3_u32", k_add3_u32}, {"v_min3_u32", k_min3_u32},
-    {"v_perm_b32", k_perm_b32}, {"v_pk_mad_u16", k_pk_mad_u16}, {"v_mad_u32_u24", k_mad_u32_u24}};
+    {"v_perm_b32", k_perm_b32}, {"v_pk_mad_u16", k_pk_mad_u16}, {"v_mad_u32_u24", k_mad_u32_u24},
+    {"v_msad_u8", k_msad_u8}, {"v_qsad_pk_u16_u8", k_qsad}, {"v_mqsad_pk_u16_u8", k_mqsad},
+    {"v_pk_add_f32", k_pk_add_f32}, {"v_pk_mul_f32", k_pk_mul_f32}};
   for (auto &x : ks) {
     const float ms = time_kernel(x.k, buf, blocks, threads);
     printf("%-16s %7.3f ms  %.2f cycles per wave-instr per SIMD (at 2.4 GHz)\n", x.n, ms, ms * 1e-3 * 2.4e9 * 1024 / wi);
