@@ -160,37 +160,59 @@ def main():
             raise SystemExit("--sgm needs a SAD config")
         args.path = "volume"
         args.no_batched = True
-    matcher = HipBlockMatcher(device=local, path=args.path, timing=True, grid_blocks=args.grid_blocks,
+    # The timed region runs without per-launch events: a HIP event pair around every launch costs
+    # ~8 us per C2 step on the GPU (72 vs 80 us, tools/launch_gap.py). Per-kernel durations come
+    # from a second handle with event timing, run after the timed region (breakdown pass).
+    matcher = HipBlockMatcher(device=local, path=args.path, timing=False, grid_blocks=args.grid_blocks,
                               aggregation=args.sgm, **kw)
+    tmatcher = HipBlockMatcher(device=local, path=args.path, timing=True, grid_blocks=args.grid_blocks,
+                               aggregation=args.sgm, **kw)
     stream = torch.cuda.current_stream(dev)
 
-    def step(i):
+    def step(i, m=matcher):
         if B == 1:
             fl, fr = frames[i % len(frames)]
-            matcher.compute_device(fl, fr, out_fixed=out_fixed[0], out_float=out_float[0], stream=stream)
+            m.compute_device(fl, fr, out_fixed=out_fixed[0], out_float=out_float[0], stream=stream)
         else:
             gl, gr = groups[i % len(groups)]
-            matcher.compute_batch_device(gl, gr, out_fixed=out_fixed, out_float=out_float, stream=stream)
+            m.compute_batch_device(gl, gr, out_fixed=out_fixed, out_float=out_float, stream=stream)
 
     for i in range(args.warmup):
         step(i)
     torch.cuda.synchronize(dev)
-    matcher.reset_times()
     if ws > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
+    ev0.record(stream)
     for i in range(args.steps):
         step(i)
+    ev1.record(stream)
     torch.cuda.synchronize(dev)
     if ws > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    region_ms = ev0.elapsed_time(ev1) / args.steps  # GPU time per step over the timed region
     if ws > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-    ktimes = matcher.kernel_times()
+    # breakdown pass: per-kernel HIP events on the same stream (outside the timed region), only for
+    # paths with several kernels per step; the fused pass without the LR check is one kernel, whose
+    # launch duration is the timed region's per-step GPU time
+    nbd = max(10, min(args.steps, 100))
+    if args.path == "fused" and cfg["disp12_max_diff"] < 0:
+        ktimes = {"bm_pass_left": (region_ms, args.steps)}
+    else:
+        for i in range(3):
+            step(i, tmatcher)
+        torch.cuda.synchronize(dev)
+        tmatcher.reset_times()
+        for i in range(nbd):
+            step(i, tmatcher)
+        torch.cuda.synchronize(dev)
+        ktimes = tmatcher.kernel_times()
 
     if args.check and rank == 0:
         from oracle.cref import CRef
@@ -233,6 +255,12 @@ def main():
         # dominant kernel of this path (largest total time)
         dom = max(ktimes.items(), key=lambda kv: kv[1][0] * kv[1][1])
         dom_name, (dom_ms, dom_n) = dom
+        if len(ktimes) == 1:
+            # one kernel per step: its average launch duration over the timed region itself (stream
+            # events around the K back-to-back launches; includes the inter-launch dispatch gaps)
+            dom_ms, dom_n, ksrc = region_ms, args.steps, "stream events over the timed region / steps"
+        else:
+            ksrc = f"per-launch HIP events, breakdown pass of {nbd} steps after the timed region"
         per_launch_bytes = ab["frame"] * (B if dom_name == "bm_pass_left" else 1)  # one launch covers B frames
         achieved = per_launch_bytes / (dom_ms * 1e-3) / 1e9
         roofline = {
@@ -243,7 +271,9 @@ def main():
             "basis": ("SURVEY 8(d) D3 B=W*H*(2+2*D*c+4) per frame; the fused kernel keeps the cost volume "
                       "in LDS/VGPRs, so this is the equivalent rate of a materialised-volume pipeline"
                       if args.path == "fused" else "SURVEY 8(d) D3 per-frame bytes over the K1+K2 pipeline"),
+            "kernel_ms_source": ksrc,
             "kernels_ms": {k: round(v[0], 5) for k, v in ktimes.items()},
+            "region_ms_per_step": round(region_ms, 5),
         }
         traffic = load_traffic()
         tr = traffic.get(f"{args.config}:{args.path}:{dom_name}")
@@ -331,6 +361,7 @@ def main():
         print(json.dumps(result), flush=True)
 
     matcher.close()
+    tmatcher.close()
     if ws > 1:
         dist.barrier()
         dist.destroy_process_group()
