@@ -98,8 +98,9 @@ def time_cpu_baseline(cfg, L, R, threads: int, min_seconds: float, max_frames: i
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=200)
-    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--steps", type=int, default=1000)
+    ap.add_argument("--warmup", type=int, default=500,
+                    help="untimed steps; the GPU needs ~20 ms of load to reach full clocks after host-side setup")
     ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
     ap.add_argument("--path", default="fused", choices=["fused", "volume"])
     ap.add_argument("--frames", type=int, default=4, help="distinct resident frame pairs per GPU")

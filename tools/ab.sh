@@ -4,7 +4,7 @@
 set -o pipefail
 for c in ${CONFIGS:-c2}; do
   for v in ${VARIANTS:-X=0}; do
-    r=$(env ${v//+/ } timeout -k 5 120 python bench.py --config $c --steps ${STEPS:-100} --warmup 10 --no-cpu-baseline --no-volume-roofline --no-e2e "$@" 2>/dev/null) || { echo "FAIL $c $v"; exit 1; }
+    r=$(env ${v//+/ } timeout -k 5 120 python bench.py --config $c --steps ${STEPS:-300} --warmup ${WARM:-500} --no-cpu-baseline --no-volume-roofline --no-e2e "$@" 2>/dev/null) || { echo "FAIL $c $v"; exit 1; }
     echo "$c $v $(echo "$r" | python -c "import json,sys;d=json.load(sys.stdin);print(d['value'], d['roofline']['kernels_ms'], 'batch4', d.get('batched',{}).get('value'))")"
   done
 done

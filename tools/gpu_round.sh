@@ -16,7 +16,7 @@ timeout -k 10 600 python bench.py > $O/bench_default.json 2> $O/bench_default.er
 cat $O/bench_default.json
 for c in ${CONFIGS:-c1 c3 c4 c5}; do
   echo "[gpu_round] bench $c"
-  timeout -k 10 300 python bench.py --config $c --steps 50 --warmup 5 --no-cpu-baseline > $O/bench_$c.json 2> $O/bench_$c.err || { tail -20 $O/bench_$c.err; exit 1; }
+  timeout -k 10 300 python bench.py --config $c --steps 300 --no-cpu-baseline > $O/bench_$c.json 2> $O/bench_$c.err || { tail -20 $O/bench_$c.err; exit 1; }
 done
 echo "[gpu_round] rocprof"
 for c in ${PROF_CONFIGS:-c2}; do
