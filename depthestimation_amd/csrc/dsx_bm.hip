@@ -436,25 +436,14 @@ __device__ __forceinline__ void bm2_segment(const Bm2Args &a, uint8_t *smem, int
             for (int q = 0; q < NCH; ++q) {
                 const int c0 = 8 * q;
                 uint32_t sn[8], so[8], rn[4], ro[4];
-                float rnf[8], rof[8];
-                if constexpr (FSS) {
-                    ref_chunkf(par, c0, rnf);
-                    ref_chunkf(par + 1, c0, rof);
-                } else {
-                    ref_chunk(par, c0, rn);
-                    ref_chunk(par + 1, c0, ro);
-                }
+                ref_chunk(par, c0, rn);
+                ref_chunk(par + 1, c0, ro);
                 s_chunk(par, c0, sn);
                 s_chunk(par + 1, c0, so);
 #pragma unroll
                 for (int c = 0; c < 8; ++c) {
                     if (c0 + c < NC) {
-                        if constexpr (FSS) {
-                            // cs + tn^2 - to^2: two v_sub_f32 + two v_fma_f32 (neg modifier)
-                            const float tn = rnf[c] - __uint_as_float(sn[c]);
-                            const float to = rof[c] - __uint_as_float(so[c]);
-                            cs[c0 + c] = __builtin_fmaf(-to, to, __builtin_fmaf(tn, tn, cs[c0 + c]));
-                        } else if constexpr (SSD) {
+                        if constexpr (SSD) {  // u32 SSD (R > 5 or the right / volume passes)
                             const int tn = (int)refv(rn, c) - (int)sn[c];
                             const int to = (int)refv(ro, c) - (int)so[c];
                             const int nto = (int)so[c] - (int)refv(ro, c);
