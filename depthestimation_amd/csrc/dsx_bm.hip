@@ -829,8 +829,8 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu((SSD &&
 }
 
 
-// Device copies of partitions, one per launch shape (kept for the process lifetime: a launch in
-// flight on any stream may still read one).
+// Device copies of partitions, one per launch shape (a launch in flight on any stream may still
+// read one, so entries are only dropped after a device-wide drain, at 256 shapes).
 struct PartKey {
     int dev, NG, S, sb, nframes, H, XL, XU, w8, nlev, w[4];
     bool operator==(const PartKey &o) const { return memcmp(this, &o, sizeof(PartKey)) == 0; }
@@ -844,6 +844,29 @@ static hipError_t bm2_partition_dev(const PartKey &k, int TX, const int **out) {
             *out = e.second;
             return hipSuccess;
         }
+    if (cache.size() >= 256) {
+        // bounded: drain every device that holds a table, then drop them all (a process cycling
+        // through many shapes pays one synchronisation per 256 new shapes)
+        int prev = 0;
+        (void)hipGetDevice(&prev);
+        for (size_t i = 0; i < cache.size(); ++i) {
+            bool seen = false;
+            for (size_t j = 0; j < i; ++j) seen = seen || cache[j].first.dev == cache[i].first.dev;
+            if (seen) continue;
+            (void)hipSetDevice(cache[i].first.dev);
+            hipError_t se = hipDeviceSynchronize();
+            if (se != hipSuccess) {
+                (void)hipSetDevice(prev);
+                return se;
+            }
+        }
+        for (auto &e : cache) {
+            (void)hipSetDevice(e.first.dev);
+            (void)hipFree(e.second);
+        }
+        (void)hipSetDevice(prev);
+        cache.clear();
+    }
     const std::vector<int> part = bm2_partition(k.NG, k.S, k.sb, k.nframes, k.H, k.XL, k.XU, TX, k.w8, k.nlev, k.w);
     int *d = nullptr;
     hipError_t e = hipMalloc(&d, part.size() * sizeof(int));

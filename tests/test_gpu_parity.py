@@ -219,3 +219,20 @@ def test_tiny_disparity_ranges_with_uniqueness(torch_dev, path, cost, D):
         kw = dict(min_disp=0, num_disp=D, block_size=3, cost=cost, uniqueness_ratio=u, disp12_max_diff=1)
         fixed, _ = _run(L, R, path=path, **kw)
         np.testing.assert_array_equal(fixed, stereo_bm(L, R, subpixel=True, **kw)["fixed"])
+
+
+def test_many_launch_shapes_partition_cache(torch_dev):
+    """More than 256 distinct launch shapes: the device partition-table cache drains and refills
+    (csrc/dsx_bm.hip, bm2_partition_dev) and results stay bit-exact across the refill."""
+    from depthestimation_amd.matcher import HipBlockMatcher
+    m = HipBlockMatcher(num_disp=16, block_size=3, uniqueness_ratio=0, disp12_max_diff=-1)
+    checked = 0
+    for W in range(40, 40 + 270):
+        L, R, _ = stereo_pair(6, W, 0, 16, seed=W)
+        fixed = m.compute(L, R)
+        if W % 67 == 0 or W >= 40 + 265:
+            ref = stereo_bm(L, R, 0, 16, 3, "sad", 0, -1, True)
+            assert np.array_equal(fixed, ref["fixed"]), W
+            checked += 1
+    m.close()
+    assert checked >= 5
