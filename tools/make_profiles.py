@@ -16,7 +16,8 @@ import shutil
 import sys
 from collections import defaultdict
 
-NAMES = {", 0>": "bm_pass_left", ", 1>": "bm_pass_right", ", 2>": "cost_volume", "vol_wta": "volume_wta"}
+NAMES = {", 0>": "bm_pass_left", ", 3>": "bm_pass_left", ", 1>": "bm_pass_right", ", 2>": "cost_volume", "vol_wta": "volume_wta",
+         "lr_fixup": "lr_fixup"}
 
 
 def short(k):
