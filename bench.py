@@ -30,20 +30,8 @@ sys.path.insert(0, ROOT)
 METRIC = "disparity Mpix/s at 1080p d_max=128; 1/2/4/8-GPU scaling + %HBM roofline"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level parameters)
 
-# BASELINE.json configs. c1 is the reference's CPU-runnable case; c4 is the
-# video stream case (its per-GPU frame is timed the same way); c2 is the headline.
-CONFIGS = {
-    "c1": dict(H=480, W=640, num_disp=64, block_size=5, cost="sad", uniqueness_ratio=0, disp12_max_diff=-1,
-               desc="C1 640x480 SAD 5x5 D=64 (stand-in for assets/stereo_pairs)"),
-    "c2": dict(H=1080, W=1920, num_disp=128, block_size=9, cost="sad", uniqueness_ratio=0, disp12_max_diff=-1,
-               desc="C2 1920x1080 synthetic rectified pair, SAD 9x9, D=128"),
-    "c3": dict(H=1080, W=1920, num_disp=256, block_size=11, cost="ssd", uniqueness_ratio=10, disp12_max_diff=1,
-               desc="C3 1920x1080 SSD 11x11 D=256 + sub-pixel + uniqueness + LR check"),
-    "c4": dict(H=720, W=1280, num_disp=128, block_size=5, cost="sad", uniqueness_ratio=10, disp12_max_diff=1,
-               desc="C4 1280x720 video frame, SAD 5x5, D=128 (reference defaults)"),
-    "c5": dict(H=2160, W=3840, num_disp=192, block_size=15, cost="sad", uniqueness_ratio=0, disp12_max_diff=-1,
-               desc="C5 3840x2160 SAD 15x15 D=192"),
-}
+# BASELINE.json configs, shared with the full-size parity tests
+from depthestimation_amd.configs import CONFIGS, REFERENCE_CHECKS, matcher_kwargs  # noqa: E402
 
 
 def algorithmic_bytes(cfg) -> dict:

@@ -102,6 +102,12 @@ struct dsx_handle {
     int cH = 0, cW = 0, cDp = 0, cCostBytes = 0;
     int lrFrames = 0;  // frames the LR buffers hold
     int lrParity = 0;  // which half of lrKeys the next frame's left pass fills
+    int lrDirty[2] = {0, 0};  // frames of each half holding keys that were not reset yet
+    // LR buffers are reused across calls: a call on another stream than the previous LR call
+    // waits for that call's lr_fixup (event) before its left pass writes the keys again
+    hipEvent_t lrDone = nullptr;
+    hipStream_t lrStream = nullptr;
+    bool lrPending = false;
     uint8_t *dL = nullptr, *dR = nullptr;
     int16_t *dFixed = nullptr;
     float *dFloat = nullptr;
@@ -139,6 +145,8 @@ void free_buffers(dsx_handle *h) {
     h->vol_bytes = 0;
     h->cH = h->cW = h->cDp = h->cCostBytes = 0;
     h->lrFrames = 0;
+    h->lrDirty[0] = h->lrDirty[1] = 0;
+    h->lrPending = false;
 }
 
 int ensure_buffers(dsx_handle *h, int H, int W, bool host_staging, int nframes = 1) {
@@ -166,6 +174,8 @@ int ensure_buffers(dsx_handle *h, int H, int W, bool host_staging, int nframes =
         DSX_HIP(hipStreamSynchronize(nullptr));
         h->lrFrames = nframes;
         h->lrParity = 0;
+        h->lrDirty[0] = h->lrDirty[1] = 0;
+        h->lrPending = false;
     }
 
     if ((h->p.path == DSX_PATH_VOLUME || h->p.aggregation) && !h->vol) {
@@ -311,6 +321,7 @@ int run(dsx_handle *h, const void *dL, const void *dR, int H, int W, int64_t str
         if (lr) {
             // the left pass also builds the right-view winners (every strip: a right pixel's
             // diagonal starts left of the valid band); lr_fixup applies the check afterwards
+            if (h->lrPending && h->lrStream != st) DSX_HIP(hipStreamWaitEvent(st, h->lrDone, 0));
             a.side = dsx::SIDE_LEFT_LR;
             a.lr_keys = h->lrKeys + (size_t)h->lrParity * H * W * h->lrFrames;
             a.dstar = h->dStar;
@@ -334,12 +345,22 @@ int run(dsx_handle *h, const void *dL, const void *dR, int H, int W, int64_t str
         if (tl) DSX_HIP(hipMemsetAsync(tl, 0, 12 * 8 * 65536, st));
         a.timeline = tl;
         DSX_LAUNCH(h, "bm_pass_left", st, dsx::launch_bm2(radius, ssd, h->g.NW, a, st));
-        if (lr)
+        if (lr) {
+            // this call dirties nframes frames of half P; lr_fixup resets every dirty frame of
+            // the other half (consumed by the previous call), however many frames that call had
+            const int P = h->lrParity;
             DSX_LAUNCH(h, "lr_fixup", st,
-                       dsx::launch_lr_fixup(h->dStar, a.lr_keys, h->lrKeys + (size_t)(h->lrParity ^ 1) * H * W * h->lrFrames,
-                                            H * nframes, W, h->p.min_disp, h->p.disp12_max_diff, a.kshift,
-                                            a.out_fixed, a.out_float, st));
-        if (lr) h->lrParity ^= 1;
+                       dsx::launch_lr_fixup(h->dStar, a.lr_keys, h->lrKeys + (size_t)(P ^ 1) * H * W * h->lrFrames,
+                                            H * nframes, H * h->lrDirty[P ^ 1], W, h->p.min_disp,
+                                            h->p.disp12_max_diff, a.kshift, a.out_fixed, a.out_float, st));
+            h->lrDirty[P ^ 1] = 0;
+            h->lrDirty[P] = nframes;
+            h->lrParity = P ^ 1;
+            if (!h->lrDone) DSX_HIP(hipEventCreateWithFlags(&h->lrDone, hipEventDisableTiming));
+            DSX_HIP(hipEventRecord(h->lrDone, st));
+            h->lrStream = st;
+            h->lrPending = true;
+        }
         if (tl) {
             std::vector<uint64_t> host(12 * 65536);
             DSX_HIP(hipStreamSynchronize(st));
@@ -718,6 +739,7 @@ int dsx_destroy(dsx_handle *h) {
         (void)hipEventDestroy(e.second);
     }
     free_buffers(h);
+    if (h->lrDone) (void)hipEventDestroy(h->lrDone);
     (void)hipStreamDestroy(h->stream);
     delete h;
     return DSX_OK;

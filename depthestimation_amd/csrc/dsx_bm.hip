@@ -830,15 +830,19 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu((SSD &&
 
 
 // Device copies of partitions, one per launch shape (a launch in flight on any stream may still
-// read one, so entries are only dropped after a device-wide drain, at 256 shapes).
+// read one, so entries are only dropped after a device-wide drain, at 256 shapes).  The caller
+// holds launch_mutex() from the lookup through the kernel launch: a table handed out is enqueued
+// on its stream before any other thread can evict (and so drain before freeing) it.
 struct PartKey {
     int dev, NG, S, sb, nframes, H, XL, XU, w8, nlev, w[4];
     bool operator==(const PartKey &o) const { return memcmp(this, &o, sizeof(PartKey)) == 0; }
 };
+static std::mutex &launch_mutex() {
+    static std::mutex mu;  // shared by every bm2 instantiation of this translation unit
+    return mu;
+}
 static hipError_t bm2_partition_dev(const PartKey &k, int TX, const int **out) {
-    static std::mutex mu;  // shared by every bm2 instantiation's launcher
     static std::vector<std::pair<PartKey, int *>> cache;
-    std::lock_guard<std::mutex> lock(mu);
     for (const auto &e : cache)
         if (e.first == k) {
             *out = e.second;
@@ -891,8 +895,9 @@ static hipError_t launch_bm2_side(const Bm2Args &a, hipStream_t st) {
     hipError_t e = hipGetDevice(&dev);
     if (e != hipSuccess) return e;
     if (dev < 0 || dev >= 64) return hipErrorInvalidDevice;
-    static std::mutex init_mu;  // first launch per device may come from several host threads
-    std::lock_guard<std::mutex> lock(init_mu);
+    // serialises the first-launch occupancy query per device and the partition-table lookup
+    // through the launch itself (see bm2_partition_dev)
+    std::lock_guard<std::mutex> lock(launch_mutex());
     if (!blocks_per_cu[dev]) {
         e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, G::SMEM);
         if (e != hipSuccess) return e;

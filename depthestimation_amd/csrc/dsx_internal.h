@@ -77,10 +77,11 @@ __device__ __forceinline__ int div_trunc_small(int num, int den2) {
 // nw = waves per block: SAD Dp = 128*nw (nw in {1,2,4}), SSD Dp = 64*nw (nw in {1,2,4,8}).
 hipError_t launch_bm2(int radius, bool ssd, int nw, const Bm2Args &a, hipStream_t st);
 hipError_t launch_volume_wta(int TX, bool ssd, const VolArgs &a, hipStream_t st);
-// LR check after the left pass: invalidate x where |dR(x - m - d*) - d*| > lr, reading this frame's
-// key buffer and resetting the other one (double-buffered keys, see dsx_api.hip).
-hipError_t launch_lr_fixup(const int16_t *dstar, const uint32_t *keys, uint32_t *keys_next, int H, int W, int m,
-                           int lr, int kshift, int16_t *out_fixed, float *out_float, hipStream_t st);
+// LR check after the left pass: invalidate x where |dR(x - m - d*) - d*| > lr over `rows` rows
+// (frames stacked), reading this call's key buffer and resetting the first `reset_rows` rows of
+// the other one (double-buffered keys, see dsx_api.hip).
+hipError_t launch_lr_fixup(const int16_t *dstar, const uint32_t *keys, uint32_t *keys_next, int rows, int reset_rows,
+                           int W, int m, int lr, int kshift, int16_t *out_fixed, float *out_float, hipStream_t st);
 
 size_t volume_smem_bytes(int TX, bool ssd, int Dp, int TPP, int W);
 

@@ -202,16 +202,18 @@ __global__ __launch_bounds__(kVolThreads) void vol_wta(VolArgs a) {
 // left pass has built the right-view winners by atomicMin over its cost diagonals.
 // ---------------------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void lr_fixup(const int16_t *__restrict__ dstar, const uint32_t *__restrict__ keys,
-                                              uint32_t *__restrict__ keys_next, int H, int W, int m, int lr, int kshift,
-                                              int16_t *out_fixed, float *out_float) {
-    // elementwise over H x W: the keys read here (this frame's buffer) are never written, and the
-    // other buffer (next frame's) is reset to ~0 - so no row-wide barrier is needed
+                                              uint32_t *__restrict__ keys_next, int rows, int reset_rows, int W, int m,
+                                              int lr, int kshift, int16_t *out_fixed, float *out_float) {
+    // elementwise over rows x W: the keys read here (this call's buffer) are never written, and
+    // the other buffer's dirty rows (reset_rows, consumed by the previous call) are reset to ~0 -
+    // so no row-wide barrier is needed
     const uint32_t mask = (1u << kshift) - 1u;
     const int y = blockIdx.y;
     const int x = blockIdx.x * blockDim.x + threadIdx.x;
     if (x >= W) return;
     const int64_t i = (int64_t)y * W + x;
-    keys_next[i] = 0xFFFFFFFFu;
+    if (y < reset_rows) keys_next[i] = 0xFFFFFFFFu;
+    if (y >= rows) return;
     const int b = dstar[i];
     if (b < 0) return;
     const int df = (int)(keys[i - m - b] & mask) - b;  // x - m - b in [0, W-1] for valid-band pixels
@@ -221,10 +223,11 @@ __global__ __launch_bounds__(256) void lr_fixup(const int16_t *__restrict__ dsta
     }
 }
 
-hipError_t launch_lr_fixup(const int16_t *dstar, const uint32_t *keys, uint32_t *keys_next, int H, int W, int m,
-                           int lr, int kshift, int16_t *out_fixed, float *out_float, hipStream_t st) {
-    hipLaunchKernelGGL(lr_fixup, dim3((unsigned)((W + 255) / 256), (unsigned)H), dim3(256), 0, st, dstar, keys, keys_next,
-                       H, W, m, lr, kshift, out_fixed, out_float);
+hipError_t launch_lr_fixup(const int16_t *dstar, const uint32_t *keys, uint32_t *keys_next, int rows, int reset_rows,
+                           int W, int m, int lr, int kshift, int16_t *out_fixed, float *out_float, hipStream_t st) {
+    const int gy = rows > reset_rows ? rows : reset_rows;
+    hipLaunchKernelGGL(lr_fixup, dim3((unsigned)((W + 255) / 256), (unsigned)gy), dim3(256), 0, st, dstar, keys, keys_next,
+                       rows, reset_rows, W, m, lr, kshift, out_fixed, out_float);
     return hipGetLastError();
 }
 

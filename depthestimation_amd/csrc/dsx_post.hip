@@ -87,11 +87,17 @@ __device__ __forceinline__ int uf_load(const int *parent, int x) {
     return __hip_atomic_load(parent + x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-__device__ __forceinline__ int uf_find(const int *parent, int x) {
+// Path halving: each visited non-root x is re-pointed at its grandparent.  Racy but safe: only
+// roots are ever CAS-linked (uf_unite), a non-root never becomes a root again, and every value
+// stored is an ancestor of x (indices only decrease along a chain), so concurrent halvings
+// and unions can only shorten chains.
+__device__ __forceinline__ int uf_find(int *parent, int x) {
     int p = uf_load(parent, x);
     while (p != x) {
+        const int g = uf_load(parent, p);
+        if (g != p) __hip_atomic_store(parent + x, g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         x = p;
-        p = uf_load(parent, x);
+        p = g;
     }
     return x;
 }

@@ -28,6 +28,38 @@ def _ptr(t):
     return t.data_ptr()
 
 
+def _device_index(t):
+    d = t.device
+    return d.index if d.index is not None else 0
+
+
+def _check_inputs_on(dev, *ts):
+    """Device tensors handed to a handle must live on the handle's GPU (the kernels read them
+    through raw pointers on that device)."""
+    for t in ts:
+        if not t.is_cuda:
+            raise ValueError("compute_device needs device tensors (use compute() for host arrays)")
+        if _device_index(t) != dev:
+            raise ValueError(f"tensor on cuda:{_device_index(t)} but the matcher runs on cuda:{dev}")
+
+
+def _check_out(t, shape, dtype_name, dev, name):
+    """Caller-owned output: a contiguous device tensor of the exact shape and dtype on the handle's
+    device (raw int pointers are the caller's responsibility and pass unchecked)."""
+    if t is None or isinstance(t, int):
+        return
+    if not hasattr(t, "data_ptr") or not getattr(t, "is_cuda", False):
+        raise ValueError(f"{name} must be a device tensor (or a raw device pointer)")
+    if str(t.dtype) != dtype_name:
+        raise ValueError(f"{name} must be {dtype_name.split('.')[-1]}, got {str(t.dtype).split('.')[-1]}")
+    if tuple(t.shape) != tuple(shape):
+        raise ValueError(f"{name} must have shape {tuple(shape)}, got {tuple(t.shape)}")
+    if not t.is_contiguous():
+        raise ValueError(f"{name} must be contiguous")
+    if _device_index(t) != dev:
+        raise ValueError(f"{name} on cuda:{_device_index(t)} but the matcher runs on cuda:{dev}")
+
+
 class HipBlockMatcher:
     """SAD/SSD block matcher running on one HIP device (one handle per thread / GPU)."""
 
@@ -132,10 +164,13 @@ class HipBlockMatcher:
             if str(left.dtype) != "torch.uint8" or left.stride(1) != 1 or right.stride(1) != 1 or \
                     left.stride(0) != right.stride(0):
                 raise ValueError("inputs must be uint8 with unit column stride and equal row strides")
-            if not left.is_cuda or not right.is_cuda:
-                raise ValueError("compute_device needs device tensors (use compute() for host arrays)")
+            _check_inputs_on(self.device, left, right)
             H, W = left.shape
             lp, rp, st = left.data_ptr(), right.data_ptr(), left.stride(0)
+        if out_fixed is None and out_float is None:
+            raise ValueError("at least one of out_fixed / out_float is required")
+        _check_out(out_fixed, (H, W), "torch.int16", self.device, "out_fixed")
+        _check_out(out_float, (H, W), "torch.float32", self.device, "out_float")
         if stream is None:
             sptr = None
         elif isinstance(stream, int):
@@ -150,19 +185,34 @@ class HipBlockMatcher:
         column stride, equal strides); outputs contiguous N x H x W.  Equals N compute_device calls."""
         if left.dim() != 3 or left.shape != right.shape or left.stride() != right.stride():
             raise ValueError("left and right must be N x H x W tensors of the same shape and strides")
-        if str(left.dtype) != "torch.uint8" or left.stride(2) != 1 or not left.is_cuda or not right.is_cuda:
+        if str(left.dtype) != "torch.uint8" or str(right.dtype) != "torch.uint8" or left.stride(2) != 1:
             raise ValueError("inputs must be uint8 device tensors with unit column stride")
+        _check_inputs_on(self.device, left, right)
         N, H, W = left.shape
+        if out_fixed is None and out_float is None:
+            raise ValueError("at least one of out_fixed / out_float is required")
+        _check_out(out_fixed, (N, H, W), "torch.int16", self.device, "out_fixed")
+        _check_out(out_float, (N, H, W), "torch.float32", self.device, "out_float")
         sptr = None if stream is None else (stream if isinstance(stream, int) else stream.cuda_stream)
         rc = _dsx.lib().dsx_compute_batch_device(self._handle(), N, left.data_ptr(), right.data_ptr(), left.stride(0),
                                                  H, W, left.stride(1), _ptr(out_fixed), _ptr(out_float), sptr)
         _dsx.check(rc, "dsx_compute_batch_device")
 
     def right_map_device(self, left, right, out_dR, stream=None):
+        """Right-view winner map dR (int16 H x W, -1 where the search range is empty)."""
+        if left.dim() != 2 or left.shape != right.shape or left.stride(0) != right.stride(0):
+            raise ValueError("left and right must be H x W tensors of the same shape and row stride")
+        if str(left.dtype) != "torch.uint8" or str(right.dtype) != "torch.uint8" or left.stride(1) != 1 \
+                or right.stride(1) != 1:
+            raise ValueError("inputs must be uint8 with unit column stride")
+        _check_inputs_on(self.device, left, right)
         H, W = left.shape
+        _check_out(out_dR, (H, W), "torch.int16", self.device, "out_dR")
+        if out_dR is None:
+            raise ValueError("out_dR is required")
         sptr = None if stream is None else (stream if isinstance(stream, int) else stream.cuda_stream)
         rc = _dsx.lib().dsx_right_map_device(self._handle(), left.data_ptr(), right.data_ptr(), H, W,
-                                             left.stride(0), out_dR.data_ptr(), sptr)
+                                             left.stride(0), _ptr(out_dR), sptr)
         _dsx.check(rc, "dsx_right_map_device")
 
     # -- timing -----------------------------------------------------------------------------
