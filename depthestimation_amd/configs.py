@@ -18,10 +18,14 @@ CONFIGS = {
                desc="C4 1280x720 video frame, SAD 5x5, D=128 (reference defaults)"),
     "c5": dict(H=2160, W=3840, num_disp=192, block_size=15, cost="sad", uniqueness_ratio=0, disp12_max_diff=-1,
                desc="C5 3840x2160 SAD 15x15 D=192"),
+    # not a BASELINE line: the C2 shape with the reference's default checks (stereo_core.py:20,22),
+    # reported beside the headline (bench.py "c2_reference_defaults")
+    "c2r": dict(H=1080, W=1920, num_disp=128, block_size=9, cost="sad", uniqueness_ratio=10, disp12_max_diff=1,
+                desc="C2 1920x1080 SAD 9x9 D=128 with the reference defaults uniqueness 10, disp12MaxDiff 1"),
 }
 
 # The reference's own defaults for the two matcher checks (stereo_core.py:20,22): the C2 shape
-# with them on is reported next to the headline (bench.py "c2_reference_defaults").
+# with them on ("c2r") is reported next to the headline (bench.py "c2_reference_defaults").
 REFERENCE_CHECKS = dict(uniqueness_ratio=10, disp12_max_diff=1)
 
 

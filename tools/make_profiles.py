@@ -2,6 +2,7 @@
   profiles/<tag>_kernel_stats.csv   rocprofv3 --kernel-trace --stats summary (verbatim)
   profiles/<tag>_pmc.txt            per-kernel average PMC values per dispatch
   profiles/traffic.json             {"<config>:<path>:<kernel>": {"hbm_bytes_per_launch": ...}}
+  profiles/valu_counts.json         {"<config>:<path>:<kernel>": {"SQ_INSTS_VALU": ...}} (VALU roofline)
 HBM bytes follow MI355X_MICROARCH.md (HBM section): FETCH_SIZE/WRITE_SIZE are KiB from separate
 --pmc passes; on gfx950 FETCH_SIZE counts half the bytes of wide coalesced reads, so it is doubled
 (exact for K2's 16-B streaming reads; an upper bound for the fused pass's 4-B row loads).
@@ -42,6 +43,8 @@ def main(src, tag, config, path):
              "# FETCH_SIZE / WRITE_SIZE in KiB; separate --pmc passes per counter group (tools/prof.sh)"]
     tp = os.path.join(prof, "traffic.json")
     traffic = json.load(open(tp)) if os.path.exists(tp) else {}
+    vp = os.path.join(prof, "valu_counts.json")
+    valu = json.load(open(vp)) if os.path.exists(vp) else {}
     for k, cs in acc.items():
         if "rocclr" in k:
             continue
@@ -56,11 +59,19 @@ def main(src, tag, config, path):
                 "hbm_bytes_per_launch": round(rd + wr), "read_bytes": round(rd), "write_bytes": round(wr),
                 "avg_ns": avg_ns.get(k), "source": f"profiles/{tag}_pmc.txt (2*FETCH_SIZE + WRITE_SIZE, KiB->B)"}
             lines.append(f"    => HBM bytes/launch (2*FETCH + WRITE) {rd + wr:,.0f}")
+        if "SQ_INSTS_VALU" in m:
+            e = {"SQ_INSTS_VALU": round(m["SQ_INSTS_VALU"]), "avg_ns": avg_ns.get(k),
+                 "source": f"profiles/{tag}_pmc.txt (rocprofv3 --pmc, average per dispatch)"}
+            for c in ("SQ_ACTIVE_INST_VALU", "SQ_ACTIVE_INST_VALU2", "SQ_THREAD_CYCLES_VALU", "GRBM_GUI_ACTIVE"):
+                if c in m:
+                    e[c] = round(m[c])
+            valu[f"{config}:{path}:{short(k)}"] = e
         if "SQ_WAVE_CYCLES" in m and "SQ_BUSY_CYCLES" in m:
             lines.append(f"    => VALU instr/wave {m.get('SQ_INSTS_VALU', 0) / max(m.get('SQ_WAVES', 1), 1):,.0f}; "
                          f"wait_any/wave_cycles {m['SQ_WAIT_ANY'] / m['SQ_WAVE_CYCLES']:.2f}")
     open(os.path.join(prof, f"{tag}_pmc.txt"), "w").write("\n".join(lines) + "\n")
     json.dump(traffic, open(tp, "w"), indent=1, sort_keys=True)
+    json.dump(valu, open(vp, "w"), indent=1, sort_keys=True)
 
 
 if __name__ == "__main__":
