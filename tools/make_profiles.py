@@ -17,8 +17,9 @@ import shutil
 import sys
 from collections import defaultdict
 
-NAMES = {", 0>": "bm_pass_left", ", 3>": "bm_pass_left", ", 1>": "bm_pass_right", ", 2>": "cost_volume", "vol_wta": "volume_wta",
-         "lr_fixup": "lr_fixup"}
+# kernel-name patterns, most specific first (vol_wta's template list also ends in ", 3>")
+NAMES = {"vol_wta": "volume_wta", "lr_fixup": "lr_fixup", ", 0>": "bm_pass_left", ", 3>": "bm_pass_left",
+         ", 1>": "bm_pass_right", ", 2>": "cost_volume"}
 
 
 def short(k):
