@@ -45,10 +45,11 @@ typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 // vol_wta: K2 of the volume path, one block per image row
 // ---------------------------------------------------------------------------------------
 // Lane (k, s) of a chunk owns the 16-disparity slice s of pixel xc0 + k (SAD 32 B, SSD 64 B)
-// and reads it straight from HBM into registers; a 3-deep register ring keeps two chunks in
-// flight while one is reduced.  Keys (cost << DB | d) give the lowest-d WTA; the TPP = Dp/16
+// and reads it straight from HBM into registers with non-temporal loads; a 3-deep register ring
+// keeps two chunks in flight while one is reduced (the prologue is issued in chunk order: a
+// prologue the scheduler reorders makes hipcc's loop vmcnt waits drain the ring every chunk).  Keys (cost << DB | d) give the lowest-d WTA; the TPP = Dp/16
 // lanes of a pixel combine with DPP / swizzle.  C(b-1), C(b+1) for the sub-pixel come from a
-// wave-private LDS copy of the slices.  With the LR check every cost also competes for its
+// wave-private LDS copy of the slices, stored vector-major so the copy is conflict-free.  With the LR check every cost also competes for its
 // right-view pixel through an LDS ds_min_u32 and the row is finalised after a barrier;
 // without it results go straight out.
 // Cost j (0..TX-1) of a lane's slice held as NV packed 16-B vectors.
@@ -86,7 +87,9 @@ __global__ __launch_bounds__(kVolThreads) void vol_wta(VolArgs a) {
     const uint32_t dmask = (1u << DB) - 1u;
 
     // LDS: per-lane slice scratch (sub-pixel neighbours, wave-private) | LR row state
-    uint4 *scratch = reinterpret_cast<uint4 *>(smem) + (size_t)tid * NV;  // lane slices in lane order
+    // vector-major (scratch[i][lane]): each ds_write_b128 group of 8 lanes covers 128 contiguous
+    // bytes; the lane-major copy (lane stride 32 / 64 B) cost 4.5 / 11 conflict cycles per LDS op
+    uint4 *scratch = reinterpret_cast<uint4 *>(smem);
     uint8_t *rowbase = smem + (size_t)kVolThreads * NV * 16;
     uint32_t *bestR = reinterpret_cast<uint32_t *>(rowbase);
     int16_t *rowFixed = reinterpret_cast<int16_t *>(rowbase + (size_t)round16(W * 4));
@@ -105,7 +108,7 @@ __global__ __launch_bounds__(kVolThreads) void vol_wta(VolArgs a) {
         const u32x4 *p = reinterpret_cast<const u32x4 *>(vrow + (size_t)x * Dp + dbase);
 #pragma unroll
         for (int i = 0; i < NV; ++i) {
-            const u32x4 t = p[i];
+            const u32x4 t = __builtin_nontemporal_load(&p[i]);
             v[i] = make_uint4(t.x, t.y, t.z, t.w);
         }
     };
@@ -115,7 +118,7 @@ __global__ __launch_bounds__(kVolThreads) void vol_wta(VolArgs a) {
         const bool inb = x < xb;
         if (a.subpix) {
 #pragma unroll
-            for (int i = 0; i < NV; ++i) scratch[i] = cur[i];
+            for (int i = 0; i < NV; ++i) scratch[i * kVolThreads + tid] = cur[i];
         }
         uint32_t best = 0xFFFFFFFFu;
 #pragma unroll
@@ -149,9 +152,14 @@ __global__ __launch_bounds__(kVolThreads) void vol_wta(VolArgs a) {
             if (a.subpix && b > 0 && b < D - 1) {
                 // the pixel's TPP slices are in consecutive lanes of this wave: scratch is in order
                 __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront", "local");
-                const CT *px = reinterpret_cast<const CT *>(reinterpret_cast<const uint4 *>(smem) + (size_t)(tid) * NV);
-                const int32_t cm = (int32_t)px[b - 1];
-                const int32_t cp = (int32_t)px[b + 1];
+                // C(d): element d % TX of lane tid + d / TX's slice
+                auto cost_at = [&](int d) __attribute__((always_inline)) -> int32_t {
+                    const int e = (d & (TX - 1)) * (int)sizeof(CT);
+                    const uint8_t *pv = reinterpret_cast<const uint8_t *>(scratch + (e >> 4) * kVolThreads + tid + d / TX);
+                    return (int32_t)*reinterpret_cast<const CT *>(pv + (e & 15));
+                };
+                const int32_t cm = cost_at(b - 1);
+                const int32_t cp = cost_at(b + 1);
                 int32_t den = cm + cp - 2 * (int32_t)cb;
                 den = den < 1 ? 1 : den;
                 f += div_trunc_small((cm - cp) * 16 + den, 2 * den);  // C division: truncation toward zero
@@ -169,7 +177,10 @@ __global__ __launch_bounds__(kVolThreads) void vol_wta(VolArgs a) {
     // RING-deep register ring: RING-1 chunks in flight while one is reduced
     uint4 rb[RING][NV];
 #pragma unroll
-    for (int i = 0; i < RING - 1; ++i) load(xa + i * XC, rb[i]);
+    for (int i = 0; i < RING - 1; ++i) {
+        load(xa + i * XC, rb[i]);
+        __builtin_amdgcn_sched_barrier(0);  // prologue in chunk order (see above)
+    }
     for (int xc0 = xa; xc0 < xb; xc0 += RING * XC) {
 #pragma unroll
         for (int i = 0; i < RING; ++i) {
