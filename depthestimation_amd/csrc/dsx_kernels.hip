@@ -213,32 +213,51 @@ __global__ __launch_bounds__(kVolThreads) void vol_wta(VolArgs a) {
 // left pass has built the right-view winners by atomicMin over its cost diagonals.
 // ---------------------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void lr_fixup(const int16_t *__restrict__ dstar, const uint32_t *__restrict__ keys,
-                                              uint32_t *__restrict__ keys_next, int rows, int reset_rows, int W, int m,
-                                              int lr, int kshift, int16_t *out_fixed, float *out_float) {
-    // elementwise over rows x W: the keys read here (this call's buffer) are never written, and
-    // the other buffer's dirty rows (reset_rows, consumed by the previous call) are reset to ~0 -
-    // so no row-wide barrier is needed
+                                              uint32_t *__restrict__ keys_next, int64_t n, int64_t nreset, int m, int lr,
+                                              int kshift, int16_t *out_fixed, float *out_float) {
+    // elementwise over the frames' flat pixel index i (4 pixels per thread, 8-B dstar / 16-B
+    // key-reset accesses): the keys read here (this call's buffer) are never written, and the
+    // other buffer's dirty pixels (nreset, consumed by the previous call) are reset to ~0 - so
+    // no row-wide barrier is needed.  Pixel i's right-view partner is key i - m - d*, inside its
+    // own row for every pixel with a winner (x >= m + D - 1 >= m + d*).
     const uint32_t mask = (1u << kshift) - 1u;
-    const int y = blockIdx.y;
-    const int x = blockIdx.x * blockDim.x + threadIdx.x;
-    if (x >= W) return;
-    const int64_t i = (int64_t)y * W + x;
-    if (y < reset_rows) keys_next[i] = 0xFFFFFFFFu;
-    if (y >= rows) return;
-    const int b = dstar[i];
-    if (b < 0) return;
-    const int df = (int)(keys[i - m - b] & mask) - b;  // x - m - b in [0, W-1] for valid-band pixels
-    if (df > lr || df < -lr) {
-        if (out_fixed) out_fixed[i] = (int16_t)((m - 1) * 16);
-        if (out_float) out_float[i] = (float)(m - 1);
+    const int64_t i0 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 4;
+    if (i0 < nreset) {
+        if (i0 + 4 <= nreset && ((uintptr_t)(keys_next + i0) & 15u) == 0) {
+            *reinterpret_cast<uint4 *>(keys_next + i0) = make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu);
+        } else {
+            for (int64_t i = i0; i < nreset && i < i0 + 4; ++i) keys_next[i] = 0xFFFFFFFFu;
+        }
+    }
+    if (i0 >= n) return;
+    int16_t b4[4];
+    if (i0 + 4 <= n) {
+        const uint2 v = *reinterpret_cast<const uint2 *>(dstar + i0);
+        b4[0] = (int16_t)(v.x & 0xFFFFu), b4[1] = (int16_t)(v.x >> 16), b4[2] = (int16_t)(v.y & 0xFFFFu), b4[3] = (int16_t)(v.y >> 16);
+    } else {
+        for (int j = 0; j < 4; ++j) b4[j] = i0 + j < n ? dstar[i0 + j] : (int16_t)-1;
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const int b = b4[j];
+        if (b < 0) continue;
+        const int64_t i = i0 + j;
+        const int df = (int)(keys[i - m - b] & mask) - b;
+        if (df > lr || df < -lr) {
+            if (out_fixed) out_fixed[i] = (int16_t)((m - 1) * 16);
+            if (out_float) out_float[i] = (float)(m - 1);
+        }
     }
 }
 
 hipError_t launch_lr_fixup(const int16_t *dstar, const uint32_t *keys, uint32_t *keys_next, int rows, int reset_rows,
                            int W, int m, int lr, int kshift, int16_t *out_fixed, float *out_float, hipStream_t st) {
-    const int gy = rows > reset_rows ? rows : reset_rows;
-    hipLaunchKernelGGL(lr_fixup, dim3((unsigned)((W + 255) / 256), (unsigned)gy), dim3(256), 0, st, dstar, keys, keys_next,
-                       rows, reset_rows, W, m, lr, kshift, out_fixed, out_float);
+    // dstar is hipMalloc'd, so the flat 4-pixel groups are 8-B aligned; the second key half
+    // starts at an odd multiple of H*W*frames elements, so its resets check 16-B alignment
+    const int64_t n = (int64_t)rows * W, nreset = (int64_t)reset_rows * W;
+    const int64_t work = (n > nreset ? n : nreset + 3) / 4 + 1;
+    hipLaunchKernelGGL(lr_fixup, dim3((unsigned)((work + 255) / 256)), dim3(256), 0, st, dstar, keys, keys_next, n, nreset,
+                       m, lr, kshift, out_fixed, out_float);
     return hipGetLastError();
 }
 
