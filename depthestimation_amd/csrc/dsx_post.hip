@@ -78,8 +78,9 @@ hipError_t launch_post_fast(const PostArgs &a, hipStream_t st) {
 //   2. detect_outliers (:37-70, :152-158): 5x5 BORDER_REFLECT_101 box mean / mean of squares
 //      (exact float64 window sums x 1/k^2 -> float32), |d - mean| > thr * std on d > 0 -> 0.
 //   3. 3x3 median (:169) and depth: post_fast with crop 0.
-// Components use atomic union-find (parents only ever point to smaller indices, CAS links a root
-// under the smaller root), a flatten + size-count pass and an apply pass.
+// Components use union-find (parents only ever point to smaller indices, CAS links a root under
+// the smaller root): tile-local in LDS first, then global merges of the tile-border edges, a
+// flatten + size-count pass (wave-aggregated atomics) and an apply pass.
 // ---------------------------------------------------------------------------------------------
 #pragma clang fp contract(off)
 
@@ -119,44 +120,122 @@ __device__ __forceinline__ void uf_unite(int *parent, int a, int b) {
     }
 }
 
-__global__ __launch_bounds__(256) void speckle_init(PostFullArgs a) {
-    const int Wc = a.W - a.crop;
-    const int64_t n = (int64_t)a.H * Wc;
-    for (int64_t p = (int64_t)blockIdx.x * 256 + threadIdx.x; p < n; p += (int64_t)gridDim.x * 256) {
-        const int y = (int)(p / Wc), x = (int)(p - (int64_t)y * Wc);
-        const float v = a.disp[(int64_t)y * a.in_pitch + a.crop + x];
-        const int16_t d16 = (int16_t)(int)__builtin_truncf(v * 16.0f);
-        a.v16[p] = d16;
-        a.parent[p] = d16 != 0 ? (int)p : -1;
-        a.count[p] = 0;
+// --- connected components: tile-local union-find in LDS, then global merges across tile edges
+constexpr int kCcTX = 32, kCcTY = 32;  // component tile (4 pixels per thread of a 256-thread block)
+
+__device__ __forceinline__ int ufl_find(int *pl, int x) {
+    int p = pl[x];
+    while (p != x) {
+        const int g = pl[p];
+        if (g != p) pl[x] = g;  // halving, as uf_find
+        x = p;
+        p = g;
+    }
+    return x;
+}
+
+__device__ __forceinline__ void ufl_unite(int *pl, int a, int b) {
+    while (true) {
+        a = ufl_find(pl, a);
+        b = ufl_find(pl, b);
+        if (a == b) return;
+        if (a < b) {
+            const int t = a;
+            a = b;
+            b = t;
+        }
+        if (atomicCAS(pl + a, a, b) == a) return;
     }
 }
 
-__global__ __launch_bounds__(256) void speckle_union(PostFullArgs a) {
+__device__ __forceinline__ bool joins(int u, int v, int md) { return u != 0 && v != 0 && abs(u - v) <= md; }
+
+// Tile pass: d16 = int16(trunc(d * 16)) of the cropped map, union-find of the tile's edges in LDS
+// (local indices are row-major, so "root = smallest index" is the same order globally), then
+// parent[p] = global index of p's tile-local root (-1 for 0 = newVal pixels), count[p] = 0.
+__global__ __launch_bounds__(256) void speckle_local(PostFullArgs a) {
+    __shared__ int pl[kCcTX * kCcTY];
+    __shared__ int16_t vl[kCcTX * kCcTY];
     const int Wc = a.W - a.crop;
-    const int64_t n = (int64_t)a.H * Wc;
-    for (int64_t p = (int64_t)blockIdx.x * 256 + threadIdx.x; p < n; p += (int64_t)gridDim.x * 256) {
-        const int v = a.v16[p];
+    const int x0 = blockIdx.x * kCcTX, y0 = blockIdx.y * kCcTY;
+    const int tw = min(kCcTX, Wc - x0), th = min(kCcTY, a.H - y0);
+    for (int i = threadIdx.x; i < kCcTX * kCcTY; i += 256) {
+        const int ly = i / kCcTX, lx = i - ly * kCcTX;
+        int16_t d16 = 0;
+        if (lx < tw && ly < th) {
+            const float v = a.disp[(int64_t)(y0 + ly) * a.in_pitch + a.crop + x0 + lx];
+            d16 = (int16_t)(int)__builtin_truncf(v * 16.0f);
+            const int64_t p = (int64_t)(y0 + ly) * Wc + x0 + lx;
+            a.v16[p] = d16;
+            a.count[p] = 0;
+        }
+        vl[i] = d16;
+        pl[i] = d16 != 0 ? i : -1;
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < kCcTX * kCcTY; i += 256) {
+        const int ly = i / kCcTX, lx = i - ly * kCcTX;
+        const int v = vl[i];
         if (v == 0) continue;
-        const int y = (int)(p / Wc), x = (int)(p - (int64_t)y * Wc);
-        if (x > 0) {
-            const int u = a.v16[p - 1];
-            if (u != 0 && abs(u - v) <= a.max_diff16) uf_unite(a.parent, (int)p, (int)p - 1);
-        }
-        if (y > 0) {
-            const int u = a.v16[p - Wc];
-            if (u != 0 && abs(u - v) <= a.max_diff16) uf_unite(a.parent, (int)p, (int)(p - Wc));
+        if (lx > 0 && joins(vl[i - 1], v, a.max_diff16)) ufl_unite(pl, i, i - 1);
+        if (ly > 0 && joins(vl[i - kCcTX], v, a.max_diff16)) ufl_unite(pl, i, i - kCcTX);
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < kCcTX * kCcTY; i += 256) {
+        const int ly = i / kCcTX, lx = i - ly * kCcTX;
+        if (lx >= tw || ly >= th) continue;
+        const int64_t p = (int64_t)(y0 + ly) * Wc + x0 + lx;
+        if (vl[i] == 0) {
+            a.parent[p] = -1;
+        } else {
+            const int r = ufl_find(pl, i);
+            const int ry = r / kCcTX, rx = r - ry * kCcTX;
+            a.parent[p] = (int)((int64_t)(y0 + ry) * Wc + x0 + rx);
         }
     }
 }
 
+// Merge pass: the edges that cross tile borders (left column and top row of every tile).
+__global__ __launch_bounds__(256) void speckle_merge(PostFullArgs a, int ntx, int nty) {
+    const int Wc = a.W - a.crop;
+    const int64_t nv = (int64_t)a.H * (ntx - 1), nh = (int64_t)(nty - 1) * Wc;
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < nv + nh; i += (int64_t)gridDim.x * 256) {
+        int y, x, q;
+        if (i < nv) {
+            y = (int)(i / (ntx - 1));
+            x = (int)(i - (int64_t)y * (ntx - 1) + 1) * kCcTX;
+            q = 1;
+        } else {
+            const int64_t j = i - nv;
+            y = (int)(j / Wc + 1) * kCcTY;
+            x = (int)(j % Wc);
+            q = Wc;
+        }
+        const int p = y * Wc + x;
+        if (joins(a.v16[p], a.v16[p - q], a.max_diff16)) uf_unite(a.parent, p, p - q);
+    }
+}
+
+// Flatten + component sizes: root[p] = find(p); one atomicAdd per (wave, root) with the number of
+// the wave's pixels in it (a large component's pixels otherwise all add into one address).
 __global__ __launch_bounds__(256) void speckle_count(PostFullArgs a) {
-    const int64_t n = (int64_t)a.H * (a.W - a.crop);
-    for (int64_t p = (int64_t)blockIdx.x * 256 + threadIdx.x; p < n; p += (int64_t)gridDim.x * 256) {
-        if (a.v16[p] == 0) continue;
-        const int r = uf_find(a.parent, (int)p);
-        atomicAdd(a.count + r, 1);
-        a.root[p] = r;
+    const int n = a.H * (a.W - a.crop);  // < 2^31 (host check)
+    const int lane = threadIdx.x & 63;
+    for (int p0 = blockIdx.x * 256 + (threadIdx.x & ~63); p0 < n; p0 += gridDim.x * 256) {
+        const int p = p0 + lane;
+        int r = -1;
+        if (p < n && a.v16[p] != 0) {
+            r = uf_find(a.parent, p);
+            a.root[p] = r;
+        }
+        uint64_t act = __ballot(r >= 0);
+        while (act) {
+            const int leader = __ffsll((unsigned long long)act) - 1;
+            const int r0 = __shfl(r, leader);
+            const uint64_t m = __ballot(r == r0);
+            if (lane == leader) atomicAdd(a.count + r0, __popcll(m));
+            act &= ~m;
+        }
     }
 }
 
@@ -221,8 +300,13 @@ hipError_t launch_post_full(PostFullArgs a, void *ws, hipStream_t st) {
     a.t0 = reinterpret_cast<float *>(w + 3 * r(n * 4) + r(n * 2));
     a.t1 = reinterpret_cast<float *>(w + 3 * r(n * 4) + r(n * 2) + r(n * 4));
     const int grid = (int)std::min<size_t>((n + 255) / 256, 4096);
-    hipLaunchKernelGGL(speckle_init, dim3(grid), dim3(256), 0, st, a);
-    hipLaunchKernelGGL(speckle_union, dim3(grid), dim3(256), 0, st, a);
+    const int ntx = (Wc + kCcTX - 1) / kCcTX, nty = (a.H + kCcTY - 1) / kCcTY;
+    hipLaunchKernelGGL(speckle_local, dim3(ntx, nty), dim3(256), 0, st, a);
+    if (ntx > 1 || nty > 1) {
+        const int64_t nb = (int64_t)a.H * (ntx - 1) + (int64_t)(nty - 1) * Wc;
+        hipLaunchKernelGGL(speckle_merge, dim3((unsigned)std::min<int64_t>((nb + 255) / 256, 4096)), dim3(256), 0, st, a,
+                           ntx, nty);
+    }
     hipLaunchKernelGGL(speckle_count, dim3(grid), dim3(256), 0, st, a);
     hipLaunchKernelGGL(speckle_apply, dim3(grid), dim3(256), 0, st, a);
     const float *med_in = a.t0;
