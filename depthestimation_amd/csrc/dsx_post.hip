@@ -187,56 +187,113 @@ __global__ __launch_bounds__(256) void speckle_local(PostFullArgs a) {
         const int64_t p = (int64_t)(y0 + ly) * Wc + x0 + lx;
         if (vl[i] == 0) {
             a.parent[p] = -1;
+            a.root[p] = -1;
         } else {
             const int r = ufl_find(pl, i);
             const int ry = r / kCcTX, rx = r - ry * kCcTX;
-            a.parent[p] = (int)((int64_t)(y0 + ry) * Wc + x0 + rx);
+            const int g = (int)((int64_t)(y0 + ry) * Wc + x0 + rx);
+            a.parent[p] = g;
+            a.root[p] = g;  // tile-local root, kept for the merge / count passes
         }
     }
 }
 
-// Merge pass: the edges that cross tile borders (left column and top row of every tile).
+// Merge pass: the edges that cross tile borders (left column and top row of every tile), one
+// union per border edge whose (local root, local root) pair differs from the previous edge's
+// along the border (a border run of one pair of tile components needs a single union).
 __global__ __launch_bounds__(256) void speckle_merge(PostFullArgs a, int ntx, int nty) {
     const int Wc = a.W - a.crop;
     const int64_t nv = (int64_t)a.H * (ntx - 1), nh = (int64_t)(nty - 1) * Wc;
+    const int md = a.max_diff16;
     for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < nv + nh; i += (int64_t)gridDim.x * 256) {
-        int y, x, q;
+        int y, x, q, s;  // edge p - q -> p; s = step to the previous edge along the border
         if (i < nv) {
             y = (int)(i / (ntx - 1));
             x = (int)(i - (int64_t)y * (ntx - 1) + 1) * kCcTX;
             q = 1;
+            s = y > 0 ? Wc : 0;
         } else {
             const int64_t j = i - nv;
             y = (int)(j / Wc + 1) * kCcTY;
             x = (int)(j % Wc);
             q = Wc;
+            s = x > 0 ? 1 : 0;
         }
         const int p = y * Wc + x;
-        if (joins(a.v16[p], a.v16[p - q], a.max_diff16)) uf_unite(a.parent, p, p - q);
+        if (!joins(a.v16[p], a.v16[p - q], md)) continue;
+        if (s && joins(a.v16[p - s], a.v16[p - s - q], md) && a.root[p] == a.root[p - s] &&
+            a.root[p - q] == a.root[p - s - q])
+            continue;  // same pair as the previous edge: already united there
+        uf_unite(a.parent, p, p - q);
     }
 }
 
-// Flatten + component sizes: root[p] = find(p); one atomicAdd per (wave, root) with the number of
-// the wave's pixels in it (a large component's pixels otherwise all add into one address).
+// Resolve pass: every tile-local root finds its global root (parents then point straight at it).
+// The walk is read-only: a halving store racing with another root's final store could put an
+// intermediate ancestor back over it.
+__global__ __launch_bounds__(256) void speckle_resolve(PostFullArgs a) {
+    const int n = a.H * (a.W - a.crop);
+    for (int p = blockIdx.x * 256 + threadIdx.x; p < n; p += gridDim.x * 256) {
+        if (a.root[p] != p) continue;
+        int x = p, q = uf_load(a.parent, p);
+        while (q != x) {
+            x = q;
+            q = uf_load(a.parent, x);
+        }
+        if (x != p) __hip_atomic_store(a.parent + p, x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
+
+// Component sizes: root[p] = parent[local root of p] (final after the resolve pass).  Counts are
+// aggregated per wave (ballot over equal roots), then per block in an LDS table of (root, count)
+// slots, and reach global memory as one atomicAdd per (block, root): a large component's pixels
+// all adding into one address serialise at the memory-side atomic unit (C4: 28k same-address
+// wave atomics took 116 us).
+constexpr int kCntSlots = 128;
 __global__ __launch_bounds__(256) void speckle_count(PostFullArgs a) {
+    __shared__ int skey[kCntSlots];
+    __shared__ int scnt[kCntSlots];
+    for (int i = threadIdx.x; i < kCntSlots; i += 256) {
+        skey[i] = -1;
+        scnt[i] = 0;
+    }
+    __syncthreads();
     const int n = a.H * (a.W - a.crop);  // < 2^31 (host check)
     const int lane = threadIdx.x & 63;
     for (int p0 = blockIdx.x * 256 + (threadIdx.x & ~63); p0 < n; p0 += gridDim.x * 256) {
         const int p = p0 + lane;
         int r = -1;
-        if (p < n && a.v16[p] != 0) {
-            r = uf_find(a.parent, p);
-            a.root[p] = r;
+        if (p < n) {
+            const int lr = a.root[p];
+            if (lr >= 0) {
+                r = a.parent[lr];
+                a.root[p] = r;
+            }
         }
         uint64_t act = __ballot(r >= 0);
         while (act) {
             const int leader = __ffsll((unsigned long long)act) - 1;
             const int r0 = __shfl(r, leader);
             const uint64_t m = __ballot(r == r0);
-            if (lane == leader) atomicAdd(a.count + r0, __popcll(m));
+            if (lane == leader) {
+                const int c = __popcll(m);
+                bool done = false;
+                for (int t = 0, h = (int)(((unsigned)r0 * 2654435761u) >> 25); t < 8; ++t, h = (h + 1) & (kCntSlots - 1)) {
+                    const int k = atomicCAS(&skey[h], -1, r0);
+                    if (k == -1 || k == r0) {
+                        atomicAdd(&scnt[h], c);
+                        done = true;
+                        break;
+                    }
+                }
+                if (!done) atomicAdd(a.count + r0, c);  // table crowded: straight to global
+            }
             act &= ~m;
         }
     }
+    __syncthreads();
+    for (int i = threadIdx.x; i < kCntSlots; i += 256)
+        if (skey[i] >= 0) atomicAdd(a.count + skey[i], scnt[i]);
 }
 
 __global__ __launch_bounds__(256) void speckle_apply(PostFullArgs a) {
@@ -307,7 +364,8 @@ hipError_t launch_post_full(PostFullArgs a, void *ws, hipStream_t st) {
         hipLaunchKernelGGL(speckle_merge, dim3((unsigned)std::min<int64_t>((nb + 255) / 256, 4096)), dim3(256), 0, st, a,
                            ntx, nty);
     }
-    hipLaunchKernelGGL(speckle_count, dim3(grid), dim3(256), 0, st, a);
+    hipLaunchKernelGGL(speckle_resolve, dim3(grid), dim3(256), 0, st, a);
+    hipLaunchKernelGGL(speckle_count, dim3((unsigned)std::min<size_t>((n + 255) / 256, 1024)), dim3(256), 0, st, a);
     hipLaunchKernelGGL(speckle_apply, dim3(grid), dim3(256), 0, st, a);
     const float *med_in = a.t0;
     if (a.apply_outliers) {
