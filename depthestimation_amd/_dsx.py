@@ -31,6 +31,7 @@ EXPORTS = (
     "dsx_version", "dsx_device_count", "dsx_default_params", "dsx_check_params", "dsx_create",
     "dsx_set_params", "dsx_compute_host", "dsx_compute_device", "dsx_compute_batch_device", "dsx_right_map_device",
     "dsx_postprocess_fast_device", "dsx_postprocess_workspace_bytes", "dsx_postprocess_full_device",
+    "dsx_postprocess_full_ex_device", "dsx_fill_holes_workspace_bytes", "dsx_fill_holes_device",
     "dsx_rectify_device",
     "dsx_kernel_times", "dsx_reset_times", "dsx_workspace_bytes", "dsx_destroy", "dsx_last_error",
     "dsx_comm_init_all", "dsx_comm_size", "dsx_bcast", "dsx_comm_destroy",
@@ -80,6 +81,12 @@ def _bind(lib):
                                                         ctypes.c_double, i32, vp, vp, ctypes.c_double,
                                                         ctypes.c_double, ctypes.c_double, ctypes.c_double,
                                                         ctypes.c_double, i32, vp, ctypes.c_size_t, vp]),
+        "dsx_postprocess_full_ex_device": (ctypes.c_int, [vp, i32, i32, i64, i32, i32, ctypes.c_double, i32,
+                                                           ctypes.c_double, i32, i32, vp, vp, ctypes.c_double,
+                                                           ctypes.c_double, ctypes.c_double, ctypes.c_double,
+                                                           ctypes.c_double, i32, vp, ctypes.c_size_t, vp]),
+        "dsx_fill_holes_workspace_bytes": (ctypes.c_size_t, [i32, i32]),
+        "dsx_fill_holes_device": (ctypes.c_int, [vp, i32, i32, i64, i32, vp, vp, ctypes.c_size_t, vp]),
         "dsx_rectify_device": (ctypes.c_int, [vp, i32, i32, i64, i32, vp, vp, i32, i32, vp, vp]),
         "dsx_postprocess_fast_device": (ctypes.c_int, [vp, i32, i32, i64, i32, vp, vp, ctypes.c_double,
                                                         ctypes.c_double, ctypes.c_double, ctypes.c_double,

@@ -571,7 +571,20 @@ int dsx_postprocess_full_device(const void *d_disp, int32_t H, int32_t W, int64_
                                 void *d_out_depth, double focal_length, double baseline, double doffs, double eps,
                                 double max_depth, int32_t has_max_depth, void *d_workspace,
                                 size_t workspace_bytes, void *hip_stream) {
+    return dsx_postprocess_full_ex_device(d_disp, H, W, in_pitch, crop, max_speckle_size, max_diff,
+                                          apply_outlier_removal, outlier_threshold, outlier_kernel, 0, d_out_disp,
+                                          d_out_depth, focal_length, baseline, doffs, eps, max_depth, has_max_depth,
+                                          d_workspace, workspace_bytes, hip_stream);
+}
+
+int dsx_postprocess_full_ex_device(const void *d_disp, int32_t H, int32_t W, int64_t in_pitch, int32_t crop,
+                                   int32_t max_speckle_size, double max_diff, int32_t apply_outlier_removal,
+                                   double outlier_threshold, int32_t outlier_kernel, int32_t fill_radius,
+                                   void *d_out_disp, void *d_out_depth, double focal_length, double baseline,
+                                   double doffs, double eps, double max_depth, int32_t has_max_depth,
+                                   void *d_workspace, size_t workspace_bytes, void *hip_stream) {
     g_err.clear();
+    if (fill_radius < 0) return fail(DSX_EINVAL, "fill_radius must be >= 0");
     if (!d_disp) return fail(DSX_EINVAL, "d_disp is NULL");
     if (H <= 0 || W <= 0 || in_pitch < W || crop < 0) return fail(DSX_EINVAL, "bad shape / pitch / crop");
     if (outlier_kernel < 1 || (outlier_kernel & 1) == 0) return fail(DSX_EINVAL, "outlier_kernel must be odd");
@@ -597,7 +610,27 @@ int dsx_postprocess_full_device(const void *d_disp, int32_t H, int32_t W, int64_
     a.eps = (float)eps;
     a.max_depth = (float)max_depth;
     a.has_max = has_max_depth ? 1 : 0;
+    a.fill_radius = fill_radius;
     DSX_HIP(dsx::launch_post_full(a, d_workspace, static_cast<hipStream_t>(hip_stream)));
+    return DSX_OK;
+}
+
+size_t dsx_fill_holes_workspace_bytes(int32_t H, int32_t W) {
+    if (H <= 0 || W <= 0) return 0;
+    return dsx::inpaint_workspace(H, W);
+}
+
+int dsx_fill_holes_device(const void *d_disp, int32_t H, int32_t W, int64_t in_pitch, int32_t radius, void *d_out,
+                          void *d_workspace, size_t workspace_bytes, void *hip_stream) {
+    g_err.clear();
+    if (!d_disp || !d_out) return fail(DSX_EINVAL, "NULL input or output");
+    if (H <= 0 || W <= 0 || in_pitch < W) return fail(DSX_EINVAL, "bad shape / pitch");
+    if (radius < 0) return fail(DSX_EINVAL, "radius must be >= 0");
+    if ((int64_t)H * W > 0x7FFFFFFF) return fail(DSX_EINVAL, "image too large");
+    if (!d_workspace || workspace_bytes < dsx::inpaint_workspace(H, W))
+        return fail(DSX_EINVAL, "workspace too small (dsx_fill_holes_workspace_bytes)");
+    DSX_HIP(dsx::launch_inpaint(static_cast<const float *>(d_disp), in_pitch, H, W, radius, static_cast<float *>(d_out),
+                                d_workspace, static_cast<hipStream_t>(hip_stream)));
     return DSX_OK;
 }
 

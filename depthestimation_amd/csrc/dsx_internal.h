@@ -118,13 +118,20 @@ struct PostFullArgs {
     float *out_disp, *out_depth;
     float fB, doffs, eps, max_depth;
     int has_max;
+    int fill_radius;  // > 0: Telea hole filling (radius) between the outlier removal and the median
+    int tail_t1;      // post_tail writes the outlier-cleaned map to t1 instead of the median (set internally)
     // workspace views (set by launch_post_full)
-    int *parent, *count, *root;
+    int *parent, *count, *root, *lsz;
     int16_t *v16;
     float *t0, *t1;
 };
 size_t post_full_workspace(int H, int W, int crop);
 hipError_t launch_post_full(PostFullArgs a, void *ws, hipStream_t st);
+
+// Hole filling (dsx_inpaint.hip): fill_holes(method='inpaint') on d <= 0, layered Telea marching.
+// Synchronises the stream once per 8 layers (frontier read-back).
+size_t inpaint_workspace(int H, int W);
+hipError_t launch_inpaint(const float *in, int64_t pitch, int H, int W, int radius, float *out, void *ws, hipStream_t st);
 
 // Rectification (dsx_rectify.hip): gray conversion fused with the fixed-point bilinear remap.
 struct RectArgs {

@@ -79,8 +79,9 @@ hipError_t launch_post_fast(const PostArgs &a, hipStream_t st) {
 //      (exact float64 window sums x 1/k^2 -> float32), |d - mean| > thr * std on d > 0 -> 0.
 //   3. 3x3 median (:169) and depth: post_fast with crop 0.
 // Components use union-find (parents only ever point to smaller indices, CAS links a root under
-// the smaller root): tile-local in LDS first, then global merges of the tile-border edges, a
-// flatten + size-count pass (wave-aggregated atomics) and an apply pass.
+// the smaller root): tile-local in LDS first (with tile-local sizes), then global merges of the
+// tile-border edges between tile-local roots, and a resolve pass that points every tile-local
+// root at its component's root and adds its size there.
 // ---------------------------------------------------------------------------------------------
 #pragma clang fp contract(off)
 
@@ -151,10 +152,12 @@ __device__ __forceinline__ void ufl_unite(int *pl, int a, int b) {
 __device__ __forceinline__ bool joins(int u, int v, int md) { return u != 0 && v != 0 && abs(u - v) <= md; }
 
 // Tile pass: d16 = int16(trunc(d * 16)) of the cropped map, union-find of the tile's edges in LDS
-// (local indices are row-major, so "root = smallest index" is the same order globally), then
-// parent[p] = global index of p's tile-local root (-1 for 0 = newVal pixels), count[p] = 0.
+// (local indices are row-major, so "root = smallest index" is the same order globally).  Writes
+// v16[p] and root[p] = global index of p's tile-local root (-1 for 0 = newVal pixels) for every
+// pixel, and for each local root g: parent[g] = g, count[g] = 0, lsz[g] = its tile-local size.
 __global__ __launch_bounds__(256) void speckle_local(PostFullArgs a) {
     __shared__ int pl[kCcTX * kCcTY];
+    __shared__ int cl[kCcTX * kCcTY];
     __shared__ int16_t vl[kCcTX * kCcTY];
     const int Wc = a.W - a.crop;
     const int x0 = blockIdx.x * kCcTX, y0 = blockIdx.y * kCcTY;
@@ -165,12 +168,11 @@ __global__ __launch_bounds__(256) void speckle_local(PostFullArgs a) {
         if (lx < tw && ly < th) {
             const float v = a.disp[(int64_t)(y0 + ly) * a.in_pitch + a.crop + x0 + lx];
             d16 = (int16_t)(int)__builtin_truncf(v * 16.0f);
-            const int64_t p = (int64_t)(y0 + ly) * Wc + x0 + lx;
-            a.v16[p] = d16;
-            a.count[p] = 0;
+            a.v16[(int64_t)(y0 + ly) * Wc + x0 + lx] = d16;
         }
         vl[i] = d16;
         pl[i] = d16 != 0 ? i : -1;
+        cl[i] = 0;
     }
     __syncthreads();
     for (int i = threadIdx.x; i < kCcTX * kCcTY; i += 256) {
@@ -186,15 +188,23 @@ __global__ __launch_bounds__(256) void speckle_local(PostFullArgs a) {
         if (lx >= tw || ly >= th) continue;
         const int64_t p = (int64_t)(y0 + ly) * Wc + x0 + lx;
         if (vl[i] == 0) {
-            a.parent[p] = -1;
             a.root[p] = -1;
         } else {
             const int r = ufl_find(pl, i);
+            pl[i] = r;  // flattened (only ever an ancestor, as the halving stores)
+            atomicAdd(&cl[r], 1);
             const int ry = r / kCcTX, rx = r - ry * kCcTX;
-            const int g = (int)((int64_t)(y0 + ry) * Wc + x0 + rx);
-            a.parent[p] = g;
-            a.root[p] = g;  // tile-local root, kept for the merge / count passes
+            a.root[p] = (int)((int64_t)(y0 + ry) * Wc + x0 + rx);
         }
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < kCcTX * kCcTY; i += 256) {
+        if (pl[i] != i) continue;  // local roots only (vl != 0)
+        const int ly = i / kCcTX, lx = i - ly * kCcTX;
+        const int g = (int)((int64_t)(y0 + ly) * Wc + x0 + lx);
+        a.parent[g] = g;
+        a.count[g] = 0;
+        a.lsz[g] = cl[i];
     }
 }
 
@@ -224,15 +234,16 @@ __global__ __launch_bounds__(256) void speckle_merge(PostFullArgs a, int ntx, in
         if (s && joins(a.v16[p - s], a.v16[p - s - q], md) && a.root[p] == a.root[p - s] &&
             a.root[p - q] == a.root[p - s - q])
             continue;  // same pair as the previous edge: already united there
-        uf_unite(a.parent, p, p - q);
+        uf_unite(a.parent, a.root[p], a.root[p - q]);  // parents exist for local roots only
     }
 }
 
-// Resolve pass: every tile-local root finds its global root (parents then point straight at it).
-// The walk is read-only: a halving store racing with another root's final store could put an
+// Resolve pass: every tile-local root g finds its global root r (parent[g] = r afterwards) and adds
+// its tile-local size to count[r] - a component's size as one atomic per tile it touches.  The
+// walk is read-only: a halving store racing with another root's final store could put an
 // intermediate ancestor back over it.
 __global__ __launch_bounds__(256) void speckle_resolve(PostFullArgs a) {
-    const int n = a.H * (a.W - a.crop);
+    const int n = a.H * (a.W - a.crop);  // < 2^31 (host check)
     for (int p = blockIdx.x * 256 + threadIdx.x; p < n; p += gridDim.x * 256) {
         if (a.root[p] != p) continue;
         int x = p, q = uf_load(a.parent, p);
@@ -241,66 +252,18 @@ __global__ __launch_bounds__(256) void speckle_resolve(PostFullArgs a) {
             q = uf_load(a.parent, x);
         }
         if (x != p) __hip_atomic_store(a.parent + p, x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        atomicAdd(a.count + x, a.lsz[p]);
     }
 }
 
-// Component sizes: root[p] = parent[local root of p] (final after the resolve pass).  Counts are
-// aggregated per wave (ballot over equal roots), then per block in an LDS table of (root, count)
-// slots, and reach global memory as one atomicAdd per (block, root): a large component's pixels
-// all adding into one address serialise at the memory-side atomic unit (C4: 28k same-address
-// wave atomics took 116 us).
-constexpr int kCntSlots = 128;
-__global__ __launch_bounds__(256) void speckle_count(PostFullArgs a) {
-    __shared__ int skey[kCntSlots];
-    __shared__ int scnt[kCntSlots];
-    for (int i = threadIdx.x; i < kCntSlots; i += 256) {
-        skey[i] = -1;
-        scnt[i] = 0;
-    }
-    __syncthreads();
-    const int n = a.H * (a.W - a.crop);  // < 2^31 (host check)
-    const int lane = threadIdx.x & 63;
-    for (int p0 = blockIdx.x * 256 + (threadIdx.x & ~63); p0 < n; p0 += gridDim.x * 256) {
-        const int p = p0 + lane;
-        int r = -1;
-        if (p < n) {
-            const int lr = a.root[p];
-            if (lr >= 0) {
-                r = a.parent[lr];
-                a.root[p] = r;
-            }
-        }
-        uint64_t act = __ballot(r >= 0);
-        while (act) {
-            const int leader = __ffsll((unsigned long long)act) - 1;
-            const int r0 = __shfl(r, leader);
-            const uint64_t m = __ballot(r == r0);
-            if (lane == leader) {
-                const int c = __popcll(m);
-                bool done = false;
-                for (int t = 0, h = (int)(((unsigned)r0 * 2654435761u) >> 25); t < 8; ++t, h = (h + 1) & (kCntSlots - 1)) {
-                    const int k = atomicCAS(&skey[h], -1, r0);
-                    if (k == -1 || k == r0) {
-                        atomicAdd(&scnt[h], c);
-                        done = true;
-                        break;
-                    }
-                }
-                if (!done) atomicAdd(a.count + r0, c);  // table crowded: straight to global
-            }
-            act &= ~m;
-        }
-    }
-    __syncthreads();
-    for (int i = threadIdx.x; i < kCntSlots; i += 256)
-        if (skey[i] >= 0) atomicAdd(a.count + skey[i], scnt[i]);
-}
+// size of pixel p's component (after speckle_resolve); p must be live (v16 != 0)
+__device__ __forceinline__ int comp_size(const PostFullArgs &a, int64_t p) { return a.count[a.parent[a.root[p]]]; }
 
 __global__ __launch_bounds__(256) void speckle_apply(PostFullArgs a) {
     const int64_t n = (int64_t)a.H * (a.W - a.crop);
     for (int64_t p = (int64_t)blockIdx.x * 256 + threadIdx.x; p < n; p += (int64_t)gridDim.x * 256) {
         int v = a.v16[p];
-        if (v != 0 && a.count[a.root[p]] <= a.max_speckle) v = 0;
+        if (v != 0 && comp_size(a, p) <= a.max_speckle) v = 0;
         a.t0[p] = (float)v / 16.0f;
     }
 }
@@ -337,12 +300,103 @@ __global__ __launch_bounds__(256) void outliers(PostFullArgs a) {
     }
 }
 
+// Fused tail (outlier kernel k <= 7): speckle apply -> outliers -> 3x3 median -> depth for one
+// TW x TH output tile.  t0 (the speckle-filtered map) is rebuilt from v16 / root / count over the
+// tile plus a halo of 1 + k/2 (BORDER_REFLECT_101 source rows / columns), the k x k box sums are
+// separable float64 row then column sums (exact, so in any order equal to the host's sums), t1
+// (outliers zeroed) is formed on the tile plus a 1-pixel ring and the median reads it with
+// BORDER_REPLICATE, as post_fast does.  Replaces speckle_apply, outliers and post_fast (three
+// passes over HBM and two intermediate maps).
+constexpr int kTailTX = 32, kTailTY = 8, kTailR = 3;
+constexpr int kT0W = kTailTX + 2 + 2 * kTailR, kT0H = kTailTY + 2 + 2 * kTailR;  // t0 tile
+constexpr int kT1W = kTailTX + 2, kT1H = kTailTY + 2;                            // t1 tile
+
+__global__ __launch_bounds__(kTailTX *kTailTY) void post_tail(PostFullArgs a) {
+    __shared__ float t0[kT0H][kT0W];
+    __shared__ double rs[kT0H][kT1W], rs2[kT0H][kT1W];
+    __shared__ float t1[kT1H][kT1W];
+    const int Wc = a.W - a.crop, H = a.H;
+    const int r = a.kernel / 2;
+    const int x0 = blockIdx.x * kTailTX, y0 = blockIdx.y * kTailTY;
+    const int tid = threadIdx.x;
+    // t0 tile: tile (ty, tx) <-> unreflected image (y0 - 1 - r + ty, x0 - 1 - r + tx)
+    const int th0 = kTailTY + 2 + 2 * r, tw0 = kTailTX + 2 + 2 * r;
+    for (int q = tid; q < th0 * tw0; q += kTailTX * kTailTY) {
+        const int ty = q / tw0, tx = q - ty * tw0;
+        const int yy = reflect101(y0 - 1 - r + ty, H), xx = reflect101(x0 - 1 - r + tx, Wc);
+        const int64_t p = (int64_t)yy * Wc + xx;
+        int v = a.v16[p];
+        if (v != 0 && comp_size(a, p) <= a.max_speckle) v = 0;
+        t0[ty][tx] = (float)v / 16.0f;
+    }
+    __syncthreads();
+    const bool outl = a.apply_outliers != 0;
+    if (outl) {
+        // horizontal k-sums for every t0 row, at the t1 columns
+        for (int q = tid; q < th0 * kT1W; q += kTailTX * kTailTY) {
+            const int ty = q / kT1W, c = q - ty * kT1W;
+            double s = 0.0, s2 = 0.0;
+            for (int i = 0; i <= 2 * r; ++i) {
+                const float v = t0[ty][c + i];
+                s += (double)v;
+                s2 += (double)(v * v);
+            }
+            rs[ty][c] = s;
+            rs2[ty][c] = s2;
+        }
+        __syncthreads();
+    }
+    const double scale = 1.0 / (double)(a.kernel * a.kernel);
+    for (int q = tid; q < kT1H * kT1W; q += kTailTX * kTailTY) {
+        const int ty = q / kT1W, c = q - ty * kT1W;
+        // t1 position (ty, c) <-> image (y0 - 1 + ty, x0 - 1 + c); positions outside the image are
+        // never read (the median clamps its taps)
+        const float d = t0[ty + r][c + r];
+        float v = d;
+        if (outl) {
+            double s = 0.0, s2 = 0.0;
+            for (int j = 0; j <= 2 * r; ++j) {
+                s += rs[ty + j][c];
+                s2 += rs2[ty + j][c];
+            }
+            const float mean = (float)(s * scale), msq = (float)(s2 * scale);
+            const float var = msq - mean * mean;
+            const float sd = sqrtf(var > 0.0f ? var : 0.0f);
+            if (d > 0.0f && fabsf(d - mean) > a.thr * sd) v = 0.0f;
+        }
+        t1[ty][c] = v;
+    }
+    __syncthreads();
+    const int lx = tid % kTailTX, ly = tid / kTailTX;
+    const int x = x0 + lx, y = y0 + ly;
+    if (x >= Wc || y >= H) return;
+    if (a.tail_t1) {  // hole filling follows: hand over the outlier-cleaned map
+        a.t1[(int64_t)y * Wc + x] = t1[ly + 1][lx + 1];
+        return;
+    }
+    auto tap = [&](int dy, int dx) __attribute__((always_inline)) -> float {
+        const int yy = min(max(y + dy, 0), H - 1), xx = min(max(x + dx, 0), Wc - 1);  // BORDER_REPLICATE
+        return t1[yy - (y0 - 1)][xx - (x0 - 1)];
+    };
+    const float med = median9(tap(-1, -1), tap(-1, 0), tap(-1, 1), tap(0, -1), tap(0, 0), tap(0, 1), tap(1, -1),
+                              tap(1, 0), tap(1, 1));
+    const int64_t o = (int64_t)y * Wc + x;
+    if (a.out_disp) a.out_disp[o] = med;
+    if (a.out_depth) {
+        const float adj = med + a.doffs;
+        float z = adj > a.eps ? __fdiv_rn(a.fB, adj) : __builtin_inff();
+        if (a.has_max && z > a.max_depth) z = a.max_depth;
+        a.out_depth[o] = z;
+    }
+}
+
 #pragma clang fp contract(on)
 
 size_t post_full_workspace(int H, int W, int crop) {
     const size_t n = (size_t)H * (size_t)(W > crop ? W - crop : 0);
     const auto r = [](size_t b) { return (b + 255) & ~(size_t)255; };
-    return r(n * 4) * 3 + r(n * 2) + r(n * 4) * 2;  // parent, count, root | v16 | t0, t1
+    // parent, count, root, lsz | v16 | t0, t1 | hole filling
+    return r(n * 4) * 4 + r(n * 2) + r(n * 4) * 2 + inpaint_workspace(H, W > crop ? W - crop : 0);
 }
 
 hipError_t launch_post_full(PostFullArgs a, void *ws, hipStream_t st) {
@@ -353,9 +407,10 @@ hipError_t launch_post_full(PostFullArgs a, void *ws, hipStream_t st) {
     a.parent = reinterpret_cast<int *>(w);
     a.count = reinterpret_cast<int *>(w + r(n * 4));
     a.root = reinterpret_cast<int *>(w + 2 * r(n * 4));
-    a.v16 = reinterpret_cast<int16_t *>(w + 3 * r(n * 4));
-    a.t0 = reinterpret_cast<float *>(w + 3 * r(n * 4) + r(n * 2));
-    a.t1 = reinterpret_cast<float *>(w + 3 * r(n * 4) + r(n * 2) + r(n * 4));
+    a.lsz = reinterpret_cast<int *>(w + 3 * r(n * 4));
+    a.v16 = reinterpret_cast<int16_t *>(w + 4 * r(n * 4));
+    a.t0 = reinterpret_cast<float *>(w + 4 * r(n * 4) + r(n * 2));
+    a.t1 = reinterpret_cast<float *>(w + 4 * r(n * 4) + r(n * 2) + r(n * 4));
     const int grid = (int)std::min<size_t>((n + 255) / 256, 4096);
     const int ntx = (Wc + kCcTX - 1) / kCcTX, nty = (a.H + kCcTY - 1) / kCcTY;
     hipLaunchKernelGGL(speckle_local, dim3(ntx, nty), dim3(256), 0, st, a);
@@ -365,12 +420,30 @@ hipError_t launch_post_full(PostFullArgs a, void *ws, hipStream_t st) {
                            ntx, nty);
     }
     hipLaunchKernelGGL(speckle_resolve, dim3(grid), dim3(256), 0, st, a);
-    hipLaunchKernelGGL(speckle_count, dim3((unsigned)std::min<size_t>((n + 255) / 256, 1024)), dim3(256), 0, st, a);
-    hipLaunchKernelGGL(speckle_apply, dim3(grid), dim3(256), 0, st, a);
+    const bool fill = a.fill_radius > 0;
+    if (a.kernel / 2 <= kTailR) {
+        a.tail_t1 = fill ? 1 : 0;
+        hipLaunchKernelGGL(post_tail, dim3((Wc + kTailTX - 1) / kTailTX, (a.H + kTailTY - 1) / kTailTY), dim3(kTailTX * kTailTY),
+                           0, st, a);
+        hipError_t e = hipGetLastError();
+        if (e != hipSuccess || !fill) return e;
+    }
     const float *med_in = a.t0;
-    if (a.apply_outliers) {
-        hipLaunchKernelGGL(outliers, dim3(grid), dim3(256), 0, st, a);
-        med_in = a.t1;
+    if (a.kernel / 2 > kTailR) {
+        hipLaunchKernelGGL(speckle_apply, dim3(grid), dim3(256), 0, st, a);
+        if (a.apply_outliers) {
+            hipLaunchKernelGGL(outliers, dim3(grid), dim3(256), 0, st, a);
+            med_in = a.t1;
+        }
+    } else {
+        med_in = a.t1;  // post_tail wrote the outlier-cleaned map (fill on)
+    }
+    if (fill) {
+        // fill_holes (postprocess.py:160-166) on the cleaned map: t1 (or t0) -> t0, then the median
+        float *dst = med_in == a.t0 ? a.t1 : a.t0;
+        hipError_t e = launch_inpaint(med_in, Wc, a.H, Wc, a.fill_radius, dst, w + 4 * r(n * 4) + r(n * 2) + 2 * r(n * 4), st);
+        if (e != hipSuccess) return e;
+        med_in = dst;
     }
     PostArgs m{};
     m.disp = med_in;

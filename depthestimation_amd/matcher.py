@@ -295,9 +295,11 @@ def rectify_device(img, mapx=None, mapy=None, out=None, stream=None):
 
 def postprocess_full_device(disp, crop, max_speckle_size=50, max_diff=1.0, apply_outlier_removal=True,
                             outlier_threshold=3.0, outlier_kernel=5, focal_length=None, baseline=None, doffs=0.0,
-                            eps=1e-6, max_depth=None, stream=None):
-    """postprocess_disparity (postprocess.py:120-171, hole filling off) + depth on the device
-    (dsx_postprocess_full_device).  ``disp``: float32 H x W HIP tensor.
+                            eps=1e-6, max_depth=None, stream=None, apply_hole_filling=False, fill_kernel=3):
+    """postprocess_disparity (postprocess.py:120-171) + depth on the device
+    (dsx_postprocess_full_ex_device): speckles -> outliers -> hole filling
+    (Telea 'inpaint' with radius ``fill_kernel`` when ``apply_hole_filling``; synchronises the
+    stream then) -> 3x3 median -> depth.  ``disp``: float32 H x W HIP tensor.
     Returns (disp_cropped, depth or None) as HIP tensors."""
     import torch
 
@@ -314,11 +316,38 @@ def postprocess_full_device(disp, crop, max_speckle_size=50, max_diff=1.0, apply
     nbytes = L.dsx_postprocess_workspace_bytes(H, W, int(crop))
     ws = torch.empty(nbytes, dtype=torch.uint8, device=disp.device)
     sptr = None if stream is None else (stream if isinstance(stream, int) else stream.cuda_stream)
-    rc = L.dsx_postprocess_full_device(
+    rc = L.dsx_postprocess_full_ex_device(
         disp.data_ptr(), H, W, disp.stride(0), int(crop), int(max_speckle_size), float(max_diff),
-        int(bool(apply_outlier_removal)), float(outlier_threshold), int(outlier_kernel), out_disp.data_ptr(),
+        int(bool(apply_outlier_removal)), float(outlier_threshold), int(outlier_kernel),
+        int(fill_kernel) if apply_hole_filling else 0, out_disp.data_ptr(),
         out_depth.data_ptr() if want_depth else None, float(focal_length or 0.0), float(baseline or 0.0),
         float(doffs or 0.0), float(eps), float(max_depth or 0.0), int(max_depth is not None), ws.data_ptr(),
         nbytes, sptr)
-    _dsx.check(rc, "dsx_postprocess_full_device")
+    _dsx.check(rc, "dsx_postprocess_full_ex_device")
     return out_disp, out_depth
+
+
+def fill_holes_device(disp, radius=5, out=None, stream=None):
+    """fill_holes(disparity, method='inpaint', kernel_size=radius) on the device
+    (postprocess.py:72-118; dsx_fill_holes_device): Telea inpainting of the pixels <= 0, equal to
+    the host restatement (postprocess._telea_inpaint).  ``disp``: float32 H x W HIP tensor (unit
+    column stride).  Synchronises ``stream``; returns the filled float32 H x W tensor."""
+    import torch
+
+    if disp.dtype != torch.float32 or disp.dim() != 2 or disp.stride(1) != 1 or not disp.is_cuda:
+        raise ValueError("disp must be a float32 H x W device tensor with unit column stride")
+    H, W = disp.shape
+    if out is None:
+        out = torch.empty((H, W), dtype=torch.float32, device=disp.device)
+    elif out.shape != (H, W) or out.dtype != torch.float32 or not out.is_contiguous() or out.device != disp.device:
+        raise ValueError("out must be a contiguous float32 H x W tensor on the input's device")
+    if H == 0 or W == 0:
+        return out
+    L = _dsx.lib()
+    nbytes = L.dsx_fill_holes_workspace_bytes(H, W)
+    ws = torch.empty(nbytes, dtype=torch.uint8, device=disp.device)
+    sptr = None if stream is None else (stream if isinstance(stream, int) else stream.cuda_stream)
+    rc = L.dsx_fill_holes_device(disp.data_ptr(), H, W, disp.stride(0), int(radius), out.data_ptr(), ws.data_ptr(),
+                                 nbytes, sptr)
+    _dsx.check(rc, "dsx_fill_holes_device")
+    return out

@@ -11,8 +11,9 @@ each function restates the documented OpenCV semantics with numpy/scipy:
                           a region.
 * ``detect_outliers``   - normalised k x k box mean / mean of squares with BORDER_REFLECT_101
                           (cv2.boxFilter default): exact float64 window sums x 1/k^2 -> float32.
-* ``fill_holes``        - 'inpaint': Telea fast-marching inpainting; 'nearest': iterated
-                          elliptical dilation (postprocess.py:106-116).
+* ``fill_holes``        - 'inpaint': Telea fast-marching inpainting, marched in 4-connected
+                          distance layers (see _telea_inpaint); 'nearest': iterated elliptical
+                          dilation (postprocess.py:106-116).
 * ``median_blur3``      - 3 x 3 median with BORDER_REPLICATE (cv2.medianBlur, ksize 3).
 
 Parity against OpenCV is unpinned (cv2 absent); the reference's own behavioural test
@@ -21,8 +22,6 @@ one) is re-run in tests/test_host_api.py. These run on the host: SURVEY.md secti
 (GPU post-processing) is the next step for them.
 """
 from __future__ import annotations
-
-import heapq
 
 import numpy as np
 from scipy import ndimage
@@ -84,87 +83,93 @@ def detect_outliers(disparity, threshold=3.0, kernel_size=5):
     return (np.abs(d - mean) > np.float32(threshold) * std) & valid
 
 
-def _telea_inpaint(img: np.ndarray, hole: np.ndarray, radius: int) -> np.ndarray:
-    """Telea (2004) fast-marching inpainting of float32 ``img`` where ``hole`` is True."""
-    H, W = img.shape
-    out = img.astype(np.float32).copy()
-    KNOWN, BAND, INSIDE = 0, 1, 2
-    flag = np.where(hole, INSIDE, KNOWN).astype(np.int8)
-    T = np.where(hole, 1e6, 0.0)
-    heap = []
-    # initial band: known pixels 4-adjacent to the hole
-    near = ndimage.binary_dilation(hole, structure=ndimage.generate_binary_structure(2, 1)) & ~hole
-    for y, x in zip(*np.nonzero(near)):
-        flag[y, x] = BAND
-        heapq.heappush(heap, (0.0, int(y), int(x)))
-    offs = [(dy, dx) for dy in range(-radius, radius + 1) for dx in range(-radius, radius + 1)
+def _telea_offsets(radius: int):
+    """Offsets (dy, dx) of the inpainting neighbourhood, 0 < dy^2 + dx^2 <= radius^2, row-major -
+    the summation order the device kernel uses too."""
+    return [(dy, dx) for dy in range(-radius, radius + 1) for dx in range(-radius, radius + 1)
             if 0 < dy * dy + dx * dx <= radius * radius]
 
-    def solve(y1, x1, y2, x2):
-        t1 = T[y1, x1] if 0 <= y1 < H and 0 <= x1 < W and flag[y1, x1] == KNOWN else 1e6
-        t2 = T[y2, x2] if 0 <= y2 < H and 0 <= x2 < W and flag[y2, x2] == KNOWN else 1e6
-        if t1 < 1e6 and t2 < 1e6:
-            r = 2.0 - (t1 - t2) ** 2
-            if r > 0:
-                s = (t1 + t2 + np.sqrt(r)) / 2.0
-                if s >= t1 and s >= t2:
-                    return s
-            return 1.0 + min(t1, t2)
-        return 1.0 + min(t1, t2)
 
-    def grad_t(y, x):
-        def tv(yy, xx):
-            if 0 <= yy < H and 0 <= xx < W and flag[yy, xx] != INSIDE:
-                return T[yy, xx]
-            return None
-        c = T[y, x]
-        gx = gy = 0.0
-        a, b = tv(y, x + 1), tv(y, x - 1)
-        if a is not None and b is not None:
-            gx = (a - b) * 0.5
-        elif a is not None:
-            gx = a - c
-        elif b is not None:
-            gx = c - b
-        a, b = tv(y + 1, x), tv(y - 1, x)
-        if a is not None and b is not None:
-            gy = (a - b) * 0.5
-        elif a is not None:
-            gy = a - c
-        elif b is not None:
-            gy = c - b
-        return gy, gx
+def _telea_solve(t1, t2):
+    """Telea's upwind eikonal update from two neighbour arrival times (1e6 = not available)."""
+    both = (t1 < 1e6) & (t2 < 1e6)
+    d = t1 - t2
+    r = 2.0 - d * d
+    s = (t1 + t2 + np.sqrt(np.maximum(r, 0.0))) / 2.0
+    ok = both & (r > 0) & (s >= t1) & (s >= t2)
+    return np.where(ok, s, 1.0 + np.minimum(t1, t2))
 
-    while heap:
-        _, y, x = heapq.heappop(heap)
-        if flag[y, x] == KNOWN:
-            continue
-        flag[y, x] = KNOWN
-        for dy, dx in ((-1, 0), (1, 0), (0, -1), (0, 1)):
-            ny, nx = y + dy, x + dx
-            if not (0 <= ny < H and 0 <= nx < W) or flag[ny, nx] != INSIDE:
-                continue
-            T[ny, nx] = min(solve(ny - 1, nx, ny, nx - 1), solve(ny + 1, nx, ny, nx - 1),
-                            solve(ny - 1, nx, ny, nx + 1), solve(ny + 1, nx, ny, nx + 1))
-            # inpaint (ny, nx) from the known pixels within `radius`
-            gy, gx = grad_t(ny, nx)
-            num = den = 0.0
-            for oy, ox in offs:
-                qy, qx = ny + oy, nx + ox
-                if not (0 <= qy < H and 0 <= qx < W) or flag[qy, qx] == INSIDE:
-                    continue
-                ry, rx = -oy, -ox  # p - q
-                d2 = ry * ry + rx * rx
-                w_dir = abs(ry * gy + rx * gx) / np.sqrt(d2)
-                w_dst = 1.0 / d2
-                w_lev = 1.0 / (1.0 + abs(T[qy, qx] - T[ny, nx]))
-                w = max(w_dir * w_dst * w_lev, 1e-6)
-                num += w * out[qy, qx]
-                den += w
-            if den > 0:
-                out[ny, nx] = num / den
-            flag[ny, nx] = BAND
-            heapq.heappush(heap, (T[ny, nx], ny, nx))
+
+def _telea_inpaint(img: np.ndarray, hole: np.ndarray, radius: int) -> np.ndarray:
+    """Telea (2004) fast-marching inpainting of float32 ``img`` where ``hole`` is True, marched in
+    4-connected distance layers (the form the GPU runs, csrc/dsx_inpaint.hip).
+
+    cv2.inpaint(INPAINT_TELEA) (postprocess.py:104) pops the narrow band from a heap ordered by
+    the arrival time T.  Here every hole pixel next to the previous layer forms the next layer and
+    the whole layer is filled at once from pixels of earlier layers only:
+      * T(p) = min over the 4 quadrants of solve(T_vertical, T_horizontal), neighbours of earlier
+        layers only (solve: Telea's first-order upwind update, float64);
+      * grad T at p from central / one-sided differences of earlier-layer neighbours' T;
+      * value(p) = sum w(q) v(q) / sum w(q) over earlier-layer q with 0 < |p - q|^2 <= radius^2,
+        w = max(|(p - q) . grad T| / |p - q| * 1 / |p - q|^2 * 1 / (1 + |T(q) - T(p)|), 1e-6)
+        (direction, distance and level-set factors), summed in float64 in offset order, rounded
+        to float32 once.
+    Hole pixels no layer reaches (no known pixel in their region) keep their value.  Parity with
+    OpenCV's heap order is unpinned (cv2 absent); the device kernel equals this bit for bit."""
+    H, W = img.shape
+    out = np.asarray(img, np.float32).copy()
+    hole = np.asarray(hole, bool)
+    INF = np.iinfo(np.int32).max
+    layer = np.where(hole, INF, 0).astype(np.int64)
+    T = np.where(hole, 1e6, 0.0)
+    offs = _telea_offsets(radius)
+    k = 0
+    while True:
+        k += 1
+        prev = layer == k - 1
+        nb = np.zeros_like(prev)
+        nb[1:, :] |= prev[:-1, :]
+        nb[:-1, :] |= prev[1:, :]
+        nb[:, 1:] |= prev[:, :-1]
+        nb[:, :-1] |= prev[:, 1:]
+        front = (layer == INF) & nb
+        if not front.any():
+            break
+        ys, xs = np.nonzero(front)
+
+        def tv(dy, dx):
+            yy, xx = ys + dy, xs + dx
+            inb = (yy >= 0) & (yy < H) & (xx >= 0) & (xx < W)
+            yc, xc = np.clip(yy, 0, H - 1), np.clip(xx, 0, W - 1)
+            ok = inb & (layer[yc, xc] < k)
+            return ok, np.where(ok, T[yc, xc], 1e6)
+
+        (ou, tu), (od, td), (ol, tl), (orr, tr) = tv(-1, 0), tv(1, 0), tv(0, -1), tv(0, 1)
+        tp = np.minimum(np.minimum(_telea_solve(tu, tl), _telea_solve(td, tl)),
+                        np.minimum(_telea_solve(tu, tr), _telea_solve(td, tr)))
+        gx = np.where(orr & ol, (tr - tl) * 0.5, np.where(orr, tr - tp, np.where(ol, tp - tl, 0.0)))
+        gy = np.where(od & ou, (td - tu) * 0.5, np.where(od, td - tp, np.where(ou, tp - tu, 0.0)))
+        num = np.zeros(ys.size)
+        den = np.zeros(ys.size)
+        for oy, ox in offs:
+            yy, xx = ys + oy, xs + ox
+            inb = (yy >= 0) & (yy < H) & (xx >= 0) & (xx < W)
+            yc, xc = np.clip(yy, 0, H - 1), np.clip(xx, 0, W - 1)
+            ok = inb & (layer[yc, xc] < k)
+            ry, rx = -oy, -ox
+            d2 = ry * ry + rx * rx
+            w_dir = np.abs(ry * gy + rx * gx) / np.sqrt(float(d2))
+            w_dst = 1.0 / d2
+            w_lev = 1.0 / (1.0 + np.abs(T[yc, xc] - tp))
+            w = np.maximum(w_dir * w_dst * w_lev, 1e-6)
+            num = np.where(ok, num + w * out[yc, xc].astype(np.float64), num)
+            den = np.where(ok, den + w, den)
+        fill = den > 0
+        vals = out[ys, xs]
+        vals[fill] = (num[fill] / den[fill]).astype(np.float32)
+        out[ys, xs] = vals
+        T[ys, xs] = tp
+        layer[ys, xs] = k
     return out
 
 

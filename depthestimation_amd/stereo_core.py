@@ -220,33 +220,21 @@ class StereoCore:
     def process_pair_device(self, left, right, stream=None):
         """Device-resident ``_process_pair`` (stereo_core.py:162-200) for rectified uint8 HIP
         tensors: matcher -> crop -> post-processing -> depth, all in HBM.  Fast mode: 3x3 median
-        (SURVEY.md 8f row F1); otherwise speckle filter + outlier removal + median (row F2).
-        Hole filling (Telea inpainting, off by default) has no device kernel: with
-        ``hole_filling`` set, that path post-processes on the host.  Returns float32 HIP tensors
+        (SURVEY.md 8f row F1); otherwise speckle filter + outlier removal (+ Telea hole filling
+        with ``hole_filling``) + median (row F2).  Returns float32 HIP tensors
         (disparity_px, depth_m or None)."""
-        import torch
         disp = self.compute_disparity_device(left, right, stream=stream)
         p = self.sgbm_params
         f, B = p.get('focal_length'), p.get('baseline')
         doffs, eps, max_depth = p.get('doffs', 0.0), p.get('min_disp', 5.0), p.get('max_depth')
         if self.fast_mode:
             return postprocess_fast_device(disp, p['num_disp'], f, B, doffs, eps, max_depth, stream=stream)
-        if not p.get('hole_filling', False):
-            return postprocess_full_device(disp, p['num_disp'], max_speckle_size=int(100 * self.downscale_factor),
-                                           max_diff=1.0, apply_outlier_removal=True, outlier_threshold=2.5,
-                                           outlier_kernel=5, focal_length=f, baseline=B, doffs=doffs, eps=eps,
-                                           max_depth=max_depth, stream=stream)
-        if stream is not None:
-            stream.synchronize()
-        else:
-            torch.cuda.synchronize(disp.device)
-        d = postprocess_disparity(disp.cpu().numpy()[:, p['num_disp']:], max_speckle_size=int(100 * self.downscale_factor),
-                                  max_diff=1.0, outlier_threshold=2.5, fill_method='inpaint',
-                                  apply_outlier_removal=True, apply_hole_filling=True)
-        depth = None
-        if f is not None and B is not None:
-            depth = torch.from_numpy(self.disparity_to_depth(d, f, B, doffs, eps=eps, max_depth=max_depth)).to(disp.device)
-        return torch.from_numpy(d).to(disp.device), depth
+        # fill_kernel 3: postprocess_disparity's default as _process_pair calls it (postprocess.py:165)
+        return postprocess_full_device(disp, p['num_disp'], max_speckle_size=int(100 * self.downscale_factor),
+                                       max_diff=1.0, apply_outlier_removal=True, outlier_threshold=2.5,
+                                       outlier_kernel=5, focal_length=f, baseline=B, doffs=doffs, eps=eps,
+                                       max_depth=max_depth, stream=stream,
+                                       apply_hole_filling=bool(p.get('hole_filling', False)), fill_kernel=3)
 
     def disparity_to_depth(self, disp: np.ndarray, f_pixels: float, baseline_m: float, doffs: float = 0.0,
                            eps: float = 1e-6, max_depth: Optional[float] = None) -> np.ndarray:
@@ -264,7 +252,7 @@ class StereoCore:
         """stereo_core.py:274-293.  Host arrays in, host arrays out; the work runs on the
         device pipeline (``estimate_depth_device``: rectify / gray, matcher, post-processing,
         depth, all in HBM - bit-identical to the host steps, tests/test_gpu_host_api.py) unless
-        hole filling (Telea inpainting, host only) is on or the matcher was replaced."""
+        the matcher was replaced."""
         if left_source is None or right_source is None:
             raise ValueError("Left and right sources must be set before estimating depth.")
         if self._device_pipeline_ok(left_source, right_source):
@@ -282,7 +270,7 @@ class StereoCore:
         return self._process_pair(self.left_rectified, self.right_rectified)
 
     def _device_pipeline_ok(self, left, right) -> bool:
-        if self.sgbm_params.get('hole_filling', False) or 'compute_disparity' in self.__dict__:
+        if 'compute_disparity' in self.__dict__:
             return False
         if not (isinstance(left, np.ndarray) and isinstance(right, np.ndarray)):
             return False
