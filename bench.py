@@ -346,32 +346,48 @@ def main():
                   "compared": "int16 x16 map of each rank's frame 0 from the timed matcher, bit for bit",
                   "oracle": "oracle/bm_ref.c (C restatement of the A5' contract; tests/test_oracle.py pins it)"}
 
-    # secondary, never `value`: host numpy frames -> pinned -> H2D -> matcher -> D2H of the int16 map,
-    # two worker streams per GPU (multigpu.MultiDeviceStereo), every rank on its own GPU and the
-    # whole-job rate over the slowest rank (SURVEY 8e / BASELINE.md: end-to-end scaling next to
-    # the device-resident `value`)
+    # secondary, never `value`: host frames -> H2D -> matcher -> D2H of the int16 map on every rank's
+    # GPU (multigpu.HostPipeline: 3 frames in flight over 2 streams, no per-frame host sync), whole-job
+    # rate over the slowest rank (SURVEY 8e / BASELINE.md: end-to-end next to the device-resident
+    # `value`).  Two sources: pinned frame buffers (a decoder writing into a pinned ring) and
+    # pageable numpy arrays (one host copy into the pinned slot per frame).
     e2e = None
     if not args.no_e2e and args.path == "fused" and not args.sgm:
-        from depthestimation_amd.multigpu import MultiDeviceStereo
-        run = MultiDeviceStereo(devices=[local], streams_per_device=2, **kw)
-        ne = 64
-        src = [(hostL[i % nres], hostR[i % nres]) for i in range(ne)]
-        for _ in run.map(iter(src[:4])):
-            pass
-        if ws > 1:
-            dist.barrier()
-        t1 = time.perf_counter()
-        n_done = sum(1 for _ in run.map(iter(src)))
-        et = time.perf_counter() - t1
-        if ws > 1:
-            t = torch.tensor([et], dtype=torch.float64, device=dev)
-            dist.all_reduce(t, op=dist.ReduceOp.MAX)
-            et = float(t.item())
-        pcie_floor_ms = H * W * (2 + 2) / 50e9 * 1e3  # 2 B/px in + 2 B/px out over ~50 GB/s (PCIe5 x16)
-        e2e = {"value": round(H * W * n_done * ws / et / 1e6, 1), "unit": "Mpix/s", "frames_per_gpu": n_done,
-               "ms_per_frame_per_gpu": round(et / n_done * 1e3, 4), "pcie_floor_ms_per_frame": round(pcie_floor_ms, 4),
-               "note": "secondary, PCIe-inclusive: host uint8 pairs in, int16 x16 out, 2 worker streams per GPU "
-                       "(multigpu.MultiDeviceStereo), all ranks, max time over ranks"}
+        from depthestimation_amd.multigpu import HostPipeline
+        pipe = HostPipeline(local, depth=3, streams=2, copy=False, **kw)
+        pinned = []
+        for i in range(nres):
+            t = torch.empty((2, H, W), dtype=torch.uint8, pin_memory=True)
+            t[0].numpy()[...] = hostL[i]
+            t[1].numpy()[...] = hostR[i]
+            pinned.append(t)
+        ne = 256
+        rates = {}
+        for name, src in (("pinned", [pinned[i % nres] for i in range(ne)]),
+                          ("pageable", [(hostL[i % nres], hostR[i % nres]) for i in range(ne)])):
+            for _ in pipe.run(iter(src[:16])):
+                pass
+            if ws > 1:
+                dist.barrier()
+            t1 = time.perf_counter()
+            n_done = sum(1 for _ in pipe.run(iter(src)))
+            et = time.perf_counter() - t1
+            if ws > 1:
+                t = torch.tensor([et], dtype=torch.float64, device=dev)
+                dist.all_reduce(t, op=dist.ReduceOp.MAX)
+                et = float(t.item())
+            rates[name] = (round(H * W * n_done * ws / et / 1e6, 1), round(et / n_done * 1e3, 4))
+        pipe.close()
+        # 2 B/px up (L + R) and 2 B/px down (int16) at ~50 GB/s per direction (PCIe 5 x16), the two
+        # directions overlapping: the floor is the larger of the two transfers
+        pcie_floor_ms = H * W * 2 / 50e9 * 1e3
+        e2e = {"value": rates["pinned"][0], "unit": "Mpix/s", "frames_per_gpu": ne,
+               "ms_per_frame_per_gpu": rates["pinned"][1], "pcie_floor_ms_per_frame": round(pcie_floor_ms, 4),
+               "pcie_floor_serial_ms_per_frame": round(2 * pcie_floor_ms, 4),
+               "pageable_source": {"value": rates["pageable"][0], "ms_per_frame_per_gpu": rates["pageable"][1]},
+               "note": "secondary, PCIe-inclusive: host uint8 pairs in (pinned frame ring; pageable_source: numpy "
+                       "arrays copied into the pinned slot), int16 x16 out in pinned memory, 3 frames in flight over "
+                       "2 streams (multigpu.HostPipeline), all ranks, max time over ranks"}
 
     # secondary: the C2 shape with the reference's own uniqueness 10 / disp12MaxDiff 1 defaults
     # (stereo_core.py:20,22), which add the LR pass (side 3 + lr_fixup)

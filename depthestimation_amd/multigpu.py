@@ -7,10 +7,10 @@ describes: ONE process drives N GPUs from threads, the generalisation of
 
 * ``DeviceComm``: one RCCL communicator per device (``dsx_comm_init_all``) and the one exchange
   the path has - the calibration block broadcast from the root GPU (``dsx_bcast``).
-* ``MultiDeviceStereo``: worker threads, two per device, each with its own matcher handle and
-  HIP stream.  Frame i goes to worker i mod (2N), i.e. device i mod N, through a bounded queue;
-  a worker stages the pair into pinned host memory, copies it up, runs the matcher and copies
-  the result back on its stream, so one worker's copies overlap the other's kernels.  Results come back in frame order, as the
+* ``HostPipeline``: one GPU's PCIe-inclusive path - a ring of pinned / device slots over two HIP
+  streams, several frames in flight, no per-frame host synchronisation.
+* ``MultiDeviceStereo``: one worker thread per device, each running a ``HostPipeline``.  Frame i
+  goes to device i mod N through a bounded queue; results come back in frame order, as the
   reference's generator yields them (StereoDepthEstimatorVideo.py:103).  ctypes drops the GIL
   inside every C-ABI call, so the devices run concurrently.
 
@@ -87,11 +87,13 @@ _STOP = object()
 
 
 def sharded_map(frames: Iterable, slots: Sequence[int], make_fn: Callable[[int], Callable],
-                queue_depth: int = 4) -> Iterator:
+                queue_depth: int = 4, pipelined: bool = False) -> Iterator:
     """Item i -> worker i mod len(slots) (worker w lives on device slots[w] and calls
     ``make_fn(slots[w])`` once, in its own thread); results are yielded in item order.  A worker
     error stops the producer and is re-raised in the consumer.  Pure host threading - the
-    devices only appear through ``make_fn``."""
+    devices only appear through ``make_fn``.  ``pipelined``: ``make_fn`` returns a stage with
+    ``push(i, item) -> [(j, result), ...]`` and ``drain_all() -> [(j, result), ...]`` (several
+    items in flight per worker, e.g. ``HostPipeline``) instead of a function."""
     N = len(slots)
     inq = [queue.Queue(maxsize=max(1, int(queue_depth))) for _ in range(N)]
     results: Dict[int, object] = {}
@@ -99,18 +101,27 @@ def sharded_map(frames: Iterable, slots: Sequence[int], make_fn: Callable[[int],
     cv = threading.Condition()
     stop = threading.Event()
 
+    def publish(done):
+        if done:
+            with cv:
+                for j, r in done:
+                    results[j] = r
+                cv.notify_all()
+
     def worker(slot: int, dev: int):
         try:
             fn = make_fn(dev)
             while True:
                 item = inq[slot].get()
                 if item is _STOP:
+                    if pipelined:
+                        publish(fn.drain_all())
                     return
                 i, payload = item
-                r = fn(payload)
-                with cv:
-                    results[i] = r
-                    cv.notify_all()
+                if pipelined:
+                    publish(fn.push(i, payload))
+                else:
+                    publish([(i, fn(payload))])
         except BaseException as e:  # surfaced in the consumer
             with cv:
                 errors.append(e)
@@ -181,13 +192,116 @@ def sharded_map(frames: Iterable, slots: Sequence[int], make_fn: Callable[[int],
             t.join(timeout=5.0)
 
 
+class HostPipeline:
+    """Host frame pairs -> HBM -> matcher -> host int16 x16 maps on one GPU, ``depth`` frames in
+    flight over ``streams`` HIP streams (the PCIe-inclusive path of SURVEY.md 8e).
+
+    Frame i uses ring slot i mod depth and stream i mod streams: its H2D copy overlaps the previous
+    frame's kernel and D2H copy, and no per-frame host synchronisation happens - ``push`` only
+    waits on the event of the frame that last used the slot, i.e. ``depth`` frames back.  A pair is
+    either two uint8 H x W numpy arrays (copied into the slot's pinned buffer) or a pinned uint8
+    (2, H, W) torch tensor (copied to the device straight from it, as a decoder writing into pinned
+    buffers would hand frames over).  Results are int16 x16 maps (the cv2 StereoMatcher.compute
+    contract, stereo_core.py:231) in pinned host memory: ``copy=False`` returns views that stay
+    valid until ``depth`` further frames are pushed."""
+
+    def __init__(self, device: int, depth: int = 3, streams: int = 2, copy: bool = True, **matcher_kw):
+        import torch
+        self.torch = torch
+        self.dev = torch.device("cuda", int(device))
+        torch.cuda.set_device(self.dev)
+        self.depth = max(2, int(depth))
+        self.copy = bool(copy)
+        kw = dict(matcher_kw)
+        kw.pop("device", None)
+        self.m = HipBlockMatcher(device=int(device), **kw)
+        self.streams = [torch.cuda.Stream(device=self.dev) for _ in range(max(1, int(streams)))]
+        self.shape = None
+        self.pending: List[Optional[Tuple[int, object]]] = [None] * self.depth  # slot -> (frame index, event)
+
+    def _alloc(self, H: int, W: int) -> None:
+        torch = self.torch
+        self.shape = (H, W)
+        d = self.depth
+        self.hin = [torch.empty((2, H, W), dtype=torch.uint8, pin_memory=True) for _ in range(d)]
+        self.din = [torch.empty((2, H, W), dtype=torch.uint8, device=self.dev) for _ in range(d)]
+        self.dfx = [torch.empty((H, W), dtype=torch.int16, device=self.dev) for _ in range(d)]
+        # output ring twice as deep as the slots: frame j's map lives in hfx[j % 2d], so a view
+        # handed out when frame j + d is pushed stays intact for d more pushes
+        self.hfx = [torch.empty((H, W), dtype=torch.int16, pin_memory=True) for _ in range(2 * d)]
+
+    def _finish(self, slot: int) -> Tuple[int, np.ndarray]:
+        i, ev = self.pending[slot]
+        ev.synchronize()
+        self.pending[slot] = None
+        out = self.hfx[i % (2 * self.depth)].numpy()
+        return i, (out.copy() if self.copy else out)
+
+    def push(self, i: int, pair) -> List[Tuple[int, np.ndarray]]:
+        """Enqueue frame ``i``; returns the frames this completed (at most one), oldest first."""
+        torch = self.torch
+        if isinstance(pair, torch.Tensor):
+            if pair.dtype != torch.uint8 or pair.dim() != 3 or pair.shape[0] != 2 or pair.is_cuda:
+                raise ValueError("a tensor pair must be a host uint8 (2, H, W) tensor")
+            H, W = pair.shape[1], pair.shape[2]
+        else:
+            L, R = pair
+            L = np.asarray(L)
+            R = np.asarray(R)
+            if L.dtype != np.uint8 or R.dtype != np.uint8 or L.ndim != 2 or L.shape != R.shape:
+                raise ValueError("left and right must be uint8 H x W arrays of the same size")
+            H, W = L.shape
+        done = []
+        if self.shape != (H, W):
+            done = self.drain_all()
+            self._alloc(H, W)
+        slot = i % self.depth
+        if self.pending[slot] is not None:
+            done.append(self._finish(slot))
+        if isinstance(pair, torch.Tensor):
+            src = pair if pair.is_pinned() else self.hin[slot].copy_(pair)
+        else:
+            hv = self.hin[slot].numpy()
+            np.copyto(hv[0], L)
+            np.copyto(hv[1], R)
+            src = self.hin[slot]
+        st = self.streams[i % len(self.streams)]
+        with torch.cuda.stream(st):
+            self.din[slot].copy_(src, non_blocking=True)
+            self.m.compute_device(self.din[slot][0], self.din[slot][1], out_fixed=self.dfx[slot], stream=st)
+            self.hfx[i % (2 * self.depth)].copy_(self.dfx[slot], non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record(st)
+        self.pending[slot] = (i, ev)
+        return done
+
+    def drain_all(self) -> List[Tuple[int, np.ndarray]]:
+        """Wait for every frame in flight; returns them oldest first."""
+        live = sorted((p[0], s) for s, p in enumerate(self.pending) if p is not None)
+        return [self._finish(s) for _, s in live]
+
+    def run(self, frames: Iterable) -> Iterator[np.ndarray]:
+        """Frames in, int16 x16 maps out, in order."""
+        for i, pair in enumerate(frames):
+            for _, r in self.push(i, pair):
+                yield r
+        for _, r in self.drain_all():
+            yield r
+
+    def close(self) -> None:
+        self.drain_all()
+        self.m.close()
+
+
 class MultiDeviceStereo:
     """Frame-sharded matcher over several GPUs of one process (see module docstring).
 
-    ``map(frames)`` yields ``(fixed, float)`` per frame pair in order: int16 x16 disparity
-    (the cv2 StereoMatcher.compute contract, stereo_core.py:231) and its float32 /16 view.
-    ``map_fn(frames, make_fn)`` runs an arbitrary per-device function instead (e.g. a whole
-    ``StereoCore.estimate_depth`` on that device) with the same ordering and sharding.
+    ``map(frames)`` yields the int16 x16 disparity (the cv2 StereoMatcher.compute contract,
+    stereo_core.py:231) of every frame pair in order: frame i on device i mod N, each device fed
+    by one worker thread running a ``HostPipeline`` (frames in flight, no per-frame
+    synchronisation).  ``map_fn(frames, make_fn)`` runs an arbitrary per-device function instead
+    (e.g. a whole ``StereoCore.estimate_depth`` on that device) with the same ordering; there
+    ``streams_per_device`` workers share each device.
     """
 
     def __init__(self, devices: Optional[Sequence[int]] = None, queue_depth: int = 4, streams_per_device: int = 2,
@@ -199,10 +313,9 @@ class MultiDeviceStereo:
         if not self.devices:
             raise ValueError("devices must not be empty")
         self.queue_depth = max(1, int(queue_depth))
-        # workers: streams_per_device per GPU (one handle + stream each), so one worker's
-        # copies overlap another's kernels on the same GPU; frame i -> worker i mod len(slots)
-        spd = max(1, int(streams_per_device))
-        self.slots = [self.devices[k % len(self.devices)] for k in range(len(self.devices) * spd)]
+        self.streams_per_device = max(1, int(streams_per_device))
+        # map_fn workers: streams_per_device per GPU, frame i -> worker i mod len(slots)
+        self.slots = [self.devices[k % len(self.devices)] for k in range(len(self.devices) * self.streams_per_device)]
         self.matcher_kw = dict(matcher_kw)
         self.matcher_kw.pop("device", None)
 
@@ -213,41 +326,10 @@ class MultiDeviceStereo:
         return sharded_map(frames, self.slots, make_fn, self.queue_depth)
 
     # -- the matcher over host frames (PCIe-inclusive) ----------------------------------------
-    def _make_matcher_fn(self, dev: int):
-        import torch
-        torch.cuda.set_device(dev)
-        m = HipBlockMatcher(device=dev, **self.matcher_kw)
-        stream = torch.cuda.Stream(device=dev)
-        state = {}
-
-        def fn(pair: Tuple[np.ndarray, np.ndarray]):
-            L, R = pair
-            L = np.ascontiguousarray(L, np.uint8)
-            R = np.ascontiguousarray(R, np.uint8)
-            if L.shape != R.shape or L.ndim != 2:
-                raise ValueError("left and right must be uint8 H x W arrays of the same size")
-            H, W = L.shape
-            if state.get("shape") != (H, W):
-                state["shape"] = (H, W)
-                state["hin"] = torch.empty((2, H, W), dtype=torch.uint8, pin_memory=True)
-                state["din"] = torch.empty((2, H, W), dtype=torch.uint8, device=dev)
-                state["dfx"] = torch.empty((H, W), dtype=torch.int16, device=dev)
-                state["hfx"] = torch.empty((H, W), dtype=torch.int16, pin_memory=True)
-            hin, din, dfx, hfx = state["hin"], state["din"], state["dfx"], state["hfx"]
-            hin[0].numpy()[...] = L
-            hin[1].numpy()[...] = R
-            with torch.cuda.stream(stream):
-                din.copy_(hin, non_blocking=True)
-                m.compute_device(din[0], din[1], out_fixed=dfx, stream=stream)
-                hfx.copy_(dfx, non_blocking=True)
-            stream.synchronize()
-            fixed = hfx.numpy().copy()
-            return fixed, fixed.astype(np.float32) / 16.0
-
-        return fn
-
-    def map(self, frames: Iterable[Tuple[np.ndarray, np.ndarray]]) -> Iterator[Tuple[np.ndarray, np.ndarray]]:
-        return self.map_fn(frames, self._make_matcher_fn)
+    def map(self, frames: Iterable[Tuple[np.ndarray, np.ndarray]]) -> Iterator[np.ndarray]:
+        return sharded_map(frames, self.devices, lambda dev: HostPipeline(
+            dev, depth=3, streams=self.streams_per_device, copy=True, **self.matcher_kw), self.queue_depth,
+            pipelined=True)
 
 
 class BandedStereo:

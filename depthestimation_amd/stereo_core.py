@@ -33,8 +33,42 @@ from .rectify import RectificationCache, rectify_images, to_grayscale_bgr
 _SGBM_MODES = ("sgbm", "hh", "sgbm_3way", "hh4")
 
 
+class _HostView:
+    """A device tensor handed out as a numpy array on first read (estimate_depth's stored
+    rectified images: copied back over PCIe only if the caller looks at them)."""
+
+    __slots__ = ("t",)
+
+    def __init__(self, t):
+        self.t = t
+
+
 class StereoCore:
     """Handles common stereo operations (stereo_core.py:7)."""
+
+    # left_rectified / right_rectified (stereo_core.py:289-291): plain attributes, except that
+    # estimate_depth's device pipeline stores them as lazy host views
+    @property
+    def left_rectified(self):
+        v = self.__dict__.get("_left_rect")
+        if isinstance(v, _HostView):
+            v = self.__dict__["_left_rect"] = v.t.cpu().numpy()
+        return v
+
+    @left_rectified.setter
+    def left_rectified(self, v):
+        self.__dict__["_left_rect"] = v
+
+    @property
+    def right_rectified(self):
+        v = self.__dict__.get("_right_rect")
+        if isinstance(v, _HostView):
+            v = self.__dict__["_right_rect"] = v.t.cpu().numpy()
+        return v
+
+    @right_rectified.setter
+    def right_rectified(self, v):
+        self.__dict__["_right_rect"] = v
 
     def __init__(self, downscale_factor=1.0, fast_mode=False) -> None:
         self.downscale_factor = downscale_factor
@@ -261,8 +295,8 @@ class StereoCore:
             tl = torch.from_numpy(np.ascontiguousarray(left_source)).to(dev)
             tr = torch.from_numpy(np.ascontiguousarray(right_source)).to(dev)
             d, z = self.estimate_depth_device(tl, tr)
-            self.left_rectified = self.left_rectified.cpu().numpy()
-            self.right_rectified = self.right_rectified.cpu().numpy()
+            self.left_rectified = _HostView(self.left_rectified)
+            self.right_rectified = _HostView(self.right_rectified)
             self.disparity_map = d.cpu().numpy()
             self.depth_map = None if z is None else z.cpu().numpy()
             return self.disparity_map, self.depth_map

@@ -135,10 +135,47 @@ def test_multi_device_stereo_matches_oracle():
     run = MultiDeviceStereo(devices=devs, **kw)
     out = list(run.map(iter(frames)))
     assert len(out) == len(frames)
-    for (L, R), (fixed, flt) in zip(frames, out):
+    for (L, R), fixed in zip(frames, out):
         ref = stereo_bm(L, R, **kw)
         np.testing.assert_array_equal(fixed, ref["fixed"])
-        np.testing.assert_array_equal(flt, ref["fixed"].astype(np.float32) / 16.0)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("depth,streams,lr", [(3, 2, 1), (2, 1, -1), (4, 3, 1)])
+def test_host_pipeline_in_flight_matches_oracle(depth, streams, lr):
+    """HostPipeline: frames in flight over several streams (LR buffers shared by one handle),
+    numpy and pinned-tensor inputs, a shape change mid-stream, views vs copies."""
+    import torch
+    from depthestimation_amd.multigpu import HostPipeline
+    from depthestimation_amd.synthetic import stereo_pair
+    from oracle.stereo_bm import stereo_bm
+    kw = dict(min_disp=0, num_disp=64, block_size=5, cost="sad", uniqueness_ratio=10, disp12_max_diff=lr,
+              subpixel=True)
+    frames = [stereo_pair(40, 200, 0, 64, seed=200 + i)[:2] for i in range(7)]
+    frames += [stereo_pair(33, 150, 0, 64, seed=300 + i)[:2] for i in range(3)]
+    inputs = []
+    for i, (L, R) in enumerate(frames):
+        if i % 2:
+            t = torch.empty((2,) + L.shape, dtype=torch.uint8, pin_memory=True)
+            t[0].numpy()[...] = L
+            t[1].numpy()[...] = R
+            inputs.append(t)
+        else:
+            inputs.append((L, R))
+    pipe = HostPipeline(0, depth=depth, streams=streams, copy=True, **kw)
+    out = list(pipe.run(iter(inputs)))
+    pipe.close()
+    assert len(out) == len(frames)
+    for (L, R), fixed in zip(frames, out):
+        np.testing.assert_array_equal(fixed, stereo_bm(L, R, **kw)["fixed"])
+    # views: valid until `depth` further frames are pushed
+    pipe = HostPipeline(0, depth=depth, streams=streams, copy=False, **kw)
+    for i, pair in enumerate(frames[:5]):
+        for j, view in pipe.push(i, pair):
+            np.testing.assert_array_equal(view, stereo_bm(*frames[j], **kw)["fixed"])
+    for j, view in pipe.drain_all():
+        np.testing.assert_array_equal(view, stereo_bm(*frames[j], **kw)["fixed"])
+    pipe.close()
 
 
 @pytest.mark.gpu
