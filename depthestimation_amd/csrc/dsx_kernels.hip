@@ -34,6 +34,9 @@ __device__ __forceinline__ uint32_t group_min(uint32_t v, int tpp) {
     return v;
 }
 
+constexpr int kVolScratch = kVolThreads + kVolThreads / 8;  // padded scratch slots per vector
+__host__ __device__ constexpr int kvpad(int W) { return W + (W >> 4) + 1; }  // padded LR key row (ridx)
+
 template <bool SSD>
 using cost_t = typename std::conditional<SSD, uint32_t, uint16_t>::type;
 
@@ -45,7 +48,7 @@ typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 // vol_wta: K2 of the volume path, one block per image row
 // ---------------------------------------------------------------------------------------
 // Lane (k, s) of a chunk owns the 16-disparity slice s of pixel xc0 + k (SAD 32 B, SSD 64 B)
-// and reads it straight from HBM into registers with non-temporal loads; a 3-deep register ring
+// and reads it straight from HBM into registers; a 3-deep register ring
 // keeps two chunks in flight while one is reduced (the prologue is issued in chunk order: a
 // prologue the scheduler reorders makes hipcc's loop vmcnt waits drain the ring every chunk).  Keys (cost << DB | d) give the lowest-d WTA; the TPP = Dp/16
 // lanes of a pixel combine with DPP / swizzle.  C(b-1), C(b+1) for the sub-pixel come from a
@@ -86,17 +89,26 @@ __global__ __launch_bounds__(kVolThreads) void vol_wta(VolArgs a) {
     const int dbase = s * TX;
     const uint32_t dmask = (1u << DB) - 1u;
 
-    // LDS: per-lane slice scratch (sub-pixel neighbours, wave-private) | LR row state
-    // vector-major (scratch[i][lane]): each ds_write_b128 group of 8 lanes covers 128 contiguous
-    // bytes; the lane-major copy (lane stride 32 / 64 B) cost 4.5 / 11 conflict cycles per LDS op
+    // LDS: per-lane slice scratch (sub-pixel neighbours, wave-private) | segment results | LR row
+    // state.  Scratch is vector-major with one 16-B pad per 8 lanes: slot(i, L) = i * 288 + L + L / 8.
+    // Each ds_write_b128 group of 8 lanes covers 128 contiguous bytes (the lane-major copy of round 1,
+    // lane stride 32 / 64 B, cost 4.5 / 11 conflict cycles per LDS op), and the pad rotates the
+    // banks of the pixels' first lanes (tid = k * TPP), which read C(b -+ 1) at data-dependent slots.
     uint4 *scratch = reinterpret_cast<uint4 *>(smem);
-    uint8_t *rowbase = smem + (size_t)kVolThreads * NV * 16;
-    uint32_t *bestR = reinterpret_cast<uint32_t *>(rowbase);
-    int16_t *rowFixed = reinterpret_cast<int16_t *>(rowbase + (size_t)round16(W * 4));
-    int16_t *rowB = rowFixed + W;
-    float *rowF = reinterpret_cast<float *>(rowbase + (size_t)round16(W * 4) + (size_t)round16(W * 4));
+    auto slot = [](int i, int L) __attribute__((always_inline)) { return i * kVolScratch + L + (L >> 3); };
+    const int S = xb - xa;  // results staged per segment, 4 B per pixel (no shared dwords)
+    uint8_t *rowbase = smem + (size_t)kVolScratch * NV * 16;
+    const size_t fbytes = a.float_mode == 1 ? (size_t)round16(S * 4) : 0;  // rowF only for float_mode 1
+    int32_t *rowFixed = reinterpret_cast<int32_t *>(rowbase);
+    float *rowF = reinterpret_cast<float *>(rowbase + (size_t)round16(S * 4));
+    // LR: right-view keys of the whole row (S = W) at ridx(xr) = xr + xr / 16.  The lanes of one
+    // ds_min_u32 scatter hit xr = x0 + k - 16 s - j (pixel k, slice s), i.e. only 8 banks for 64
+    // lanes unpadded; one pad word per 16 keys spreads the slices over the banks (17 s mod 32).
+    uint32_t *bestR = reinterpret_cast<uint32_t *>(rowbase + (size_t)round16(S * 4) + fbytes);
+    auto ridx = [](int xr) __attribute__((always_inline)) { return xr + (xr >> 4); };
+    int16_t *rowB = reinterpret_cast<int16_t *>(rowbase + (size_t)round16(S * 4) + fbytes + (size_t)round16(kvpad(W) * 4));
     if (lr) {
-        for (int i = tid; i < W; i += kVolThreads) bestR[i] = 0xFFFFFFFFu;
+        for (int i = tid; i < W + (W >> 4) + 1; i += kVolThreads) bestR[i] = 0xFFFFFFFFu;
         __syncthreads();
     }
 
@@ -108,7 +120,10 @@ __global__ __launch_bounds__(kVolThreads) void vol_wta(VolArgs a) {
         const u32x4 *p = reinterpret_cast<const u32x4 *>(vrow + (size_t)x * Dp + dbase);
 #pragma unroll
         for (int i = 0; i < NV; ++i) {
-            const u32x4 t = __builtin_nontemporal_load(&p[i]);
+            // SAD: non-temporal (C2 K2 146 -> 111-122 us under rocprofv3); SSD: plain (its four
+            // 16-B pieces per lane split each line over four instructions, and non-temporal loads
+            // then refetch it: C3 K2 536 -> 798 us, 2.15 -> 2.95 GB)
+            const u32x4 t = SSD ? p[i] : __builtin_nontemporal_load(&p[i]);
             v[i] = make_uint4(t.x, t.y, t.z, t.w);
         }
     };
@@ -118,7 +133,7 @@ __global__ __launch_bounds__(kVolThreads) void vol_wta(VolArgs a) {
         const bool inb = x < xb;
         if (a.subpix) {
 #pragma unroll
-            for (int i = 0; i < NV; ++i) scratch[i * kVolThreads + tid] = cur[i];
+            for (int i = 0; i < NV; ++i) scratch[slot(i, tid)] = cur[i];
         }
         uint32_t best = 0xFFFFFFFFu;
 #pragma unroll
@@ -143,7 +158,7 @@ __global__ __launch_bounds__(kVolThreads) void vol_wta(VolArgs a) {
             for (int j = 0; j < TX; ++j) {
                 const int dj = dbase + j;
                 const int xr = x - m - dj;
-                if (dj < D && xr >= 0 && xr < W) atomicMin(&bestR[xr], (slice_cost<SSD>(cur, j) << DB) | (uint32_t)dj);
+                if (dj < D && xr >= 0 && xr < W) atomicMin(&bestR[ridx(xr)], (slice_cost<SSD>(cur, j) << DB) | (uint32_t)dj);
             }
         }
         if (s == 0 && inb) {
@@ -155,7 +170,7 @@ __global__ __launch_bounds__(kVolThreads) void vol_wta(VolArgs a) {
                 // C(d): element d % TX of lane tid + d / TX's slice
                 auto cost_at = [&](int d) __attribute__((always_inline)) -> int32_t {
                     const int e = (d & (TX - 1)) * (int)sizeof(CT);
-                    const uint8_t *pv = reinterpret_cast<const uint8_t *>(scratch + (e >> 4) * kVolThreads + tid + d / TX);
+                    const uint8_t *pv = reinterpret_cast<const uint8_t *>(scratch + slot(e >> 4, tid + d / TX));
                     return (int32_t)*reinterpret_cast<const CT *>(pv + (e & 15));
                 };
                 const int32_t cm = cost_at(b - 1);
@@ -168,9 +183,9 @@ __global__ __launch_bounds__(kVolThreads) void vol_wta(VolArgs a) {
             const int16_t fx = (int16_t)(m * 16 + f);
             // results go to LDS row buffers: no global stores inside the streaming loop, so the
             // compiler's vmcnt counting stays exact and the ring keeps two chunks in flight
-            rowFixed[x] = valid ? fx : (int16_t)((m - 1) * 16);
+            rowFixed[x - xa] = valid ? fx : (int16_t)((m - 1) * 16);
             if (lr) rowB[x] = valid ? (int16_t)b : (int16_t)-1;
-            if (a.float_mode == 1) rowF[x] = valid ? pf : (float)(m - 1);
+            if (a.float_mode == 1) rowF[x - xa] = valid ? pf : (float)(m - 1);
         }
         if (a.subpix) __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront", "local");  // reads before next writes
     };
@@ -190,21 +205,21 @@ __global__ __launch_bounds__(kVolThreads) void vol_wta(VolArgs a) {
     }
     __syncthreads();
     for (int x = xa + tid; x < xb; x += kVolThreads) {
-        int16_t fx = rowFixed[x];
+        int16_t fx = (int16_t)rowFixed[x - xa];
         bool valid = true;
         if (lr) {
             const int b = rowB[x];
             valid = b >= 0;
             if (valid) {
                 const int xr = x - m - b;
-                const int df = (int)(bestR[xr] & dmask) - b;
+                const int df = (int)(bestR[ridx(xr)] & dmask) - b;
                 if (df > a.lr || df < -a.lr) valid = false;
             }
             if (!valid) fx = (int16_t)((m - 1) * 16);
         }
         const long o = (long)y * W + x;
         if (a.out_fixed) a.out_fixed[o] = fx;
-        if (a.out_float) a.out_float[o] = a.float_mode == 0 ? (float)fx * 0.0625f : (valid ? rowF[x] : (float)(m - 1));
+        if (a.out_float) a.out_float[o] = a.float_mode == 0 ? (float)fx * 0.0625f : (valid ? rowF[x - xa] : (float)(m - 1));
     }
 }
 
@@ -264,15 +279,20 @@ hipError_t launch_lr_fixup(const int16_t *dstar, const uint32_t *keys, uint32_t 
 // ---------------------------------------------------------------------------------------
 // Host-side dispatch
 // ---------------------------------------------------------------------------------------
+// scratch (padded slots) + segment results (int32, and f32 for float_mode 1, per pixel of an
+// S-pixel segment) + LR row state (bestR u32 + rowB int16 per pixel of the row)
+static size_t vol_smem(bool ssd, int S, int W, bool lr, bool fm1) {
+    return (size_t)kVolScratch * (ssd ? 64 : 32) + (size_t)round16(S * 4) * (fm1 ? 2 : 1) +
+           (lr ? (size_t)round16(kvpad(W) * 4) + (size_t)round16(W * 2) : 0);
+}
+
 size_t volume_smem_bytes(int TX, bool ssd, int Dp, int TPP, int W) {
     (void)TX, (void)Dp, (void)TPP;
-    // per-lane 16-disparity slice scratch + bestR (LR), rowFixed + rowB, rowF
-    return (size_t)kVolThreads * (ssd ? 64 : 32) + (size_t)round16(W * 4) * 2 + (size_t)W * 4;
+    return vol_smem(ssd, W, W, true, true);  // the largest form (one segment per row, LR, float_mode 1)
 }
 
 template <bool SSD, bool UNIQ, bool LR, int RING>
 static hipError_t launch_vol_ring(const VolArgs &a, hipStream_t st) {
-    const size_t smem = volume_smem_bytes(16, SSD, a.Dp, a.TPP, a.W);
     static bool attr_done[64] = {};
     int dev = 0;
     (void)hipGetDevice(&dev);
@@ -289,6 +309,9 @@ static hipError_t launch_vol_ring(const VolArgs &a, hipStream_t st) {
         return e ? atoi(e) : 4;
     }();
     const int nseg = LR ? 1 : (seg > 1 ? seg : 1);
+    const int XC = kVolThreads / (a.Dp / 16);
+    const int XSg = ((a.W + nseg - 1) / nseg + XC - 1) / XC * XC;  // as the kernel computes it
+    const size_t smem = vol_smem(SSD, std::min(XSg, a.W), a.W, LR, a.float_mode == 1);
     hipLaunchKernelGGL((vol_wta<SSD, UNIQ, LR, RING>), dim3(a.H, nseg), dim3(kVolThreads), smem, st, a);
     return hipGetLastError();
 }
