@@ -10,7 +10,8 @@
 // where Lp(d +- 1) across lane boundaries come from DPP wave_shr:1 / wave_shl:1, and
 // mp = min_d Lp(d) from a DPP row reduction plus four readlanes.  The first direction writes
 // S = L, later ones add.  Disparities >= D are +inf in the recurrence and hold `pads` in S so
-// the K2 epilogue never picks them.  C and S are loaded RING steps ahead (ring of registers).
+// the K2 epilogue never picks them.  C and S are loaded a chunk of RING steps ahead (two register
+// buffers).
 #include "dsx_internal.h"
 
 #include <type_traits>
@@ -98,8 +99,11 @@ __host__ __device__ inline int sgm_num_paths(int H, int W, int dx, int dy) {
 template <int NPL, bool FIRST>
 __global__ __launch_bounds__(256) void sgm_path(SgmArgs a) {
     using CV = CostVec<NPL>;
-    // loads run RING steps ahead of the recurrence: a path's pixels are a fixed stride apart,
-    // so the addresses are known and HBM latency hides behind RING steps of compute
+    // The path is walked in chunks of RING steps held in two register buffers: the loads of chunk
+    // j+1 are issued before chunk j is computed and its S vectors stored.  (A ring that loads one
+    // step ahead per step interleaves every load with a store, and hipcc, whose vmcnt counts both
+    // on gfx950, then waits vmcnt(0) on every step: each step paid a full HBM round trip.  Round 1's
+    // kernel did that.)
     constexpr int RING = NPL == 2 ? 16 : 8;
     const int wv = threadIdx.x >> 6, ln = threadIdx.x & 63;
     const int H = a.H, W = a.W, dx = a.dx, dy = a.dy;
@@ -129,27 +133,21 @@ __global__ __launch_bounds__(256) void sgm_path(SgmArgs a) {
     auto loadC = [&](int k) -> typename CV::C { return *reinterpret_cast<const typename CV::C *>(Cb + k * step); };
     auto loadS = [&](int k) -> typename CV::S { return *reinterpret_cast<const typename CV::S *>(Sb + k * step); };
 
-    typename CV::C cr[RING];
-    typename CV::S sr[RING];
+    typename CV::C ca[RING], cb[RING];
+    typename CV::S sa[RING], sb[RING];
+    // chunk starting at step k0 into a buffer (steps past the path re-read its last pixel)
+    auto load_chunk = [&](int k0, typename CV::C(&cr)[RING], typename CV::S(&sr)[RING]) __attribute__((always_inline)) {
 #pragma unroll
-    for (int i = 0; i < RING; ++i) {
-        const int kk = i < n ? i : n - 1;
-        cr[i] = loadC(kk);
-        if constexpr (!FIRST) sr[i] = loadS(kk);
-    }
+        for (int i = 0; i < RING; ++i) {
+            const int kk = k0 + i < n ? k0 + i : n - 1;
+            cr[i] = loadC(kk);
+            if constexpr (!FIRST) sr[i] = loadS(kk);
+        }
+    };
     uint32_t Lp[NPL];
     uint32_t mp = 0;
-    // one recurrence step on ring slot I (compile-time, so the ring stays in registers)
-    auto stepk = [&](auto Ic, int k) __attribute__((always_inline)) {
-        constexpr int I = decltype(Ic)::value;
-        const typename CV::C cv = cr[I];
-        typename CV::S sv{};
-        if constexpr (!FIRST) sv = sr[I];
-        {
-            const int kn = k + RING < n ? k + RING : n - 1;
-            cr[I] = loadC(kn);
-            if constexpr (!FIRST) sr[I] = loadS(kn);
-        }
+    // one recurrence step on buffer slot i (compile-time, so the buffers stay in registers)
+    auto stepk = [&](const typename CV::C &cv, const typename CV::S &sv, int k) __attribute__((always_inline)) {
         uint32_t c[NPL], L[NPL];
         unpackC<NPL>(cv, c);
         if (k == 0) {
@@ -180,13 +178,25 @@ __global__ __launch_bounds__(256) void sgm_path(SgmArgs a) {
         }
         *reinterpret_cast<typename CV::S *>(Sb + k * step) = packS<NPL>(sarr);
     };
-    const int nfull = n - n % RING;
-    for (int k0 = 0; k0 < nfull; k0 += RING)
-        sfor_sgm<0, RING>([&](auto Ic) __attribute__((always_inline)) { stepk(Ic, k0 + decltype(Ic)::value); });
-    // tail: fewer than RING steps (wave-uniform guards)
-    sfor_sgm<0, RING>([&](auto Ic) __attribute__((always_inline)) {
-        if (nfull + decltype(Ic)::value < n) stepk(Ic, nfull + decltype(Ic)::value);
-    });
+    auto run_chunk = [&](int k0, const typename CV::C(&cr)[RING], const typename CV::S(&sr)[RING]) __attribute__((always_inline)) {
+        sfor_sgm<0, RING>([&](auto Ic) __attribute__((always_inline)) {
+            constexpr int I = decltype(Ic)::value;
+            if (k0 + I < n) stepk(cr[I], sr[I], k0 + I);  // wave-uniform guard (the last chunk)
+        });
+    };
+    // Each chunk's loads are issued behind an explicit full wait (the previous chunk's stores and
+    // the chunk about to be computed): hipcc then sees only loads pending while a chunk computes,
+    // and the next wait lands after a whole chunk of compute instead of before every step.
+    load_chunk(0, ca, sa);
+    for (int k0 = 0; k0 < n; k0 += 2 * RING) {
+        __builtin_amdgcn_s_waitcnt(0);
+        if (k0 + RING < n) load_chunk(k0 + RING, cb, sb);
+        run_chunk(k0, ca, sa);
+        if (k0 + RING >= n) break;
+        __builtin_amdgcn_s_waitcnt(0);
+        if (k0 + 2 * RING < n) load_chunk(k0 + 2 * RING, ca, sa);
+        run_chunk(k0 + RING, cb, sb);
+    }
 }
 
 template <int NPL>
