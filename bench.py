@@ -218,6 +218,7 @@ def main():
     ap.add_argument("--batch", type=int, default=1, help="frame pairs per GPU per step (one launch)")
     ap.add_argument("--no-batched", action="store_true", help="skip the secondary batched measurement")
     ap.add_argument("--no-e2e", action="store_true", help="skip the PCIe-inclusive host-buffer measurement")
+    ap.add_argument("--no-post", action="store_true", help="skip the device post-processing timings")
     ap.add_argument("--no-ref-defaults", action="store_true",
                     help="skip the secondary C2 measurement with the reference's uniqueness/LR defaults")
     ap.add_argument("--sgm", default=None, choices=["sgbm_3way", "hh4", "sgbm", "hh"],
@@ -428,6 +429,43 @@ def main():
         mr.close()
         mrt.close()
 
+    # secondary: the reference's per-frame steps after the matcher on the device (SURVEY 8f F1/F2 and
+    # hole filling, stereo_core.py:168-196 / postprocess.py), on this rank's matcher output for frame 0:
+    # median of 30 stream-event timings each
+    post = None
+    if args.config in ("c2", "c4") and args.path == "fused" and not args.sgm and not args.no_post and B == 1:
+        from depthestimation_amd.matcher import fill_holes_device, postprocess_fast_device, postprocess_full_device
+        dsp = torch.empty((H, W), dtype=torch.float32, device=dev)
+        matcher.compute_device(frames[0][0], frames[0][1], out_float=dsp, stream=stream)
+        D = cfg["num_disp"]
+
+        def tmed(fn, n=30):
+            ts = []
+            for i in range(n + 3):
+                a_, b_ = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                a_.record(stream)
+                fn()
+                b_.record(stream)
+                b_.synchronize()
+                if i >= 3:
+                    ts.append(a_.elapsed_time(b_))
+            return round(float(np.median(ts)), 4)
+
+        with torch.cuda.stream(stream):
+            clean, _ = postprocess_full_device(dsp, D, max_speckle_size=100, max_diff=1.0, outlier_threshold=2.5,
+                                               stream=stream)
+            post = {"matcher_ms": tmed(lambda: matcher.compute_device(frames[0][0], frames[0][1], out_float=dsp,
+                                                                      stream=stream)),
+                    "fast_mode_ms": tmed(lambda: postprocess_fast_device(dsp, D, 700.0, 0.1, stream=stream)),
+                    "default_mode_ms": tmed(lambda: postprocess_full_device(
+                        dsp, D, max_speckle_size=100, max_diff=1.0, outlier_threshold=2.5, focal_length=700.0,
+                        baseline=0.1, stream=stream)),
+                    "hole_filling_ms": tmed(lambda: fill_holes_device(clean, radius=3, stream=stream), 10),
+                    "hole_pixels": int((clean <= 0).sum().item()),
+                    "note": "secondary: device post-processing of this frame's map (fast mode: crop + median + depth; "
+                            "default mode: speckles + outliers + median + depth; hole filling: Telea radius 3 on the "
+                            "default-mode map's holes), stream events, median of 30 (10)"}
+
     result = None
     if rank == 0:
         px_total = H * W * B * args.steps * ws
@@ -540,6 +578,8 @@ def main():
             result["e2e_host"] = e2e
         if refdef is not None:
             result["c2_reference_defaults"] = refdef
+        if post is not None:
+            result["post_processing"] = post
 
         if not args.no_cpu_baseline and ws == 1:
             result["cpu_baseline"] = cpu_baseline(args, cfg, hostL[0], hostR[0])
