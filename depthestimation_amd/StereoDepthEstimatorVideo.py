@@ -11,8 +11,8 @@ downscale_factor squared) is kept, so results match the reference's.
 Multi-GPU, two forms: pass ``rank``/``world_size`` (or let them come from the
 torch.distributed env) to process only frames i with i % world_size == rank in one process per
 GPU (``sharding.py``); or pass ``devices=[0, 1, ...]`` to drive several GPUs from this one
-process (``multigpu.MultiDeviceStereo``: frame i on devices[i % N], one StereoCore per worker,
-results yielded in frame order).
+process (``multigpu.DepthPipeline`` per device: frame i on devices[i % N], several frames in flight
+per device, results yielded in frame order).
 """
 from __future__ import annotations
 
@@ -92,9 +92,11 @@ class StereoDepthEstimatorVideo:
             frame_start_time = time.time()
 
     def _estimate_multi_device(self):
-        """Single-process multi-GPU form: every worker owns a StereoCore with this facade's
-        (already re-scaled) parameters on its device; depth maps come back in frame order."""
-        from .multigpu import MultiDeviceStereo
+        """Single-process multi-GPU form: every device runs a ``multigpu.DepthPipeline`` (frames in
+        flight, gray / rectify -> match -> post-process -> depth in HBM, equal bit for bit to the
+        host path, tests/test_gpu_host_api.py) over its own StereoCore with this facade's (already
+        re-scaled) parameters; depth maps come back in frame order."""
+        from .multigpu import DepthPipeline, sharded_map
 
         params = dict(self.core.get_sgbm_params())
         ds, fast = self.downscale_factor, self.fast_mode
@@ -106,25 +108,10 @@ class StereoDepthEstimatorVideo:
             core.sgbm_params.update(params)
             core.sgbm_params['device'] = dev
             core._build_sgbm()
-            if core.sgbm_params.get('hole_filling', False):  # Telea inpainting: host path
-                return lambda pair: core.estimate_depth(pair[0], pair[1])[1]
-            stream = torch.cuda.Stream(device=dev)
+            return DepthPipeline(core, dev, depth=3, streams=2)
 
-            def run(pair):
-                # device pipeline (rectify/gray -> match -> post-process -> depth in HBM), equal
-                # bit for bit to the host path (tests/test_gpu_host_api.py)
-                with torch.cuda.stream(stream):
-                    tl = torch.from_numpy(np.ascontiguousarray(pair[0])).to(dev, non_blocking=True)
-                    tr = torch.from_numpy(np.ascontiguousarray(pair[1])).to(dev, non_blocking=True)
-                    _, depth = core.estimate_depth_device(tl, tr, stream=stream)
-                    out = None if depth is None else depth.cpu().numpy()
-                stream.synchronize()
-                return out
-            return run
-
-        runner = MultiDeviceStereo(devices=self.devices, streams_per_device=1)
         frame_start_time = time.time()
-        for depth_m in runner.map_fn(self._frames(), make):
+        for depth_m in sharded_map(self._frames(), self.devices, make, queue_depth=4, pipelined=True):
             yield depth_m
             if self._frame_interval > 0:
                 sleep_time = self._frame_interval - (time.time() - frame_start_time)

@@ -293,6 +293,75 @@ class HostPipeline:
         self.m.close()
 
 
+class DepthPipeline:
+    """The video path's per-frame work on one GPU with ``depth`` frames in flight: host frame
+    pairs (uint8 BGR H x W x 3 or gray) -> pinned slot -> HBM -> ``StereoCore.estimate_depth_device``
+    (gray / rectify, matcher, post-processing, depth; stereo_core.py:274-293) -> depth map back in
+    pinned memory.  Frame i runs on stream i mod ``streams`` in ring slot i mod ``depth``; a push
+    waits only on the frame that last used its slot.  ``push`` returns the completed frames'
+    depth maps (numpy copies, None when focal length / baseline are unset - what the reference's
+    generator yields, StereoDepthEstimatorVideo.py:101-103)."""
+
+    def __init__(self, core, device: int, depth: int = 3, streams: int = 2):
+        import torch
+        self.torch = torch
+        self.core = core
+        self.dev = torch.device("cuda", int(device))
+        torch.cuda.set_device(self.dev)
+        self.depth = max(2, int(depth))
+        self.streams = [torch.cuda.Stream(device=self.dev) for _ in range(max(1, int(streams)))]
+        self.shape = None
+        self.pending: List[Optional[Tuple[int, object, object]]] = [None] * self.depth
+
+    def _alloc(self, shape) -> None:
+        torch = self.torch
+        self.shape = shape
+        self.hin = [(torch.empty(shape, dtype=torch.uint8, pin_memory=True),
+                     torch.empty(shape, dtype=torch.uint8, pin_memory=True)) for _ in range(self.depth)]
+        self.hout = [None] * self.depth  # pinned depth maps, allocated on first use (size known then)
+
+    def _finish(self, slot: int):
+        i, ev, z = self.pending[slot]
+        ev.synchronize()
+        self.pending[slot] = None
+        return i, (None if z is None else self.hout[slot][: z[0], : z[1]].numpy().copy())
+
+    def push(self, i: int, pair) -> List[Tuple[int, Optional[np.ndarray]]]:
+        torch = self.torch
+        L, R = (np.asarray(pair[0]), np.asarray(pair[1]))
+        if L.dtype != np.uint8 or L.shape != R.shape or L.ndim not in (2, 3):
+            raise ValueError("frames must be uint8 arrays of one shape (H x W x 3 BGR or H x W)")
+        done = []
+        if self.shape != L.shape:
+            done = self.drain_all()
+            self._alloc(L.shape)
+        slot = i % self.depth
+        if self.pending[slot] is not None:
+            done.append(self._finish(slot))
+        hl, hr = self.hin[slot]
+        np.copyto(hl.numpy(), L)
+        np.copyto(hr.numpy(), R)
+        st = self.streams[i % len(self.streams)]
+        with torch.cuda.stream(st):
+            dl = hl.to(self.dev, non_blocking=True)
+            dr = hr.to(self.dev, non_blocking=True)
+            _, z = self.core.estimate_depth_device(dl, dr, stream=st)
+            zshape = None
+            if z is not None:
+                if self.hout[slot] is None or self.hout[slot].shape != z.shape:
+                    self.hout[slot] = torch.empty(z.shape, dtype=torch.float32, pin_memory=True)
+                self.hout[slot].copy_(z, non_blocking=True)
+                zshape = tuple(z.shape)
+            ev = torch.cuda.Event()
+            ev.record(st)
+        self.pending[slot] = (i, ev, zshape)
+        return done
+
+    def drain_all(self) -> List[Tuple[int, Optional[np.ndarray]]]:
+        live = sorted((p[0], s) for s, p in enumerate(self.pending) if p is not None)
+        return [self._finish(s) for _, s in live]
+
+
 class MultiDeviceStereo:
     """Frame-sharded matcher over several GPUs of one process (see module docstring).
 

@@ -179,22 +179,28 @@ def test_host_pipeline_in_flight_matches_oracle(depth, streams, lr):
 
 
 @pytest.mark.gpu
-def test_video_estimator_devices_matches_single_device():
-    devs = _devices()
+@pytest.mark.parametrize("fast,holes,rep", [(True, False, 1), (False, False, 2), (False, True, 1)])
+def test_video_estimator_devices_matches_single_device(fast, holes, rep):
+    """devices=[...]: DepthPipeline per device (frames in flight over two streams, pinned slots)
+    yields exactly the sequential facade's depth maps, in order; fast and default (+ hole filling)
+    post-processing, two workers on one GPU.  (Without focal length the facade raises, as the
+    reference does: estimate_depth re-applies configure_sgbm, which scales focal_length=None,
+    StereoDepthEstimatorVideo.py:78 -> stereo_core.py:114-115.)"""
+    devs = _devices() * rep
     from depthestimation_amd import StereoDepthEstimatorVideo
     from depthestimation_amd.synthetic import stereo_pair
-    frames = [stereo_pair(48, 160, 0, 32, seed=i) for i in range(5)]
+    frames = [stereo_pair(48, 160, 0, 32, seed=i) for i in range(11)]
     Ls = [np.repeat(f[0][:, :, None], 3, 2) for f in frames]
     Rs = [np.repeat(f[1][:, :, None], 3, 2) for f in frames]
 
     def run(devices):
-        v = StereoDepthEstimatorVideo(list(Ls), list(Rs), fast_mode=True, target_fps=0, use_threading=False,
+        v = StereoDepthEstimatorVideo(list(Ls), list(Rs), fast_mode=fast, target_fps=0, use_threading=False,
                                       devices=devices)
-        v.configure_sgbm(num_disp=32, block_size=5, focal_length=100.0, baseline=0.1)
+        v.configure_sgbm(num_disp=32, block_size=5, focal_length=100.0, baseline=0.1, hole_filling=holes)
         return list(v.estimate_depth())
 
     a, b = run(None), run(devs)
-    assert len(a) == len(b) == 5
+    assert len(a) == len(b) == len(frames)
     for x, y in zip(a, b):
         np.testing.assert_array_equal(x, y)
 
