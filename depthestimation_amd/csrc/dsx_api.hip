@@ -51,6 +51,18 @@ bool pick_geometry(int D, int cost, dsx::Geometry &g) {
     return true;
 }
 
+// SGM path sets by mode (oracle/sgm.py DIRECTIONS order)
+const int kSgmDirs[8][2] = {{1, 0}, {-1, 0}, {0, 1}, {0, -1}, {1, 1}, {-1, 1}, {1, -1}, {-1, -1}};
+int sgm_set(int mode, const int **set) {
+    static const int set3[] = {0, 1, 2}, set4[] = {0, 1, 2, 3}, set5[] = {0, 1, 2, 4, 5}, set8[] = {0, 1, 2, 3, 4, 5, 6, 7};
+    switch (mode) {
+        case DSX_AGG_HH4: *set = set4; return 4;
+        case DSX_AGG_SGBM: *set = set5; return 5;
+        case DSX_AGG_HH: *set = set8; return 8;
+        default: *set = set3; return 3;
+    }
+}
+
 uint64_t max_cost(const dsx_params &p) {
     const uint64_t n = (uint64_t)p.block_size * p.block_size;
     return n * (p.cost == DSX_COST_SSD ? 255ull * 255ull : 255ull);
@@ -115,7 +127,8 @@ struct dsx_handle {
     int16_t *dStar = nullptr;    // LR check: left winners (or -1) for lr_fixup
     void *vol = nullptr;
     size_t vol_bytes = 0;
-    uint32_t *sgmS = nullptr;  // SGM path sums [H][W][Dp] u32
+    uint32_t *sgmS = nullptr;  // SGM path sums [H][W][Dp] u32 (sequential directions)
+    uint16_t *sgmL = nullptr;  // SGM L_r per direction, ndir x [H][W][Dp] u16 (concurrent directions)
     // timing
     std::vector<std::string> knames;
     std::vector<double> ktotal;
@@ -136,6 +149,8 @@ void free_buffers(dsx_handle *h) {
     (void)hipFree(h->vol);
     (void)hipFree(h->sgmS);
     h->sgmS = nullptr;
+    (void)hipFree(h->sgmL);
+    h->sgmL = nullptr;
     h->dL = h->dR = nullptr;
     h->dFixed = nullptr;
     h->dFloat = nullptr;
@@ -147,6 +162,20 @@ void free_buffers(dsx_handle *h) {
     h->lrFrames = 0;
     h->lrDirty[0] = h->lrDirty[1] = 0;
     h->lrPending = false;
+}
+
+int sgm_p1(const dsx_handle *h) { return h->p.p1 > 0 ? h->p.p1 : 8 * h->p.block_size * h->p.block_size; }
+int sgm_p2(const dsx_handle *h) { return h->p.p2 > 0 ? h->p.p2 : 32 * h->p.block_size * h->p.block_size; }
+
+// All directions in one launch with u16 L_r per direction while max cost + P2 stays below 0xFFFF
+// (L_r <= C + P2; the default P2 = 32 bs^2 always does), else the sequential u32 accumulation.
+// DSX_SGM_SEQ=1 forces the sequential form.
+bool sgm_concurrent(const dsx_handle *h) {
+    static const bool seq = [] {
+        const char *e = getenv("DSX_SGM_SEQ");
+        return e && *e == '1';
+    }();
+    return !seq && max_cost(h->p) + (uint64_t)sgm_p2(h) < 0xFFFFull;
 }
 
 int ensure_buffers(dsx_handle *h, int H, int W, bool host_staging, int nframes = 1) {
@@ -182,7 +211,15 @@ int ensure_buffers(dsx_handle *h, int H, int W, bool host_staging, int nframes =
         h->vol_bytes = n * h->g.Dp * cbytes;
         DSX_HIP(hipMalloc(&h->vol, h->vol_bytes));
     }
-    if (h->p.aggregation && !h->sgmS) DSX_HIP(hipMalloc(&h->sgmS, n * h->g.Dp * 4));
+    if (h->p.aggregation) {
+        if (sgm_concurrent(h)) {
+            const int *set;
+            const int nd = sgm_set(h->p.aggregation, &set);
+            if (!h->sgmL) DSX_HIP(hipMalloc(&h->sgmL, (size_t)nd * n * h->g.Dp * 2));
+        } else if (!h->sgmS) {
+            DSX_HIP(hipMalloc(&h->sgmS, n * h->g.Dp * 4));
+        }
+    }
     h->cH = H;
     h->cW = W;
     h->cDp = h->g.Dp;
@@ -383,17 +420,31 @@ int run(dsx_handle *h, const void *dL, const void *dR, int H, int W, int64_t str
             a.vol = h->vol;
             DSX_LAUNCH(h, "cost_volume", st, dsx::launch_bm2(radius, ssd, h->g.NW, a, st));
             const bool agg = h->p.aggregation != DSX_AGG_NONE;
-            if (agg) {
+            const bool agg_all = agg && sgm_concurrent(h);
+            const int *set = nullptr;
+            const int nd = agg ? sgm_set(h->p.aggregation, &set) : 0;
+            if (agg_all) {
+                // every path of every direction in one launch, L_r per direction (u16)
+                dsx::SgmAllArgs sa{};
+                sa.C = static_cast<const uint16_t *>(h->vol);
+                sa.L = h->sgmL;
+                sa.lstride = (size_t)H * W * h->g.Dp;
+                sa.H = H;
+                sa.W = W;
+                sa.D = h->p.num_disp;
+                sa.Dp = h->g.Dp;
+                sa.ndir = nd;
+                sa.poff[0] = 0;
+                for (int i = 0; i < nd; ++i) {
+                    sa.dx[i] = kSgmDirs[set[i]][0];
+                    sa.dy[i] = kSgmDirs[set[i]][1];
+                    sa.poff[i + 1] = sa.poff[i] + dsx::sgm_num_paths_host(H, W, sa.dx[i], sa.dy[i]);
+                }
+                sa.P1 = sgm_p1(h);
+                sa.P2 = sgm_p2(h);
+                DSX_LAUNCH(h, "sgm_paths", st, dsx::launch_sgm_all(sa, st));
+            } else if (agg) {
                 // SGM: one pass per direction of the mode's path set (oracle/sgm.py DIRECTIONS)
-                static const int dirs[8][2] = {{1, 0}, {-1, 0}, {0, 1}, {0, -1}, {1, 1}, {-1, 1}, {1, -1}, {-1, -1}};
-                static const int set3[] = {0, 1, 2}, set4[] = {0, 1, 2, 3}, set5[] = {0, 1, 2, 4, 5},
-                                 set8[] = {0, 1, 2, 3, 4, 5, 6, 7};
-                const int *set = set3;
-                int nd = 3;
-                if (h->p.aggregation == DSX_AGG_HH4) set = set4, nd = 4;
-                if (h->p.aggregation == DSX_AGG_SGBM) set = set5, nd = 5;
-                if (h->p.aggregation == DSX_AGG_HH) set = set8, nd = 8;
-                const int bs2 = h->p.block_size * h->p.block_size;
                 dsx::SgmArgs sa{};
                 sa.C = static_cast<const uint16_t *>(h->vol);
                 sa.S = h->sgmS;
@@ -401,17 +452,19 @@ int run(dsx_handle *h, const void *dL, const void *dR, int H, int W, int64_t str
                 sa.W = W;
                 sa.D = h->p.num_disp;
                 sa.Dp = h->g.Dp;
-                sa.P1 = h->p.p1 > 0 ? h->p.p1 : 8 * bs2;
-                sa.P2 = h->p.p2 > 0 ? h->p.p2 : 32 * bs2;
+                sa.P1 = sgm_p1(h);
+                sa.P2 = sgm_p2(h);
                 sa.pads = (uint32_t)((1ull << (32 - h->g.DB)) - 1ull);
                 for (int i = 0; i < nd; ++i) {
-                    sa.dx = dirs[set[i]][0];
-                    sa.dy = dirs[set[i]][1];
+                    sa.dx = kSgmDirs[set[i]][0];
+                    sa.dy = kSgmDirs[set[i]][1];
                     DSX_LAUNCH(h, "sgm_path", st, dsx::launch_sgm_path(sa, i == 0, st));
                 }
             }
             dsx::VolArgs v{};
-            v.vol = agg ? static_cast<const void *>(h->sgmS) : h->vol;
+            v.vol = agg_all ? static_cast<const void *>(h->sgmL) : (agg ? static_cast<const void *>(h->sgmS) : h->vol);
+            v.nsum = agg_all ? nd : 0;
+            v.sstride = (size_t)H * W * h->g.Dp;
             v.H = H;
             v.W = W;
             v.m = h->p.min_disp;

@@ -50,7 +50,9 @@ struct Bm2Args {
 };
 
 struct VolArgs {
-    const void *vol;  // [H][W][Dp] u16 (SAD) or u32 (SSD)
+    const void *vol;  // [H][W][Dp] u16 (SAD) or u32 (SSD); with nsum > 0: nsum u16 volumes summed
+    int nsum;         // > 0: vol = nsum u16 volumes `sstride` elements apart (SGM L_r per direction)
+    size_t sstride;
     int H, W, m, D, Dp, DB, TPP;
     int uniq, lr, subpix, float_mode;
     int16_t *out_fixed;
@@ -95,6 +97,22 @@ struct SgmArgs {
     uint32_t pads;      // S value for disparities >= D (never wins in K2)
 };
 hipError_t launch_sgm_path(const SgmArgs &a, bool first, hipStream_t st);
+
+// All directions of a path set in one launch (dsx_sgm.hip, sgm_paths_all): every path writes its
+// L_r (u16, exact while max cost + P2 < 65535) into its direction's [H][W][Dp] buffer; the K2
+// variant (VolArgs.nsum) sums the buffers per slice.  Disparities >= D hold 0xFFFF.
+struct SgmAllArgs {
+    const uint16_t *C;  // [H][W][Dp] u16 SAD block costs (K1 output)
+    uint16_t *L;        // ndir buffers of [H][W][Dp] u16, dir i at L + i * lstride
+    size_t lstride;
+    int H, W, D, Dp;
+    int ndir;
+    int dx[8], dy[8];
+    int poff[9];        // first global path index of each direction (prefix sums)
+    int P1, P2;
+};
+hipError_t launch_sgm_all(const SgmAllArgs &a, hipStream_t st);
+int sgm_num_paths_host(int H, int W, int dx, int dy);
 
 // Fast-mode epilogue (dsx_post.hip): crop + 3x3 median + optional depth.
 struct PostArgs {

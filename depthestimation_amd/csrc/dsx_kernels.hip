@@ -70,8 +70,12 @@ __device__ __forceinline__ uint32_t slice_cost(const uint4 (&v)[NV], int j) {
     }
 }
 
-template <bool SSD, bool UNIQ, bool LR, int RING>
+template <bool SSD, bool UNIQ, bool LR, int RING, int NSUM = 0>
 __global__ __launch_bounds__(kVolThreads) void vol_wta(VolArgs a) {
+    // NSUM > 0 (SGM, SSD = true): the u32 costs are the sums of NSUM u16 volumes (one L_r per
+    // path direction), loaded as 2 x 16 B per volume and summed when the chunk is processed
+    static_assert(NSUM == 0 || SSD, "summed volumes are reduced as u32 costs");
+    constexpr int RAWN = NSUM > 0 ? 2 * NSUM : (SSD ? 4 : 2);  // 16-B vectors per lane in the ring
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     using CT = cost_t<SSD>;
     constexpr int TX = 16;                          // disparities per lane
@@ -113,10 +117,23 @@ __global__ __launch_bounds__(kVolThreads) void vol_wta(VolArgs a) {
     }
 
     const CT *vrow = reinterpret_cast<const CT *>(a.vol) + (size_t)y * W * Dp;
+    const uint16_t *vrow16 = reinterpret_cast<const uint16_t *>(a.vol) + (size_t)y * W * Dp;
     // unconditional loads (clamped pixel): no branch around them, so the compiler keeps partial
     // vmcnt waits and the ring really has two chunks in flight
-    auto load = [&](int xc0, uint4(&v)[NV]) __attribute__((always_inline)) {
+    auto load = [&](int xc0, uint4(&v)[RAWN]) __attribute__((always_inline)) {
         const int x = min(xc0 + k, xb - 1);
+        if constexpr (NSUM > 0) {
+#pragma unroll
+            for (int b = 0; b < NSUM; ++b) {
+                const u32x4 *p = reinterpret_cast<const u32x4 *>(vrow16 + b * a.sstride + (size_t)x * Dp + dbase);
+#pragma unroll
+                for (int i = 0; i < 2; ++i) {
+                    const u32x4 t = __builtin_nontemporal_load(&p[i]);
+                    v[2 * b + i] = make_uint4(t.x, t.y, t.z, t.w);
+                }
+            }
+            return;
+        }
         const u32x4 *p = reinterpret_cast<const u32x4 *>(vrow + (size_t)x * Dp + dbase);
 #pragma unroll
         for (int i = 0; i < NV; ++i) {
@@ -127,8 +144,32 @@ __global__ __launch_bounds__(kVolThreads) void vol_wta(VolArgs a) {
             v[i] = make_uint4(t.x, t.y, t.z, t.w);
         }
     };
-    auto process = [&](int xc0, const uint4(&cur)[NV]) __attribute__((always_inline)) {
+    auto process = [&](int xc0, const uint4(&raw)[RAWN]) __attribute__((always_inline)) {
         if (xc0 >= xb) return;
+        uint4 cur[NV];
+        if constexpr (NSUM > 0) {
+            // 16 u32 sums of the NSUM u16 slices (u16 pairs: low half = even disparity)
+            uint32_t sum[16];
+#pragma unroll
+            for (int j = 0; j < 16; ++j) sum[j] = 0;
+#pragma unroll
+            for (int b = 0; b < NSUM; ++b) {
+#pragma unroll
+                for (int i = 0; i < 2; ++i) {
+                    const uint32_t w[4] = {raw[2 * b + i].x, raw[2 * b + i].y, raw[2 * b + i].z, raw[2 * b + i].w};
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) {
+                        sum[8 * i + 2 * q] += w[q] & 0xFFFFu;
+                        sum[8 * i + 2 * q + 1] += w[q] >> 16;
+                    }
+                }
+            }
+#pragma unroll
+            for (int i = 0; i < 4; ++i) cur[i] = make_uint4(sum[4 * i], sum[4 * i + 1], sum[4 * i + 2], sum[4 * i + 3]);
+        } else {
+#pragma unroll
+            for (int i = 0; i < NV; ++i) cur[i] = raw[i];
+        }
         const int x = xc0 + k;
         const bool inb = x < xb;
         if (a.subpix) {
@@ -190,7 +231,7 @@ __global__ __launch_bounds__(kVolThreads) void vol_wta(VolArgs a) {
         if (a.subpix) __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront", "local");  // reads before next writes
     };
     // RING-deep register ring: RING-1 chunks in flight while one is reduced
-    uint4 rb[RING][NV];
+    uint4 rb[RING][RAWN];
 #pragma unroll
     for (int i = 0; i < RING - 1; ++i) {
         load(xa + i * XC, rb[i]);
@@ -291,13 +332,13 @@ size_t volume_smem_bytes(int TX, bool ssd, int Dp, int TPP, int W) {
     return vol_smem(ssd, W, W, true, true);  // the largest form (one segment per row, LR, float_mode 1)
 }
 
-template <bool SSD, bool UNIQ, bool LR, int RING>
+template <bool SSD, bool UNIQ, bool LR, int RING, int NSUM = 0>
 static hipError_t launch_vol_ring(const VolArgs &a, hipStream_t st) {
     static bool attr_done[64] = {};
     int dev = 0;
     (void)hipGetDevice(&dev);
     if (dev < 0 || dev >= 64 || !attr_done[dev]) {
-        hipError_t e = hipFuncSetAttribute((const void *)vol_wta<SSD, UNIQ, LR, RING>,
+        hipError_t e = hipFuncSetAttribute((const void *)vol_wta<SSD, UNIQ, LR, RING, NSUM>,
                                            hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         if (e != hipSuccess) return e;
         if (dev >= 0 && dev < 64) attr_done[dev] = true;
@@ -312,7 +353,7 @@ static hipError_t launch_vol_ring(const VolArgs &a, hipStream_t st) {
     const int XC = kVolThreads / (a.Dp / 16);
     const int XSg = ((a.W + nseg - 1) / nseg + XC - 1) / XC * XC;  // as the kernel computes it
     const size_t smem = vol_smem(SSD, std::min(XSg, a.W), a.W, LR, a.float_mode == 1);
-    hipLaunchKernelGGL((vol_wta<SSD, UNIQ, LR, RING>), dim3(a.H, nseg), dim3(kVolThreads), smem, st, a);
+    hipLaunchKernelGGL((vol_wta<SSD, UNIQ, LR, RING, NSUM>), dim3(a.H, nseg), dim3(kVolThreads), smem, st, a);
     return hipGetLastError();
 }
 
@@ -328,8 +369,26 @@ static hipError_t launch_vol_cost(const VolArgs &a, hipStream_t st) {
     return l ? launch_vol_one<SSD, false, true>(a, st) : launch_vol_one<SSD, false, false>(a, st);
 }
 
+// summed SGM volumes: ring depth 3 up to 4 directions, 2 beyond (register budget of 2 x 16 B per
+// direction per chunk in flight)
+template <int N>
+static hipError_t launch_vol_sum(const VolArgs &a, hipStream_t st) {
+    constexpr int RING = N <= 4 ? 3 : 2;
+    const bool u = a.uniq > 0, l = a.lr >= 0;
+    if (u) return l ? launch_vol_ring<true, true, true, RING, N>(a, st) : launch_vol_ring<true, true, false, RING, N>(a, st);
+    return l ? launch_vol_ring<true, false, true, RING, N>(a, st) : launch_vol_ring<true, false, false, RING, N>(a, st);
+}
+
 hipError_t launch_volume_wta(int TX, bool ssd, const VolArgs &a, hipStream_t st) {
     (void)TX;  // slices are 32 disparities (Dp is a multiple of 64)
+    switch (a.nsum) {
+        case 0: break;
+        case 3: return launch_vol_sum<3>(a, st);
+        case 4: return launch_vol_sum<4>(a, st);
+        case 5: return launch_vol_sum<5>(a, st);
+        case 8: return launch_vol_sum<8>(a, st);
+        default: return hipErrorInvalidValue;
+    }
     return ssd ? launch_vol_cost<true>(a, st) : launch_vol_cost<false>(a, st);
 }
 

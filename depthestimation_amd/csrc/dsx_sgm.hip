@@ -199,6 +199,117 @@ __global__ __launch_bounds__(256) void sgm_path(SgmArgs a) {
     }
 }
 
+// All paths of all directions in one launch (3 to 8 times the paths in flight of one direction:
+// each path is a sequential recurrence, so a single direction leaves most SIMDs waiting on memory).
+// Block b's 4 waves take global paths 4b..4b+3; direction i owns [poff[i], poff[i+1]).  Each path
+// writes L_r as u16 into its direction's buffer (no read-modify-write of a shared S).
+template <int NPL>
+__global__ __launch_bounds__(256) void sgm_paths_all(SgmAllArgs a) {
+    constexpr int RING = NPL == 2 ? 16 : 8;
+    typedef typename std::conditional<NPL == 2, uint32_t, uint2>::type LV;  // NPL u16
+    const int wv = threadIdx.x >> 6, ln = threadIdx.x & 63;
+    const int g = blockIdx.x * 4 + wv;
+    if (g >= a.poff[a.ndir]) return;  // wave-uniform; no block barriers below
+    int dir = 0;
+    while (dir + 1 < a.ndir && g >= a.poff[dir + 1]) ++dir;
+    const int path = g - a.poff[dir];
+    const int H = a.H, W = a.W, dx = a.dx[dir], dy = a.dy[dir];
+    int x, y;
+    if (dy == 0) {
+        x = dx > 0 ? 0 : W - 1;
+        y = path;
+    } else if (dx == 0 || path < W) {
+        x = path;
+        y = dy > 0 ? 0 : H - 1;
+    } else {
+        const int k = path - W + 1;
+        x = dx > 0 ? 0 : W - 1;
+        y = dy > 0 ? k : H - 1 - k;
+    }
+    const int nx = dx > 0 ? W - x : (dx < 0 ? x + 1 : 1 << 30);
+    const int ny = dy > 0 ? H - y : (dy < 0 ? y + 1 : 1 << 30);
+    const int n = nx < ny ? nx : ny;
+    const int d0 = ln * NPL;
+    const int Dp = a.Dp, D = a.D;
+    const uint32_t P1 = (uint32_t)a.P1, P2 = (uint32_t)a.P2;
+    const long step = ((long)dy * W + dx) * Dp;
+    const uint16_t *Cb = a.C + ((size_t)y * W + x) * Dp + d0;
+    uint16_t *Lb = a.L + (size_t)dir * a.lstride + ((size_t)y * W + x) * Dp + d0;
+    typedef typename CostVec<NPL>::C CVC;
+    CVC ca[RING], cb[RING];
+    auto load_chunk = [&](int k0, CVC(&cr)[RING]) __attribute__((always_inline)) {
+#pragma unroll
+        for (int i = 0; i < RING; ++i) {
+            const int kk = k0 + i < n ? k0 + i : n - 1;
+            cr[i] = *reinterpret_cast<const CVC *>(Cb + kk * step);
+        }
+    };
+    uint32_t Lp[NPL];
+    uint32_t mp = 0;
+    auto stepk = [&](const CVC &cv, int k) __attribute__((always_inline)) {
+        uint32_t c[NPL], L[NPL];
+        unpackC<NPL>(cv, c);
+        if (k == 0) {
+#pragma unroll
+            for (int j = 0; j < NPL; ++j) L[j] = d0 + j < D ? c[j] : kInf;
+        } else {
+            const uint32_t lo = (uint32_t)__builtin_amdgcn_update_dpp((int)kInf, (int)Lp[NPL - 1], 0x138, 0xF, 0xF, false);
+            const uint32_t hi = (uint32_t)__builtin_amdgcn_update_dpp((int)kInf, (int)Lp[0], 0x130, 0xF, 0xF, false);
+            const uint32_t jump = mp + P2;
+#pragma unroll
+            for (int j = 0; j < NPL; ++j) {
+                const uint32_t lm = j > 0 ? Lp[j - 1] : lo;
+                const uint32_t lh = j < NPL - 1 ? Lp[j + 1] : hi;
+                const uint32_t t = umin_(umin_(Lp[j], lm + P1), umin_(lh + P1, jump));
+                L[j] = d0 + j < D ? c[j] + t - mp : kInf;
+            }
+        }
+        uint32_t lmin = L[0];
+#pragma unroll
+        for (int j = 1; j < NPL; ++j) lmin = umin_(lmin, L[j]);
+        mp = wave_min(lmin);
+        uint32_t o[NPL];
+#pragma unroll
+        for (int j = 0; j < NPL; ++j) {
+            o[j] = d0 + j < D ? L[j] : 0xFFFFu;  // L <= C + P2 < 65535 (host check)
+            Lp[j] = L[j];
+        }
+        LV v;
+        if constexpr (NPL == 2) v = o[0] | (o[1] << 16);
+        else v = make_uint2(o[0] | (o[1] << 16), o[2] | (o[3] << 16));
+        *reinterpret_cast<LV *>(Lb + k * step) = v;
+    };
+    auto run_chunk = [&](int k0, const CVC(&cr)[RING]) __attribute__((always_inline)) {
+        sfor_sgm<0, RING>([&](auto Ic) __attribute__((always_inline)) {
+            constexpr int I = decltype(Ic)::value;
+            if (k0 + I < n) stepk(cr[I], k0 + I);
+        });
+    };
+    load_chunk(0, ca);
+    for (int k0 = 0; k0 < n; k0 += 2 * RING) {
+        __builtin_amdgcn_s_waitcnt(0);
+        if (k0 + RING < n) load_chunk(k0 + RING, cb);
+        run_chunk(k0, ca);
+        if (k0 + RING >= n) break;
+        __builtin_amdgcn_s_waitcnt(0);
+        if (k0 + 2 * RING < n) load_chunk(k0 + 2 * RING, ca);
+        run_chunk(k0 + RING, cb);
+    }
+}
+
+int sgm_num_paths_host(int H, int W, int dx, int dy) { return sgm_num_paths(H, W, dx, dy); }
+
+hipError_t launch_sgm_all(const SgmAllArgs &a, hipStream_t st) {
+    const int np = a.poff[a.ndir];
+    const dim3 grid((np + 3) / 4), block(256);
+    switch (a.Dp / 64) {
+        case 2: hipLaunchKernelGGL(sgm_paths_all<2>, grid, block, 0, st, a); break;
+        case 4: hipLaunchKernelGGL(sgm_paths_all<4>, grid, block, 0, st, a); break;
+        default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
 template <int NPL>
 static hipError_t launch_sgm_npl(const SgmArgs &a, bool first, hipStream_t st) {
     const int np = sgm_num_paths(a.H, a.W, a.dx, a.dy);

@@ -151,3 +151,22 @@ def test_gpu_sgm_golden_fixtures():
                             aggregation=str(z["mode"]))
         np.testing.assert_array_equal(m.compute(z["L"], z["R"]), z["fixed"], err_msg=os.path.basename(f))
         m.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode", ["sgbm_3way", "hh"])
+@pytest.mark.parametrize("bs,p1,p2", [(15, 0, 9000), (5, 50, 60000), (3, 7, 13)])
+def test_gpu_sgm_custom_penalties(mode, bs, p1, p2):
+    """Custom P1/P2: concurrent directions with u16 L_r while max cost + P2 < 65535 ((3, 7, 13)),
+    the sequential u32 accumulation beyond ((15, 0, 9000): 57,375 + 9,000; (5, 50, 60000))."""
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from depthestimation_amd.matcher import HipBlockMatcher
+    L, R, _ = stereo_pair(29, 96, 0, 32, seed=bs + p2)
+    kw = dict(min_disp=0, num_disp=32, block_size=bs, uniqueness_ratio=10, disp12_max_diff=1, subpixel=True)
+    ref = stereo_sgm(L, R, mode=mode, P1=p1 or None, P2=p2, **kw)
+    m = HipBlockMatcher(cost="sad", aggregation=mode, p1=p1, p2=p2, **kw)
+    got = m.compute(L, R)
+    m.close()
+    np.testing.assert_array_equal(got, ref["fixed"])
