@@ -321,7 +321,11 @@ __device__ __forceinline__ void bm2_segment(const Bm2Args &a, uint8_t *smem, int
     block_sync<NW>();
     {
         // groups of IG rows in flight: bounds the init phase's VGPRs below the main loop's
+#ifdef DSX_IG
+        constexpr int IG = DSX_IG;
+#else
         constexpr int IG = 3;
+#endif
 #pragma unroll 1
         for (int i0 = 0; i0 <= 2 * R; i0 += IG) {
             uint32_t iw[IG][5];
