@@ -317,7 +317,129 @@ __device__ __forceinline__ void bm2_segment(const Bm2Args &a, uint8_t *smem, int
         }
     };
 
-    // ---- segment init: rows yb-R .. yb+R staged in slots 0..2R (may overlap the tile) ----
+    // ---- segment init: column sums over rows yb-R .. yb+R ----
+    acc_t cs[NC];
+#pragma unroll
+    for (int c = 0; c < NC; ++c) cs[c] = acc_t(0);
+#ifndef DSX_SADINIT
+#define DSX_SADINIT 1
+#endif
+    // Measured per instantiation (r02, tools/si_ab.sh, same box): C1 (R=2) 20.5 -> 19.5 us, C4 (R=2)
+    // 57.3 -> 56.3 us, C5 (R=7) 610 -> 581 us; but the R=4 instantiation (C2) runs 72.9 -> 79.0 us
+    // with it - its row loop is scheduled worse (more full vmcnt drains), not its init - so R=4 keeps
+    // the row-by-row init.
+    constexpr bool SADINIT = DSX_SADINIT && R != 4;
+    if constexpr (!SSD && side != 1 && SADINIT) {
+        // SAD (left / volume passes): rows in groups of 4, bytes transposed so that one v_sad_u8
+        // sums a column's 4 row terms for one disparity: TP_g[j] = {P(j), P(j+1)} with P(j) the
+        // group's 4 search bytes at position pos(j) (one per row), R_g[c] the 4 reference bytes
+        // of column c.  Per column 2 v_sad_u8 per group instead of 2 absolute differences and an
+        // add per row (C2 init 115 -> ~30 issue cycles per column).  Rows past 2R are zero in
+        // both, so they add nothing.
+        constexpr int NGR = (2 * R + 1 + 3) / 4;  // row groups
+        constexpr int TPG = rnd16(NJ4 * 32);   // pair entries of a group (8 B each)
+        constexpr int RG = rnd16(NC4 * 16);     // reference dwords of a group
+        static_assert(NGR * (TPG + RG) <= G::SMEM, "transposed init rows must fit the block's LDS");
+        block_sync<NW>();
+        // byte loader in the FAST layout for both paths: w = bytes of entries 3, 2, 1, 0 (byte k =
+        // entry 3 - k: positions PB - 4 tj - 3 .. PB - 4 tj), e = entry 4, rf = 4 reference bytes
+        auto ldb = [&](int r, uint32_t &w, uint32_t &e, uint32_t &rf) __attribute__((always_inline)) {
+            const int yy = clampi2(r, 0, H - 1);
+            const uint8_t *srow = a.src + fin + (long)yy * stride;
+            const uint8_t *rrow = a.ref + fin + (long)yy * stride;
+            const int tj = min(tid, NJ4 - 1), tr = min(tid, NC4 - 1);
+            if constexpr (FAST) {
+                const uint8_t *pp = srow + PB - 4 * tj - 3;
+                w = *reinterpret_cast<const uint32_t *>(pp);
+                e = pp[-1];
+                rf = *reinterpret_cast<const uint32_t *>(rrow + x0 - R + 4 * tr);
+            } else {
+                uint32_t v = 0;
+#pragma unroll
+                for (int q = 0; q < 4; ++q) v |= (uint32_t)srow[clampi2(PB - 4 * tj - q, 0, W - 1)] << (8 * (3 - q));
+                w = v;
+                e = srow[clampi2(PB - 4 * tj - 4, 0, W - 1)];
+                v = 0;
+#pragma unroll
+                for (int q = 0; q < 4; ++q) v |= (uint32_t)rrow[clampi2(x0 - R + 4 * tr + q, 0, W - 1)] << (8 * q);
+                rf = v;
+            }
+        };
+#pragma unroll 1
+        for (int g = 0; g < NGR; ++g) {
+            uint32_t w[4], e[4], rf[4];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                if (4 * g + r <= 2 * R) {
+                    ldb(yb - R + 4 * g + r, w[r], e[r], rf[r]);
+                } else {
+                    w[r] = 0;
+                    e[r] = 0;
+                    rf[r] = 0;
+                }
+            }
+            // P(entry q) = {w0.byte(3-q), w1.byte(3-q), w2.byte(3-q), w3.byte(3-q)}, q = 0..3
+            uint32_t P[5];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const uint32_t b = 3 - q;
+                const uint32_t lo = __builtin_amdgcn_perm(w[1], w[0], 0x0C0C0000u | ((4u + b) << 8) | b);
+                const uint32_t hi = __builtin_amdgcn_perm(w[3], w[2], 0x0C0C0000u | ((4u + b) << 8) | b);
+                P[q] = __builtin_amdgcn_perm(hi, lo, 0x05040100u);
+            }
+            {
+                const uint32_t lo = __builtin_amdgcn_perm(e[1], e[0], 0x0C0C0400u);
+                const uint32_t hi = __builtin_amdgcn_perm(e[3], e[2], 0x0C0C0400u);
+                P[4] = __builtin_amdgcn_perm(hi, lo, 0x05040100u);
+            }
+            if (tid < NJ4) {
+                uint4 *tp = reinterpret_cast<uint4 *>(smem + g * TPG + 32 * tid);
+                tp[0] = make_uint4(P[0], P[1], P[1], P[2]);
+                tp[1] = make_uint4(P[2], P[3], P[3], P[4]);
+            }
+            // R(column 4 tr + k) = {rf0.byte(k), rf1.byte(k), rf2.byte(k), rf3.byte(k)}
+            if (tid < NC4) {
+                uint32_t Rv[4];
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    const uint32_t lo = __builtin_amdgcn_perm(rf[1], rf[0], 0x0C0C0000u | ((4u + k) << 8) | (uint32_t)k);
+                    const uint32_t hi = __builtin_amdgcn_perm(rf[3], rf[2], 0x0C0C0000u | ((4u + k) << 8) | (uint32_t)k);
+                    Rv[k] = __builtin_amdgcn_perm(hi, lo, 0x05040100u);
+                }
+                *reinterpret_cast<uint4 *>(smem + NGR * TPG + g * RG + 16 * tid) = make_uint4(Rv[0], Rv[1], Rv[2], Rv[3]);
+            }
+        }
+        block_sync<NW>();
+        // this lane's pair entry for column c: TP_g[d0 + NC - 1 - c] (8-B aligned); groups in a
+        // runtime loop, columns unrolled (a full unroll of both hoists every LDS read and spills)
+        const uint8_t *tb = smem + d0 * 8;
+        {
+        uint32_t ae[NC], ao[NC];
+#pragma unroll
+        for (int c = 0; c < NC; ++c) ae[c] = ao[c] = 0;
+#pragma unroll 1
+        for (int g = 0; g < NGR; ++g) {
+#pragma unroll
+            for (int q = 0; q < NC4; ++q) {
+                const int c0 = 4 * q;
+                const uint4 rr = *reinterpret_cast<const uint4 *>(smem + NGR * TPG + g * RG + 4 * c0);  // broadcast
+                const uint32_t rv[4] = {rr.x, rr.y, rr.z, rr.w};
+#pragma unroll
+                for (int c = 0; c < 4; ++c) {
+                    if (c0 + c < NC) {
+                        const uint2 pr = *reinterpret_cast<const uint2 *>(tb + g * TPG + (NC - 1 - c0 - c) * 8);
+                        ae[c0 + c] = __builtin_amdgcn_sad_u8(rv[c], pr.x, ae[c0 + c]);
+                        ao[c0 + c] = __builtin_amdgcn_sad_u8(rv[c], pr.y, ao[c0 + c]);
+                    }
+                }
+            }
+        }
+#pragma unroll
+        for (int c = 0; c < NC; ++c) cs[c] = as2(ae[c] | (ao[c] << 16));  // <= 255 (2R+1) < 2^16
+        }
+
+    } else {
+    // rows yb-R .. yb+R staged in slots 0..2R (may overlap the tile)
     block_sync<NW>();
     {
         // groups of IG rows in flight: bounds the init phase's VGPRs below the main loop's
@@ -338,9 +460,6 @@ __device__ __forceinline__ void bm2_segment(const Bm2Args &a, uint8_t *smem, int
         }
     }
     block_sync<NW>();
-    acc_t cs[NC];
-#pragma unroll
-    for (int c = 0; c < NC; ++c) cs[c] = acc_t(0);
 #pragma unroll 1
     for (int i = 0; i <= 2 * R; ++i) {  // runtime loop: a full unroll makes compile time explode
 #pragma unroll
@@ -367,6 +486,7 @@ __device__ __forceinline__ void bm2_segment(const Bm2Args &a, uint8_t *smem, int
                 }
             }
         }
+    }
     }
     block_sync<NW>();  // init rows (which overlap the tile) are consumed
 
