@@ -10,9 +10,12 @@
 //   value  = sum w v / sum w over earlier-layer pixels q with 0 < |p-q|^2 <= r^2 (offset order),
 //            w = max(|(p-q).gradT| / |p-q| / |p-q|^2 / (1 + |T(q) - T(p)|), 1e-6).
 // One launch per layer: a layer only reads pixels whose layer is < k, which no thread of that
-// launch writes (a pixel being filled goes from "unfilled" straight to k), so a launch is race-free
-// and the kernel boundary orders the layers.  Layers run in batches with one host read-back of the
-// last layer's frontier size per batch; the loop ends at the first empty frontier.
+// launch writes (a pixel being filled goes from "queued" straight to k), so a launch is race-free
+// and the kernel boundary orders the layers.  The frontiers are explicit lists: layer k's launch
+// walks list k and queues the still-untouched hole 4-neighbours of the pixels it fills (one CAS
+// unfilled -> queued each, so a pixel is listed once) as list k+1 - exactly layer k+1.  Layers run
+// in batches with one host read-back of the next frontier's size per batch; the loop ends at the
+// first empty frontier.
 #include "dsx_internal.h"
 
 #include <algorithm>
@@ -24,7 +27,8 @@ namespace dsx {
 
 namespace {
 
-constexpr int kUnfilled = 0x7FFFFFFF;
+constexpr int kUnfilled = 0x7FFFFFFF;  // hole pixel not yet in any frontier list
+constexpr int kQueued = 0x7FFFFFFE;    // listed for the next layer (still >= every layer index)
 
 __device__ __forceinline__ double telea_solve(double t1, double t2) {
     if (t1 < 1e6 && t2 < 1e6) {
@@ -38,71 +42,237 @@ __device__ __forceinline__ double telea_solve(double t1, double t2) {
     return 1.0 + (t1 < t2 ? t1 : t2);
 }
 
-__global__ __launch_bounds__(256) void inpaint_init(const float *in, int64_t pitch, int H, int W, float *out, int *layer,
-                                                    double *T) {
-    const int64_t n = (int64_t)H * W;
-    for (int64_t p = (int64_t)blockIdx.x * 256 + threadIdx.x; p < n; p += (int64_t)gridDim.x * 256) {
-        const int y = (int)(p / W), x = (int)(p - (int64_t)y * W);
-        const float v = in[(int64_t)y * pitch + x];
-        const bool hole = v <= 0.0f;  // fill_holes' mask = disparity <= 0 (postprocess.py:96-97)
-        out[p] = v;
-        layer[p] = hole ? kUnfilled : 0;
-        T[p] = hole ? 1e6 : 0.0;
-    }
+__device__ __forceinline__ uint64_t lanes_below(int lane) { return (1ull << lane) - 1ull; }
+
+// A block's slice of the next frontier list, gathered in LDS and appended with one global atomic
+// per flush: a wave-per-atomic append serialises on the one counter when a frontier is tens of
+// thousands of pixels (the first layers of a map with scattered holes).
+template <int CAP>
+struct BlockQueue {
+    int buf[CAP];
+    int n, base;
+};
+
+// Adds the lanes with `want` set (one LDS atomic per wave).  Called by the whole wave.
+template <int CAP>
+__device__ __forceinline__ void bq_push(BlockQueue<CAP> &bq, bool want, int value) {
+    const int lane = threadIdx.x & 63;
+    const uint64_t m = __ballot(want);
+    if (!m) return;
+    int at = 0;
+    if (lane == 0) at = atomicAdd(&bq.n, __popcll(m));
+    at = __shfl(at, 0);
+    if (want) bq.buf[at + __popcll(m & lanes_below(lane))] = value;
 }
 
-__global__ __launch_bounds__(256) void inpaint_layer(float *out, int *layer, double *T, int H, int W, int radius, int k,
-                                                     int *front) {
-    __shared__ int bcount;
-    if (threadIdx.x == 0) bcount = 0;
+// Moves the gathered entries to list (slots from *cnt).  Called by the whole block; leaves n = 0.
+template <int CAP>
+__device__ __forceinline__ void bq_flush(BlockQueue<CAP> &bq, int *list, int *cnt) {
     __syncthreads();
-    const int64_t n = (int64_t)H * W;
-    int mine = 0;
-    for (int64_t p = (int64_t)blockIdx.x * 256 + threadIdx.x; p < n; p += (int64_t)gridDim.x * 256) {
-        if (layer[p] != kUnfilled) continue;
-        const int y = (int)(p / W), x = (int)(p - (int64_t)y * W);
-        const bool nu = y > 0 && layer[p - W] == k - 1, nd = y < H - 1 && layer[p + W] == k - 1;
-        const bool nl = x > 0 && layer[p - 1] == k - 1, nr = x < W - 1 && layer[p + 1] == k - 1;
-        if (!(nu || nd || nl || nr)) continue;
-        // earlier-layer neighbours (layer < k) and their T (1e6 when absent)
-        const bool ou = y > 0 && layer[p - W] < k, od = y < H - 1 && layer[p + W] < k;
-        const bool ol = x > 0 && layer[p - 1] < k, orr = x < W - 1 && layer[p + 1] < k;
-        const double tu = ou ? T[p - W] : 1e6, td = od ? T[p + W] : 1e6;
-        const double tl = ol ? T[p - 1] : 1e6, tr = orr ? T[p + 1] : 1e6;
-        const double a0 = telea_solve(tu, tl), a1 = telea_solve(td, tl);
-        const double a2 = telea_solve(tu, tr), a3 = telea_solve(td, tr);
-        const double m01 = a0 < a1 ? a0 : a1, m23 = a2 < a3 ? a2 : a3;
-        const double tp = m01 < m23 ? m01 : m23;
-        const double gx = (orr && ol) ? (tr - tl) * 0.5 : (orr ? tr - tp : (ol ? tp - tl : 0.0));
-        const double gy = (od && ou) ? (td - tu) * 0.5 : (od ? td - tp : (ou ? tp - tu : 0.0));
-        double num = 0.0, den = 0.0;
-        for (int oy = -radius; oy <= radius; ++oy) {
-            const int qy = y + oy;
-            for (int ox = -radius; ox <= radius; ++ox) {
-                const int d2 = oy * oy + ox * ox;
-                if (d2 == 0 || d2 > radius * radius) continue;
-                const int qx = x + ox;
-                if (qy < 0 || qy >= H || qx < 0 || qx >= W) continue;
-                const int64_t q = (int64_t)qy * W + qx;
-                if (layer[q] >= k) continue;
-                const double ry = (double)(-oy), rx = (double)(-ox);
-                const double w_dir = __builtin_fabs(ry * gy + rx * gx) / __builtin_sqrt((double)d2);
-                const double w_dst = 1.0 / (double)d2;
-                const double w_lev = 1.0 / (1.0 + __builtin_fabs(T[q] - tp));
-                double w = w_dir * w_dst * w_lev;
-                w = w > 1e-6 ? w : 1e-6;
-                num = num + w * (double)out[q];
-                den = den + w;
-            }
-        }
-        if (den > 0) out[p] = (float)(num / den);
-        T[p] = tp;
-        layer[p] = k;
-        ++mine;
+    const int n = bq.n;
+    if (n) {
+        if (threadIdx.x == 0) bq.base = atomicAdd(cnt, n);
+        __syncthreads();
+        const int base = bq.base;
+        for (int j = threadIdx.x; j < n; j += blockDim.x) list[base + j] = bq.buf[j];
+        __syncthreads();
+        if (threadIdx.x == 0) bq.n = 0;
     }
-    if (mine) atomicAdd(&bcount, mine);
     __syncthreads();
-    if (threadIdx.x == 0 && bcount) atomicAdd(front, bcount);
+}
+
+// Copies the map, sets layer 0 / unfilled / T, and lists layer 1: the holes with a known 4-neighbour.
+// Each block covers kInitChunk consecutive pixels and appends its layer-1 pixels with one atomic.
+constexpr int kInitChunk = 4096;
+
+__global__ __launch_bounds__(256) void inpaint_init(const float *in, int64_t pitch, int H, int W, float *out, int *layer,
+                                                    double *T, int *list1, int *cnt1) {
+    __shared__ BlockQueue<kInitChunk> bq;
+    if (threadIdx.x == 0) bq.n = 0;
+    __syncthreads();
+    const int n = H * W;  // < 2^31 (host check)
+    const int c0 = blockIdx.x * kInitChunk;
+    for (int p = c0 + (int)threadIdx.x; p < c0 + kInitChunk; p += 256) {  // block-uniform trip count
+        bool first = false;
+        if (p < n) {
+            const int y = p / W, x = p - y * W;
+            const float *row = in + (int64_t)y * pitch;
+            const float v = row[x];
+            const bool hole = v <= 0.0f;  // fill_holes' mask = disparity <= 0 (postprocess.py:96-97)
+            if (hole)
+                first = (x > 0 && row[x - 1] > 0.0f) || (x < W - 1 && row[x + 1] > 0.0f) ||
+                        (y > 0 && row[x - pitch] > 0.0f) || (y < H - 1 && row[x + pitch] > 0.0f);
+            out[p] = v;
+            layer[p] = hole ? (first ? kQueued : kUnfilled) : 0;
+            T[p] = hole ? 1e6 : 0.0;
+        }
+        bq_push(bq, first, p);
+    }
+    bq_flush(bq, list1, cnt1);
+}
+
+struct Front {
+    double tp, gx, gy;
+    int lay[4];  // the 4-neighbours' layers (up, down, left, right; kQueued when outside the map)
+};
+
+// T and grad T of a frontier pixel p (layer k) from its earlier-layer 4-neighbours (T 1e6 when
+// absent).  The neighbours' layers and T load together (one memory round trip).
+__device__ __forceinline__ Front front_of(const int *layer, const double *T, int p, int y, int x, int H, int W, int k) {
+    Front f;
+    const bool iu = y > 0, id = y < H - 1, il = x > 0, ir = x < W - 1;
+    f.lay[0] = iu ? layer[p - W] : kQueued;
+    f.lay[1] = id ? layer[p + W] : kQueued;
+    f.lay[2] = il ? layer[p - 1] : kQueued;
+    f.lay[3] = ir ? layer[p + 1] : kQueued;
+    const double Tu = iu ? T[p - W] : 1e6, Td = id ? T[p + W] : 1e6;
+    const double Tl = il ? T[p - 1] : 1e6, Tr = ir ? T[p + 1] : 1e6;
+    const bool ou = f.lay[0] < k, od = f.lay[1] < k, ol = f.lay[2] < k, orr = f.lay[3] < k;
+    const double tu = ou ? Tu : 1e6, td = od ? Td : 1e6, tl = ol ? Tl : 1e6, tr = orr ? Tr : 1e6;
+    const double a0 = telea_solve(tu, tl), a1 = telea_solve(td, tl);
+    const double a2 = telea_solve(tu, tr), a3 = telea_solve(td, tr);
+    const double m01 = a0 < a1 ? a0 : a1, m23 = a2 < a3 ? a2 : a3;
+    f.tp = m01 < m23 ? m01 : m23;
+    f.gx = (orr && ol) ? (tr - tl) * 0.5 : (orr ? tr - f.tp : (ol ? f.tp - tl : 0.0));
+    f.gy = (od && ou) ? (td - tu) * 0.5 : (od ? td - f.tp : (ou ? f.tp - tu : 0.0));
+    return f;
+}
+
+// Weight of the window cell (oy, ox) for the pixel (y, x); false when the cell is outside the disc,
+// the image or the earlier layers.  The cell's layer, T and value load together.
+__device__ __forceinline__ bool cell_term(const float *out, const int *layer, const double *T, int y, int x, int oy,
+                                          int ox, int H, int W, int r2, int k, const Front &f, double &w, double &wv) {
+    const int d2 = oy * oy + ox * ox;
+    const int qy = y + oy, qx = x + ox;
+    if (d2 == 0 || d2 > r2 || qy < 0 || qy >= H || qx < 0 || qx >= W) return false;
+    const int64_t q = (int64_t)qy * W + qx;
+    const int lq = layer[q];
+    const double tq = T[q];
+    const float vq = out[q];
+    if (lq >= k) return false;
+    const double ry = (double)(-oy), rx = (double)(-ox);
+    const double w_dir = __builtin_fabs(ry * f.gy + rx * f.gx) / __builtin_sqrt((double)d2);
+    const double w_dst = 1.0 / (double)d2;
+    const double w_lev = 1.0 / (1.0 + __builtin_fabs(tq - f.tp));
+    w = w_dir * w_dst * w_lev;
+    w = w > 1e-6 ? w : 1e-6;
+    wv = w * (double)vq;
+    return true;
+}
+
+// Claims 4-neighbour `dir` (0..3 = up, down, left, right) of a pixel just filled for layer k+1:
+// only a neighbour that was still unfilled when the pixel's step read it can be, and the CAS makes
+// one claimant win.
+__device__ __forceinline__ bool claim_neighbour(int *layer, const Front &f, int p, int W, int dir, int &q) {
+    q = dir == 0 ? p - W : dir == 1 ? p + W : dir == 2 ? p - 1 : p + 1;
+    return f.lay[dir] == kUnfilled && atomicCAS(&layer[q], kUnfilled, kQueued) == kUnfilled;
+}
+
+constexpr int kQueueCap = 2048;  // per-block next-frontier entries between flushes
+
+// One frontier pixel per half-wave (radius <= 7): its 32 lanes evaluate the window cells (row-major
+// cell c on lane c mod 32 in pass c / 32: the divisions, square roots and neighbour loads run in
+// parallel), then every lane accumulates the terms in cell order through shuffles - the operation
+// sequence of the host restatement's loop, so the result keeps its bits.  (One pixel per thread left
+// a layer of a few thousand frontier pixels to a few dozen waves walking 28 dependent
+// double-precision terms each: ~30 us per layer at C4.)  Lanes 0-3 then claim the 4 neighbours.
+template <int NPASS>
+__global__ __launch_bounds__(256) void inpaint_layer_hw(float *out, int *layer, double *T, int H, int W, int radius,
+                                                        int k, const int *list, const int *cnt, int *nlist, int *ncnt) {
+    const int count = *cnt;
+    if ((int)blockIdx.x * 8 >= count) return;  // block-uniform
+    __shared__ BlockQueue<kQueueCap> bq;
+    if (threadIdx.x == 0) bq.n = 0;
+    __syncthreads();
+    const int hl = threadIdx.x & 31;  // lane within the half-wave
+    const int r2 = radius * radius, side = 2 * radius + 1, ncell = side * side;
+    for (int b0 = blockIdx.x * 8; b0 < count; b0 += gridDim.x * 8) {  // block-uniform trip count
+        const int i = b0 + ((int)threadIdx.x >> 5);
+        const bool valid = i < count;
+        const int p = valid ? list[i] : 0;
+        const int y = p / W, x = p - y * W;
+        bool want = false;
+        int q = 0;
+        if (valid) {
+            const Front f = front_of(layer, T, p, y, x, H, W, k);
+            double wt[NPASS], wv[NPASS];
+#pragma unroll
+            for (int ps = 0; ps < NPASS; ++ps) {
+                const int c = ps * 32 + hl;
+                wt[ps] = 0.0;  // w >= 1e-6 on every used cell: 0 marks the unused ones
+                wv[ps] = 0.0;
+                if (c < ncell)
+                    cell_term(out, layer, T, y, x, c / side - radius, c % side - radius, H, W, r2, k, f, wt[ps], wv[ps]);
+            }
+            double num = 0.0, den = 0.0;
+#pragma unroll
+            for (int ps = 0; ps < NPASS; ++ps) {
+                const int nc = ncell - ps * 32 < 32 ? ncell - ps * 32 : 32;
+                for (int s = 0; s < nc; ++s) {
+                    const double w = __shfl(wt[ps], s, 32), v = __shfl(wv[ps], s, 32);
+                    if (w != 0.0) {
+                        num = num + v;
+                        den = den + w;
+                    }
+                }
+            }
+            if (hl == 0) {
+                if (den > 0) out[p] = (float)(num / den);
+                T[p] = f.tp;
+                layer[p] = k;
+            }
+            if (hl < 4) want = claim_neighbour(layer, f, p, W, hl, q);
+        }
+        bq_push(bq, want, q);
+        __syncthreads();
+        const int held = bq.n;
+        __syncthreads();  // every thread has read it before the next pushes
+        if (held > kQueueCap - 32) bq_flush(bq, nlist, ncnt);
+    }
+    bq_flush(bq, nlist, ncnt);
+}
+
+// Larger windows: one pixel per thread, cells walked in order.
+__global__ __launch_bounds__(256) void inpaint_layer_px(float *out, int *layer, double *T, int H, int W, int radius,
+                                                        int k, const int *list, const int *cnt, int *nlist, int *ncnt) {
+    const int count = *cnt;
+    if ((int)blockIdx.x * 256 >= count) return;
+    __shared__ BlockQueue<kQueueCap> bq;
+    if (threadIdx.x == 0) bq.n = 0;
+    __syncthreads();
+    const int r2 = radius * radius;
+    for (int b0 = blockIdx.x * 256; b0 < count; b0 += gridDim.x * 256) {
+        const int i = b0 + (int)threadIdx.x;
+        const bool valid = i < count;
+        const int p = valid ? list[i] : 0;
+        const int y = p / W, x = p - y * W;
+        Front f;
+        if (valid) {
+            f = front_of(layer, T, p, y, x, H, W, k);
+            double num = 0.0, den = 0.0;
+            for (int oy = -radius; oy <= radius; ++oy)
+                for (int ox = -radius; ox <= radius; ++ox) {
+                    double w, wv;
+                    if (cell_term(out, layer, T, y, x, oy, ox, H, W, r2, k, f, w, wv)) {
+                        num = num + wv;
+                        den = den + w;
+                    }
+                }
+            if (den > 0) out[p] = (float)(num / den);
+            T[p] = f.tp;
+            layer[p] = k;
+        }
+        for (int dir = 0; dir < 4; ++dir) {
+            int q = 0;
+            const bool want = valid && claim_neighbour(layer, f, p, W, dir, q);
+            bq_push(bq, want, q);
+        }
+        __syncthreads();
+        const int held = bq.n;
+        __syncthreads();
+        if (held > kQueueCap - 1024) bq_flush(bq, nlist, ncnt);
+    }
+    bq_flush(bq, nlist, ncnt);
 }
 
 size_t align256(size_t b) { return (b + 255) & ~(size_t)255; }
@@ -111,7 +281,8 @@ size_t align256(size_t b) { return (b + 255) & ~(size_t)255; }
 
 size_t inpaint_workspace(int H, int W) {
     const size_t n = (size_t)H * W;
-    return align256(n * 4) + align256(n * 8) + align256((size_t)(H + W + 2) * 4);
+    // layer | T | 2 frontier lists (ping-pong) | per-layer frontier sizes
+    return align256(n * 4) + align256(n * 8) + 2 * align256(n * 4) + align256((size_t)(H + W + 3) * 4);
 }
 
 hipError_t launch_inpaint(const float *in, int64_t pitch, int H, int W, int radius, float *out, void *ws, hipStream_t st) {
@@ -119,25 +290,34 @@ hipError_t launch_inpaint(const float *in, int64_t pitch, int H, int W, int radi
     uint8_t *w = static_cast<uint8_t *>(ws);
     int *layer = reinterpret_cast<int *>(w);
     double *T = reinterpret_cast<double *>(w + align256(n * 4));
-    int *front = reinterpret_cast<int *>(w + align256(n * 4) + align256(n * 8));
+    int *lists[2] = {reinterpret_cast<int *>(w + align256(n * 4) + align256(n * 8)),
+                     reinterpret_cast<int *>(w + align256(n * 4) + align256(n * 8) + align256(n * 4))};
+    int *cnt = reinterpret_cast<int *>(w + align256(n * 4) + align256(n * 8) + 2 * align256(n * 4));
     const int maxk = H + W + 1;  // no 4-connected distance exceeds H + W
-    const int grid = (int)std::min<size_t>((n + 255) / 256, 2048);
-    hipError_t e = hipMemsetAsync(front, 0, (size_t)(maxk + 1) * 4, st);
+    const int grid = (int)((n + kInitChunk - 1) / kInitChunk);
+    hipError_t e = hipMemsetAsync(cnt, 0, (size_t)(maxk + 2) * 4, st);  // cnt[k] = size of layer k
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(inpaint_init, dim3(grid), dim3(256), 0, st, in, pitch, H, W, out, layer, T);
+    hipLaunchKernelGGL(inpaint_init, dim3(grid), dim3(256), 0, st, in, pitch, H, W, out, layer, T, lists[1], cnt + 1);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     if (radius < 1) return hipSuccess;  // no neighbourhood: nothing changes (cv2 uses radius >= 1)
+    // a fixed grid strides over each frontier's device-side size (8 half-waves or 256 threads a
+    // block; the blocks past it return at once); batches of 8 layers between read-backs of the next frontier's size
     constexpr int kBatch = 8;
+    const bool hw = radius <= 7;
+    const int lgrid = (int)std::min<size_t>(hw ? (n + 7) / 8 : (n + 255) / 256, 2048);
+    auto lay = radius <= 3 ? inpaint_layer_hw<2> : radius <= 5 ? inpaint_layer_hw<4> : hw ? inpaint_layer_hw<8>
+                                                                                          : inpaint_layer_px;
     for (int k0 = 1; k0 <= maxk; k0 += kBatch) {
         const int k1 = std::min(maxk, k0 + kBatch - 1);
         for (int k = k0; k <= k1; ++k) {
-            hipLaunchKernelGGL(inpaint_layer, dim3(grid), dim3(256), 0, st, out, layer, T, H, W, radius, k, front + k);
+            hipLaunchKernelGGL(lay, dim3(lgrid), dim3(256), 0, st, out, layer, T, H, W, radius, k, lists[k & 1], cnt + k,
+                               lists[(k + 1) & 1], cnt + k + 1);
             if ((e = hipGetLastError()) != hipSuccess) return e;
         }
-        int last = 0;
-        if ((e = hipMemcpyAsync(&last, front + k1, 4, hipMemcpyDeviceToHost, st)) != hipSuccess) return e;
+        int next = 0;
+        if ((e = hipMemcpyAsync(&next, cnt + k1 + 1, 4, hipMemcpyDeviceToHost, st)) != hipSuccess) return e;
         if ((e = hipStreamSynchronize(st)) != hipSuccess) return e;
-        if (last == 0) break;
+        if (next == 0) break;
     }
     return hipSuccess;
 }
