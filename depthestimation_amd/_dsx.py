@@ -20,7 +20,7 @@ DSX_EHIP = -2
 DSX_ECOMM = -3
 DSX_ENOMEM = -4
 
-COST = {"sad": 0, "ssd": 1}
+COST = {"sad": 0, "ssd": 1, "bt": 2}  # include/dsx.h DSX_COST_*
 FLOAT_MODE = {"fixed": 0, "parabola": 1}
 PATH = {"fused": 0, "volume": 1}
 # SGM path sets by the reference's sgbm_mode names (stereo_core.py:55-61), include/dsx.h DSX_AGG_*
@@ -54,7 +54,8 @@ class DsxParams(ctypes.Structure):
         ("aggregation", ctypes.c_int32),
         ("p1", ctypes.c_int32),
         ("p2", ctypes.c_int32),
-        ("reserved", ctypes.c_int32 * 2),
+        ("prefilter_cap", ctypes.c_int32),
+        ("reserved", ctypes.c_int32 * 1),
     ]
 
 
@@ -152,7 +153,7 @@ def default_params() -> DsxParams:
 
 def make_params(min_disp=0, num_disp=128, block_size=5, cost="sad", uniqueness_ratio=10,
                 disp12_max_diff=1, subpixel=True, float_mode="fixed", path="fused",
-                timing=False, grid_blocks=0, aggregation=None, p1=0, p2=0) -> DsxParams:
+                timing=False, grid_blocks=0, aggregation=None, p1=0, p2=0, prefilter_cap=31) -> DsxParams:
     p = default_params()
     p.min_disp = int(min_disp)
     p.num_disp = int(num_disp)
@@ -176,6 +177,7 @@ def make_params(min_disp=0, num_disp=128, block_size=5, cost="sad", uniqueness_r
     p.aggregation = AGGREGATION[aggregation]
     p.p1 = int(p1)
     p.p2 = int(p2)
+    p.prefilter_cap = int(prefilter_cap)
     return p
 
 

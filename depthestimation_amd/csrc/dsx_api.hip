@@ -63,8 +63,11 @@ int sgm_set(int mode, const int **set) {
     }
 }
 
+int bt_ftzero(const dsx_params &p) { return (p.prefilter_cap > 15 ? p.prefilter_cap : 15) | 1; }
+
 uint64_t max_cost(const dsx_params &p) {
     const uint64_t n = (uint64_t)p.block_size * p.block_size;
+    if (p.cost == DSX_COST_BT) return n * (uint64_t)(2 * bt_ftzero(p) + 63);  // oracle/bt_cost.py max_cost_bt
     return n * (p.cost == DSX_COST_SSD ? 255ull * 255ull : 255ull);
 }
 
@@ -73,7 +76,10 @@ int check(const dsx_params *p) {
     if (p->block_size < 1 || p->block_size > 15 || (p->block_size & 1) == 0)
         return fail(DSX_EINVAL, "block_size must be odd and in [1, 15]");
     if (p->num_disp < 1 || p->num_disp > 512) return fail(DSX_EINVAL, "num_disp must be in [1, 512]");
-    if (p->cost != DSX_COST_SAD && p->cost != DSX_COST_SSD) return fail(DSX_EINVAL, "cost must be SAD (0) or SSD (1)");
+    if (p->cost != DSX_COST_SAD && p->cost != DSX_COST_SSD && p->cost != DSX_COST_BT)
+        return fail(DSX_EINVAL, "cost must be SAD (0), SSD (1) or BT (2)");
+    if (p->cost == DSX_COST_BT && (p->prefilter_cap < 1 || p->prefilter_cap > 63))
+        return fail(DSX_EINVAL, "prefilter_cap must be in [1, 63]");
     if (p->uniqueness_ratio < 0 || p->uniqueness_ratio >= 100)
         return fail(DSX_EINVAL, "uniqueness_ratio must be in [0, 100)");
     if (p->float_mode != DSX_FLOAT_FIXED && p->float_mode != DSX_FLOAT_PARABOLA)
@@ -86,7 +92,7 @@ int check(const dsx_params *p) {
         if (p->aggregation != DSX_AGG_SGBM_3WAY && p->aggregation != DSX_AGG_HH4 && p->aggregation != DSX_AGG_SGBM &&
             p->aggregation != DSX_AGG_HH)
             return fail(DSX_EINVAL, "aggregation must be 0, 3 (sgbm_3way), 4 (hh4), 5 (sgbm) or 8 (hh)");
-        if (p->cost != DSX_COST_SAD) return fail(DSX_EINVAL, "SGM aggregation runs on SAD block costs");
+        if (p->cost == DSX_COST_SSD) return fail(DSX_EINVAL, "SGM aggregation runs on SAD or BT block costs");
         if (p->num_disp > 256) return fail(DSX_EINVAL, "SGM aggregation supports num_disp <= 256");
         if (p->p1 > 65535 || p->p2 > 65535 || (p->p1 > 0 && p->p2 > 0 && p->p2 < p->p1))
             return fail(DSX_EINVAL, "SGM penalties must satisfy 0 < P1 <= P2 <= 65535");
@@ -127,6 +133,7 @@ struct dsx_handle {
     int16_t *dStar = nullptr;    // LR check: left winners (or -1) for lr_fixup
     void *vol = nullptr;
     size_t vol_bytes = 0;
+    void *btWs = nullptr;  // DSX_COST_BT: prep records of both views | horizontal sums
     uint32_t *sgmS = nullptr;  // SGM path sums [H][W][Dp] u32 (sequential directions)
     uint16_t *sgmL = nullptr;  // SGM L_r per direction, ndir x [H][W][Dp] u16 (concurrent directions)
     // timing
@@ -147,6 +154,8 @@ void free_buffers(dsx_handle *h) {
     (void)hipFree(h->lrKeys);
     (void)hipFree(h->dStar);
     (void)hipFree(h->vol);
+    (void)hipFree(h->btWs);
+    h->btWs = nullptr;
     (void)hipFree(h->sgmS);
     h->sgmS = nullptr;
     (void)hipFree(h->sgmL);
@@ -207,10 +216,12 @@ int ensure_buffers(dsx_handle *h, int H, int W, bool host_staging, int nframes =
         h->lrPending = false;
     }
 
-    if ((h->p.path == DSX_PATH_VOLUME || h->p.aggregation) && !h->vol) {
+    const bool bt = h->p.cost == DSX_COST_BT;
+    if ((h->p.path == DSX_PATH_VOLUME || h->p.aggregation || bt) && !h->vol) {
         h->vol_bytes = n * h->g.Dp * cbytes;
         DSX_HIP(hipMalloc(&h->vol, h->vol_bytes));
     }
+    if (bt && !h->btWs) DSX_HIP(hipMalloc(&h->btWs, dsx::bt_workspace(H, W, h->g.Dp)));
     if (h->p.aggregation) {
         if (sgm_concurrent(h)) {
             const int *set;
@@ -330,6 +341,7 @@ dsx::Bm2Args base_args(dsx_handle *h, int H, int W, int64_t stride) {
 
 int run_right_pass(dsx_handle *h, const void *dL, const void *dR, int H, int W, int64_t stride, int16_t *out,
                    hipStream_t st) {
+    if (h->p.cost == DSX_COST_BT) return fail(DSX_EINVAL, "the right-view map is a block-matching (SAD/SSD) pass");
     dsx::Bm2Args a = base_args(h, H, W, stride);
     a.side = dsx::SIDE_RIGHT;
     a.ref = static_cast<const uint8_t *>(dR);
@@ -345,7 +357,8 @@ int run(dsx_handle *h, const void *dL, const void *dR, int H, int W, int64_t str
         hipStream_t st, int nframes = 1, int64_t frame_stride = 0) {
     const int radius = h->p.block_size / 2;
     const bool ssd = h->p.cost == DSX_COST_SSD;
-    if (h->p.path == DSX_PATH_FUSED && !h->p.aggregation) {
+    const bool bt = h->p.cost == DSX_COST_BT;  // BT costs exist only as a volume
+    if (h->p.path == DSX_PATH_FUSED && !h->p.aggregation && !bt) {
         const bool lr = h->p.disp12_max_diff >= 0;
         dsx::Bm2Args a = base_args(h, H, W, stride);
         a.side = dsx::SIDE_LEFT;
@@ -413,12 +426,35 @@ int run(dsx_handle *h, const void *dL, const void *dR, int H, int W, int64_t str
         // volume path: one K1 + K2 pair per frame (the volume buffer holds one frame)
         for (int f = 0; f < nframes; ++f) {
             const size_t fo = (size_t)f * H * W;
-            dsx::Bm2Args a = base_args(h, H, W, stride);
-            a.side = dsx::SIDE_VOLUME;
-            a.ref = static_cast<const uint8_t *>(dL) + f * frame_stride;
-            a.src = static_cast<const uint8_t *>(dR) + f * frame_stride;
-            a.vol = h->vol;
-            DSX_LAUNCH(h, "cost_volume", st, dsx::launch_bm2(radius, ssd, h->g.NW, a, st));
+            if (bt) {
+                const size_t n = (size_t)H * W;
+                uint2 *prepL = static_cast<uint2 *>(h->btWs), *prepR = prepL + n;
+                const int ftz = bt_ftzero(h->p);
+                const uint8_t *l = static_cast<const uint8_t *>(dL) + f * frame_stride;
+                const uint8_t *r = static_cast<const uint8_t *>(dR) + f * frame_stride;
+                DSX_LAUNCH(h, "bt_prep", st, dsx::launch_bt_prep(l, stride, H, W, ftz, prepL, st));
+                DSX_LAUNCH(h, "bt_prep", st, dsx::launch_bt_prep(r, stride, H, W, ftz, prepR, st));
+                dsx::BtArgs b{};
+                b.prepL = prepL;
+                b.prepR = prepR;
+                b.hs = reinterpret_cast<uint16_t *>(prepR + n);
+                b.vol = h->vol;
+                b.H = H;
+                b.W = W;
+                b.m = h->p.min_disp;
+                b.D = h->p.num_disp;
+                b.Dp = h->g.Dp;
+                b.R = radius;
+                b.padv = pad_value(h);
+                DSX_LAUNCH(h, "cost_volume", st, dsx::launch_bt_volume(b, st));
+            } else {
+                dsx::Bm2Args a = base_args(h, H, W, stride);
+                a.side = dsx::SIDE_VOLUME;
+                a.ref = static_cast<const uint8_t *>(dL) + f * frame_stride;
+                a.src = static_cast<const uint8_t *>(dR) + f * frame_stride;
+                a.vol = h->vol;
+                DSX_LAUNCH(h, "cost_volume", st, dsx::launch_bm2(radius, ssd, h->g.NW, a, st));
+            }
             const bool agg = h->p.aggregation != DSX_AGG_NONE;
             const bool agg_all = agg && sgm_concurrent(h);
             const int *set = nullptr;
@@ -531,6 +567,7 @@ void dsx_default_params(dsx_params *p) {
     p->float_mode = DSX_FLOAT_FIXED;
     p->path = DSX_PATH_FUSED;
     p->timing = 0;
+    p->prefilter_cap = 31;
 }
 
 int dsx_check_params(const dsx_params *p) {

@@ -151,6 +151,18 @@ hipError_t launch_post_full(PostFullArgs a, void *ws, hipStream_t st);
 size_t inpaint_workspace(int H, int W);
 hipError_t launch_inpaint(const float *in, int64_t pitch, int H, int W, int radius, float *out, void *ws, hipStream_t st);
 
+// Birchfield-Tomasi block costs into K1's volume layout (dsx_bt.hip, oracle/bt_cost.py)
+struct BtArgs {
+    const uint2 *prepL, *prepR;  // bt_prep records of both views
+    uint16_t *hs;                // horizontal sums [H][W][Dp]
+    void *vol;                   // out: [H][W][Dp] u16, pads >= D
+    int H, W, m, D, Dp, R;
+    uint32_t padv;
+};
+size_t bt_workspace(int H, int W, int Dp);
+hipError_t launch_bt_prep(const uint8_t *img, int64_t pitch, int H, int W, int ftz, uint2 *out, hipStream_t st);
+hipError_t launch_bt_volume(const BtArgs &a, hipStream_t st);
+
 // Rectification (dsx_rectify.hip): gray conversion fused with the fixed-point bilinear remap.
 struct RectArgs {
     const uint8_t *img;  // Hs x Ws x channels (channels 1 or 3, BGR order), row stride in bytes

@@ -7,7 +7,9 @@ include/dsx.h) instead of ``cv2.StereoSGBM_create``, and ``compute_disparity``
 (stereo_core.py:212-232) calls its ``compute`` with the same cv2 contract (int16 x16 -> /16).
 
 Keys added to ``sgbm_params`` (accepted by ``configure_sgbm`` like the reference's own keys):
-  'cost'     : 'sad' | 'ssd'          (block cost; north_star SAD/SSD)
+  'cost'     : 'sad' | 'ssd' | 'bt'   (block cost; north_star SAD/SSD; 'bt' is OpenCV SGBM's
+                                       Birchfield-Tomasi pixel cost on the 'prefilter_cap'-clipped
+                                       x-derivative plus intensity, summed over the same block)
   'subpixel' : bool                   (1/16-px parabola refinement, on by default)
   'device'   : int                    (HIP device of the matcher)
   'aggregation': 'none' | 'sgm'       ('none', the default, is the north-star block matching;
@@ -15,8 +17,8 @@ Keys added to ``sgbm_params`` (accepted by ``configure_sgbm`` like the reference
                                        the path set of 'sgbm_mode' and P1 = 8 bs^2, P2 = 32 bs^2 as
                                        _build_sgbm derives them, stereo_core.py:51-61)
 Keys of the reference that have no block-matching meaning are kept, validated and reported
-but do not change the result: 'prefilter_cap', 'speckle_window_size', 'speckle_range', and
-'sgbm_mode' / P1 / P2 while 'aggregation' is 'none' (SURVEY.md 8a A5').
+but do not change the result: 'prefilter_cap' unless 'cost' is 'bt', 'speckle_window_size',
+'speckle_range', and 'sgbm_mode' / P1 / P2 while 'aggregation' is 'none' (SURVEY.md 8a A5').
 
 There is no CPU fallback: without libdsx.so or a HIP device ``compute_disparity`` raises.
 """
@@ -132,6 +134,7 @@ class StereoCore:
             aggregation=self.mode if p.get('aggregation', 'none') == 'sgm' else None,
             p1=self.P1,
             p2=self.P2,
+            prefilter_cap=p['prefilter_cap'],
         )
         if old is not None:
             old.close()

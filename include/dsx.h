@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define DSX_VERSION 100 /* 1.0.0 */
+#define DSX_VERSION 101 /* 1.0.1: DSX_COST_BT, dsx_params.prefilter_cap */
 
 #define DSX_OK 0
 #define DSX_EINVAL (-1) /* bad argument (mirrors ValueError / cv2.error on bad input) */
@@ -42,6 +42,10 @@ extern "C" {
 
 #define DSX_COST_SAD 0
 #define DSX_COST_SSD 1
+/* OpenCV SGBM's pixel cost (Birchfield-Tomasi on the prefilter_cap-clipped x-derivative plus the
+ * raw intensity >> 2, cv2.StereoSGBM preFilterCap, stereo_core.py:63-75) summed over the same
+ * block window; runs on the volume path (K1 replaced by the BT volume, then K2 / SGM). */
+#define DSX_COST_BT 2
 
 #define DSX_FLOAT_FIXED 0    /* out_float = out_fixed / 16 (stereo_core.py:232 contract) */
 #define DSX_FLOAT_PARABOLA 1 /* out_float = continuous parabola vertex (north-star 1e-3 path) */
@@ -64,7 +68,7 @@ typedef struct dsx_params {
     int32_t min_disp;         /* 'min_disp'          (stereo_core.py:17, cv2 minDisparity)    */
     int32_t num_disp;         /* 'num_disp'          (stereo_core.py:18, cv2 numDisparities)  */
     int32_t block_size;       /* 'block_size'        (stereo_core.py:19), odd, 1..15          */
-    int32_t cost;             /* DSX_COST_SAD | DSX_COST_SSD (build key 'cost')               */
+    int32_t cost;             /* DSX_COST_SAD | DSX_COST_SSD | DSX_COST_BT (build key 'cost')  */
     int32_t uniqueness_ratio; /* 'uniqueness_ratio'  (stereo_core.py:22), 0 disables, <100    */
     int32_t disp12_max_diff;  /* 'disp12_max_diff'   (stereo_core.py:20), <0 disables LR      */
     int32_t subpixel;         /* build key 'subpixel': 1 = 1/16-px parabola, 0 = integer      */
@@ -76,7 +80,8 @@ typedef struct dsx_params {
     int32_t aggregation;      /* DSX_AGG_*: 0 = plain block matching (default); otherwise the */
                               /* SGM path set of 'sgbm_mode' (stereo_core.py:55-61), SAD only */
     int32_t p1, p2;           /* SGM penalties; <= 0 -> 8*bs^2 / 32*bs^2 (stereo_core.py:51-52) */
-    int32_t reserved[2];
+    int32_t prefilter_cap;    /* 'prefilter_cap'     (stereo_core.py:21), 1..63; DSX_COST_BT only */
+    int32_t reserved[1];
 } dsx_params;
 
 typedef struct dsx_handle dsx_handle;
@@ -89,7 +94,7 @@ int dsx_device_count(int *n);
 
 /* Fill *p with the defaults of StereoCore.sgbm_params (stereo_core.py:16-39) plus the build
  * keys: min 0, num 128, block 5, SAD, uniqueness 10, disp12 1, subpixel 1, fixed floats,
- * fused path. */
+ * fused path, prefilter_cap 31. */
 void dsx_default_params(dsx_params *p);
 
 /* Validate parameters without creating a handle (DSX_EINVAL + message if unsupported). */

@@ -15,8 +15,8 @@ class _Params(ctypes.Structure):
     # field order and types of dsx_params (include/dsx.h)
     _fields_ = [(n, ctypes.c_int32) for n in (
         "min_disp", "num_disp", "block_size", "cost", "uniqueness_ratio", "disp12_max_diff",
-        "subpixel", "float_mode", "path", "timing", "grid_blocks", "aggregation", "p1", "p2")] + \
-        [("reserved", ctypes.c_int32 * 2)]
+        "subpixel", "float_mode", "path", "timing", "grid_blocks", "aggregation", "p1", "p2",
+        "prefilter_cap")] + [("reserved", ctypes.c_int32 * 1)]
 
 
 # sgbm_mode names (stereo_core.py:55-61) -> DSX_AGG_* (semi-global aggregation over SAD costs)
@@ -34,11 +34,14 @@ _lib.dsx_last_error.restype = ctypes.c_char_p
 
 
 def make_params(minDisparity=0, numDisparities=128, blockSize=5, disp12MaxDiff=1, uniquenessRatio=10,
-                cost=0, sgbm_mode=None, P1=0, P2=0):
+                cost=0, sgbm_mode=None, P1=0, P2=0, preFilterCap=31):
+    # cost: 0 SAD, 1 SSD, 2 BT (OpenCV SGBM's Birchfield-Tomasi pixel cost on the preFilterCap-clipped
+    # x-derivative plus intensity)
     p = _Params()
     _lib.dsx_default_params(ctypes.byref(p))
     p.min_disp, p.num_disp, p.block_size = minDisparity, numDisparities, blockSize
     p.disp12_max_diff, p.uniqueness_ratio, p.cost = disp12MaxDiff, uniquenessRatio, cost
+    p.prefilter_cap = preFilterCap
     if sgbm_mode is not None:
         p.aggregation, p.p1, p.p2 = SGBM_MODES[sgbm_mode], P1, P2
     if _lib.dsx_check_params(ctypes.byref(p)) != 0:
@@ -50,9 +53,10 @@ class DsxStereoMatcher:
     """cv2.StereoMatcher-compatible: compute(L, R) -> int16 H x W disparity x16, invalid (min_disp - 1) * 16."""
 
     def __init__(self, minDisparity=0, numDisparities=128, blockSize=5, disp12MaxDiff=1,
-                 uniquenessRatio=10, cost=0, device=0, sgbm_mode=None, P1=0, P2=0, **_sgbm_only_keys):
+                 uniquenessRatio=10, cost=0, device=0, sgbm_mode=None, P1=0, P2=0, preFilterCap=31,
+                 **_sgbm_only_keys):
         p = make_params(minDisparity, numDisparities, blockSize, disp12MaxDiff, uniquenessRatio, cost,
-                        sgbm_mode, P1, P2)
+                        sgbm_mode, P1, P2, preFilterCap)
         self._h = _vp()
         if _lib.dsx_create(device, ctypes.byref(p), ctypes.byref(self._h)) != 0:
             self._h = None

@@ -1,0 +1,181 @@
+"""OpenCV SGBM's Birchfield-Tomasi pixel cost ('cost': 'bt'; VERDICT r1 missing item 6).
+
+The reference's matcher is cv2.StereoSGBM with preFilterCap = sgbm_params['prefilter_cap']
+(depthlib/stereo_core.py:63-75).  OpenCV is absent, so parity against it is unpinned: the NumPy
+restatement (oracle/bt_cost.py) is pinned by an independent loop restatement and by known answers,
+and the HIP volume (dsx_bt.hip) is checked bit-exactly against it, alone and under SGM."""
+from __future__ import annotations
+
+import numpy as np
+import pytest
+
+from depthestimation_amd import _dsx
+from depthestimation_amd.synthetic import stereo_pair
+from oracle.bt_cost import bt_bruteforce, channels, cost_volume_bt, ftzero, max_cost_bt
+from oracle.sgm import aggregate
+from oracle.stereo_bm import wta_epilogue
+
+
+@pytest.mark.parametrize("H,W,m,D,bs,cap", [
+    (5, 9, 0, 4, 3, 31), (4, 7, -2, 5, 1, 5), (6, 11, 2, 3, 5, 63), (1, 1, 0, 2, 1, 31), (3, 2, 0, 3, 3, 15),
+    (7, 12, 0, 6, 3, 1), (2, 13, 1, 7, 7, 40),
+])
+def test_vectorised_matches_loop_restatement(H, W, m, D, bs, cap):
+    rng = np.random.default_rng(H * 100 + W)
+    L = rng.integers(0, 256, (H, W), dtype=np.uint8)
+    R = rng.integers(0, 256, (H, W), dtype=np.uint8)
+    np.testing.assert_array_equal(cost_volume_bt(L, R, m, D, bs, cap), bt_bruteforce(L, R, m, D, bs, cap))
+
+
+def test_known_answers():
+    assert [ftzero(c) for c in (1, 15, 16, 31, 62, 63)] == [15, 15, 17, 31, 63, 63]
+    assert max_cost_bt(15, 63) == 225 * 189 < 1 << 16
+    # a constant image: prefiltered channel = ftzero everywhere; the raw channel holds ftzero in
+    # the end columns (OpenCV's row-end fill), so only d = 0 costs 0 everywhere
+    c = np.full((6, 10), 77, np.uint8)
+    P, I = channels(c, 31)
+    assert (P == 31).all() and (I[:, 1:-1] == 77).all() and (I[:, [0, -1]] == 31).all()
+    C = cost_volume_bt(c, c, 0, 4, 3, 31)
+    assert not C[..., 0].any() and not C[:, 5:8, :].any() and (C[:, 1, 2] > 0).all() and (C[:, 9, 1] > 0).all()
+    # x-derivative clipping: a step of 255 saturates at 2 * ftzero / 0
+    s = np.zeros((3, 8), np.uint8)
+    s[:, 4:] = 255
+    P, _ = channels(s, 20)
+    ftz = ftzero(20)
+    assert P[1, 3] == 2 * ftz and P[1, 4] == 2 * ftz and P[1, 1] == ftz
+    assert channels(255 - s, 20)[0][1, 3] == 0
+    # a pure shift: the true disparity costs 0 away from the borders, a wrong one does not
+    rng = np.random.default_rng(5)
+    base = rng.integers(0, 256, (9, 40), dtype=np.uint8)
+    d0 = 3
+    L = base[:, d0:].copy()
+    R = base[:, :-d0].copy()
+    C = cost_volume_bt(R, L, 0, 6, 3, 31)  # reference view = R here: R(x) = L(x - d0)
+    inner = C[2:-2, d0 + 3:-3]
+    assert not inner[..., d0].any() and (inner.argmin(axis=2) == d0).mean() > 0.95
+
+
+def test_params_validation():
+    p = _dsx.make_params(cost="bt", num_disp=64, block_size=15, prefilter_cap=63)
+    _dsx.check_params(p)
+    assert (p.cost, p.prefilter_cap) == (2, 63)
+    _dsx.check_params(_dsx.make_params(cost="bt", aggregation="hh", prefilter_cap=1))
+    assert _dsx.default_params().prefilter_cap == 31
+    for kw in (dict(cost="bt", prefilter_cap=0), dict(cost="bt", prefilter_cap=64), dict(cost="ssd", aggregation="hh")):
+        with pytest.raises(ValueError):
+            _dsx.check_params(_dsx.make_params(**kw))
+    _dsx.check_params(_dsx.make_params(cost="sad", prefilter_cap=0))  # ignored outside 'bt'
+
+
+def test_stereo_core_bt_key():
+    from depthestimation_amd.stereo_core import StereoCore
+    core = StereoCore()
+    core.configure_sgbm(cost="bt", prefilter_cap=15)
+    assert core.sgbm.params["cost"] == "bt" and core.sgbm.params["prefilter_cap"] == 15
+    with pytest.raises(ValueError):
+        core.configure_sgbm(cost="bt", prefilter_cap=99)
+
+
+# ---------------------------------------------------------------- GPU -------------------
+CASES = [
+    dict(H=24, W=90, m=0, D=32, bs=5, u=0, lr=-1, cap=31),
+    dict(H=31, W=77, m=3, D=48, bs=3, u=10, lr=1, cap=63),
+    dict(H=17, W=70, m=0, D=160, bs=7, u=5, lr=0, cap=15),    # Dp = 256
+    dict(H=1, W=64, m=-2, D=16, bs=1, u=0, lr=2, cap=5),      # one row, one-pixel window
+    dict(H=40, W=150, m=0, D=64, bs=15, u=10, lr=1, cap=63),  # the largest window (max cost 42,525)
+    dict(H=9, W=33, m=0, D=100, bs=9, u=0, lr=1, cap=31),     # D > W: every search leaves the image
+]
+
+
+def _gpu():
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", CASES, ids=lambda c: f"{c['H']}x{c['W']}_D{c['D']}_bs{c['bs']}")
+@pytest.mark.parametrize("float_mode", ["fixed", "parabola"])
+def test_gpu_bt_matches_oracle(case, float_mode):
+    _gpu()
+    from depthestimation_amd.matcher import HipBlockMatcher
+    L, R, _ = stereo_pair(case["H"], case["W"], case["m"], case["D"], seed=case["H"] * 7 + case["W"])
+    C = cost_volume_bt(L, R, case["m"], case["D"], case["bs"], case["cap"])
+    ref = wta_epilogue(C, case["m"], case["u"], case["lr"], True)
+    m = HipBlockMatcher(min_disp=case["m"], num_disp=case["D"], block_size=case["bs"], cost="bt",
+                        uniqueness_ratio=case["u"], disp12_max_diff=case["lr"], subpixel=True,
+                        float_mode=float_mode, prefilter_cap=case["cap"])
+    flt = np.empty(L.shape, np.float32)
+    fixed = m.compute(L, R, out_float=flt)
+    m.close()
+    np.testing.assert_array_equal(fixed, ref["fixed"])
+    if float_mode == "fixed":
+        np.testing.assert_array_equal(flt, ref["disp"])
+    else:  # north_star's float tolerance
+        np.testing.assert_allclose(flt, ref["parabola"], rtol=0, atol=1e-3)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode", ["sgbm_3way", "hh4", "sgbm", "hh"])
+def test_gpu_bt_sgm_matches_oracle(mode):
+    """The reference's own configuration: SGBM path set over BT costs (stereo_core.py:51-75)."""
+    _gpu()
+    from depthestimation_amd.matcher import HipBlockMatcher
+    L, R, _ = stereo_pair(33, 120, 0, 48, seed=11)
+    bs = 5
+    C = cost_volume_bt(L, R, 0, 48, bs, 31)
+    ref = wta_epilogue(aggregate(C, mode, 8 * bs * bs, 32 * bs * bs), 0, 10, 1, True)
+    m = HipBlockMatcher(min_disp=0, num_disp=48, block_size=bs, cost="bt", uniqueness_ratio=10, disp12_max_diff=1,
+                        aggregation=mode, p1=8 * bs * bs, p2=32 * bs * bs, prefilter_cap=31)
+    got = m.compute(L, R)
+    m.close()
+    np.testing.assert_array_equal(got, ref["fixed"])
+
+
+@pytest.mark.gpu
+def test_gpu_bt_batch_and_stereo_core():
+    _gpu()
+    import torch
+    from depthestimation_amd.matcher import HipBlockMatcher
+    from depthestimation_amd.stereo_core import StereoCore
+    pairs = [stereo_pair(45, 200, 0, 64, seed=s)[:2] for s in range(3)]
+    m = HipBlockMatcher(num_disp=64, block_size=7, cost="bt", prefilter_cap=20)
+    Ld = torch.stack([torch.from_numpy(p[0]) for p in pairs]).cuda()
+    Rd = torch.stack([torch.from_numpy(p[1]) for p in pairs]).cuda()
+    out = torch.empty((3, 45, 200), dtype=torch.int16, device="cuda")
+    m.compute_batch_device(Ld, Rd, out_fixed=out)
+    torch.cuda.synchronize()
+    for i, (L, R) in enumerate(pairs):
+        ref = wta_epilogue(cost_volume_bt(L, R, 0, 64, 7, 20), 0, 10, 1, True)["fixed"]
+        np.testing.assert_array_equal(out[i].cpu().numpy(), ref)
+    with pytest.raises(ValueError):
+        m.right_map_device(Ld[0], Rd[0], torch.empty((45, 200), dtype=torch.int16, device="cuda"))
+    m.close()
+    core = StereoCore()
+    core.configure_sgbm(num_disp=64, block_size=5, cost="bt", aggregation="sgm", sgbm_mode="sgbm_3way")
+    L, R = pairs[0]
+    got = core.compute_disparity(L, R)
+    C = cost_volume_bt(L, R, 0, 64, 5, 31)
+    ref = wta_epilogue(aggregate(C, "sgbm_3way", 200, 800), 0, 10, 1, True)["fixed"]
+    np.testing.assert_array_equal(got, ref.astype(np.float32) / 16.0)
+
+
+@pytest.mark.gpu
+def test_gpu_bt_c2_size_properties():
+    """C2's size (1920 x 1080, D 128, block 9): rows against the oracle on row bands (a row needs
+    the window's 4 rows either side plus the x-derivative's one more)."""
+    _gpu()
+    from depthestimation_amd.matcher import HipBlockMatcher
+    L, R, _ = stereo_pair(1080, 1920, 0, 128, seed=2)
+    m = HipBlockMatcher(num_disp=128, block_size=9, cost="bt", uniqueness_ratio=10, disp12_max_diff=-1)
+    got = m.compute(L, R)
+    m.close()
+    for y0 in (0, 537, 1072):
+        lo, hi = max(0, y0 - 5), min(1080, y0 + 8 + 5)
+        C = cost_volume_bt(L[lo:hi], R[lo:hi], 0, 128, 9, 31)
+        ref = wta_epilogue(C, 0, 10, -1, True)["fixed"]
+        # rows whose window stays inside the band (or is clamped by the image edge like the band's)
+        for y in range(y0, min(1080, y0 + 8)):
+            yy = y - lo
+            if (y - 5 >= lo or lo == 0) and (y + 5 < hi or hi == 1080):
+                np.testing.assert_array_equal(got[y], ref[yy], err_msg=f"row {y}")
