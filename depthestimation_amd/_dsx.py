@@ -55,7 +55,10 @@ class DsxParams(ctypes.Structure):
         ("p1", ctypes.c_int32),
         ("p2", ctypes.c_int32),
         ("prefilter_cap", ctypes.c_int32),
-        ("reserved", ctypes.c_int32 * 1),
+        ("sgbm_post", ctypes.c_int32),
+        ("speckle_window_size", ctypes.c_int32),
+        ("speckle_range", ctypes.c_int32),
+        ("reserved", ctypes.c_int32 * 4),
     ]
 
 
@@ -153,7 +156,8 @@ def default_params() -> DsxParams:
 
 def make_params(min_disp=0, num_disp=128, block_size=5, cost="sad", uniqueness_ratio=10,
                 disp12_max_diff=1, subpixel=True, float_mode="fixed", path="fused",
-                timing=False, grid_blocks=0, aggregation=None, p1=0, p2=0, prefilter_cap=31) -> DsxParams:
+                timing=False, grid_blocks=0, aggregation=None, p1=0, p2=0, prefilter_cap=31,
+                sgbm_post=False, speckle_window_size=50, speckle_range=2) -> DsxParams:
     p = default_params()
     p.min_disp = int(min_disp)
     p.num_disp = int(num_disp)
@@ -178,6 +182,9 @@ def make_params(min_disp=0, num_disp=128, block_size=5, cost="sad", uniqueness_r
     p.p1 = int(p1)
     p.p2 = int(p2)
     p.prefilter_cap = int(prefilter_cap)
+    p.sgbm_post = int(bool(sgbm_post))
+    p.speckle_window_size = int(speckle_window_size)
+    p.speckle_range = int(speckle_range)
     return p
 
 

@@ -80,6 +80,13 @@ int check(const dsx_params *p) {
         return fail(DSX_EINVAL, "cost must be SAD (0), SSD (1) or BT (2)");
     if (p->cost == DSX_COST_BT && (p->prefilter_cap < 1 || p->prefilter_cap > 63))
         return fail(DSX_EINVAL, "prefilter_cap must be in [1, 63]");
+    if (p->sgbm_post != 0 && p->sgbm_post != 1) return fail(DSX_EINVAL, "sgbm_post must be 0 or 1");
+    if (p->sgbm_post) {
+        if (p->float_mode != DSX_FLOAT_FIXED)
+            return fail(DSX_EINVAL, "sgbm_post filters the int16 map: float_mode must be fixed");
+        if (p->speckle_window_size < 0 || p->speckle_range < 0 || p->speckle_range > 2047)
+            return fail(DSX_EINVAL, "speckle_window_size must be >= 0 and speckle_range in [0, 2047]");
+    }
     if (p->uniqueness_ratio < 0 || p->uniqueness_ratio >= 100)
         return fail(DSX_EINVAL, "uniqueness_ratio must be in [0, 100)");
     if (p->float_mode != DSX_FLOAT_FIXED && p->float_mode != DSX_FLOAT_PARABOLA)
@@ -134,6 +141,9 @@ struct dsx_handle {
     void *vol = nullptr;
     size_t vol_bytes = 0;
     void *btWs = nullptr;  // DSX_COST_BT: prep records of both views | horizontal sums
+    int16_t *postIn = nullptr;  // sgbm_post: the matcher's int16 maps (postFrames frames)
+    void *postWs = nullptr;     // sgbm_post: median | speckle components
+    int postFrames = 0;
     uint32_t *sgmS = nullptr;  // SGM path sums [H][W][Dp] u32 (sequential directions)
     uint16_t *sgmL = nullptr;  // SGM L_r per direction, ndir x [H][W][Dp] u16 (concurrent directions)
     // timing
@@ -156,6 +166,11 @@ void free_buffers(dsx_handle *h) {
     (void)hipFree(h->vol);
     (void)hipFree(h->btWs);
     h->btWs = nullptr;
+    (void)hipFree(h->postIn);
+    (void)hipFree(h->postWs);
+    h->postIn = nullptr;
+    h->postWs = nullptr;
+    h->postFrames = 0;
     (void)hipFree(h->sgmS);
     h->sgmS = nullptr;
     (void)hipFree(h->sgmL);
@@ -222,6 +237,14 @@ int ensure_buffers(dsx_handle *h, int H, int W, bool host_staging, int nframes =
         DSX_HIP(hipMalloc(&h->vol, h->vol_bytes));
     }
     if (bt && !h->btWs) DSX_HIP(hipMalloc(&h->btWs, dsx::bt_workspace(H, W, h->g.Dp)));
+    if (h->p.sgbm_post && h->postFrames < nframes) {
+        (void)hipFree(h->postIn);
+        h->postIn = nullptr;
+        h->postFrames = 0;
+        DSX_HIP(hipMalloc(&h->postIn, n * nframes * 2));
+        h->postFrames = nframes;
+    }
+    if (h->p.sgbm_post && !h->postWs) DSX_HIP(hipMalloc(&h->postWs, dsx::sgbm_post_workspace(H, W)));
     if (h->p.aggregation) {
         if (sgm_concurrent(h)) {
             const int *set;
@@ -358,6 +381,12 @@ int run(dsx_handle *h, const void *dL, const void *dR, int H, int W, int64_t str
     const int radius = h->p.block_size / 2;
     const bool ssd = h->p.cost == DSX_COST_SSD;
     const bool bt = h->p.cost == DSX_COST_BT;  // BT costs exist only as a volume
+    // sgbm_post: the matcher writes int16 maps into postIn, the tail then writes the outputs
+    void *const finalFixed = outFixed, *const finalFloat = outFloat;
+    if (h->p.sgbm_post) {
+        outFixed = h->postIn;
+        outFloat = nullptr;
+    }
     if (h->p.path == DSX_PATH_FUSED && !h->p.aggregation && !bt) {
         const bool lr = h->p.disp12_max_diff >= 0;
         dsx::Bm2Args a = base_args(h, H, W, stride);
@@ -520,6 +549,17 @@ int run(dsx_handle *h, const void *dL, const void *dR, int H, int W, int64_t str
             DSX_LAUNCH(h, "volume_wta", st, dsx::launch_volume_wta(h->g.TX, wide, v, st));
         }
     }
+    if (h->p.sgbm_post) {
+        for (int f = 0; f < nframes; ++f) {
+            const size_t fo = (size_t)f * H * W;
+            DSX_LAUNCH(h, "sgbm_post", st,
+                       dsx::launch_sgbm_post(h->postIn + fo, H, W, (h->p.min_disp - 1) * 16, h->p.speckle_window_size,
+                                             16 * h->p.speckle_range,
+                                             finalFixed ? static_cast<int16_t *>(finalFixed) + fo : nullptr,
+                                             finalFloat ? static_cast<float *>(finalFloat) + fo : nullptr, h->postWs,
+                                             st));
+        }
+    }
     return DSX_OK;
 }
 
@@ -568,6 +608,9 @@ void dsx_default_params(dsx_params *p) {
     p->path = DSX_PATH_FUSED;
     p->timing = 0;
     p->prefilter_cap = 31;
+    p->sgbm_post = 0;
+    p->speckle_window_size = 50;
+    p->speckle_range = 2;
 }
 
 int dsx_check_params(const dsx_params *p) {

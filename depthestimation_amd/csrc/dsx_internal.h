@@ -142,8 +142,19 @@ struct PostFullArgs {
     int *parent, *count, *root, *lsz;
     int16_t *v16;
     float *t0, *t1;
+    // speckles of an int16 x16 map (launch_sgbm_post): in16 replaces disp, newv is the value that
+    // marks removed / never-joining pixels (0 on the postprocess_disparity path)
+    const int16_t *in16;
+    int newv;
+    int16_t *out16;
 };
 size_t post_full_workspace(int H, int W, int crop);
+// cv2.StereoSGBM::compute's own tail on an int16 x16 map: 3x3 median (BORDER_REPLICATE), then
+// filterSpeckles(newVal, maxSpeckleSize, maxDiff) when max_speckle > 0.  Writes out16 and / or
+// outf (= out16 / 16); `in` must not alias the outputs.
+size_t sgbm_post_workspace(int H, int W);
+hipError_t launch_sgbm_post(const int16_t *in, int H, int W, int newv, int max_speckle, int max_diff16, int16_t *out16,
+                            float *outf, void *ws, hipStream_t st);
 hipError_t launch_post_full(PostFullArgs a, void *ws, hipStream_t st);
 
 // Hole filling (dsx_inpaint.hip): fill_holes(method='inpaint') on d <= 0, layered Telea marching.

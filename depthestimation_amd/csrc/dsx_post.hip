@@ -149,7 +149,7 @@ __device__ __forceinline__ void ufl_unite(int *pl, int a, int b) {
     }
 }
 
-__device__ __forceinline__ bool joins(int u, int v, int md) { return u != 0 && v != 0 && abs(u - v) <= md; }
+__device__ __forceinline__ bool joins(int u, int v, int md, int nv) { return u != nv && v != nv && abs(u - v) <= md; }
 
 // Tile pass: d16 = int16(trunc(d * 16)) of the cropped map, union-find of the tile's edges in LDS
 // (local indices are row-major, so "root = smallest index" is the same order globally).  Writes
@@ -164,30 +164,35 @@ __global__ __launch_bounds__(256) void speckle_local(PostFullArgs a) {
     const int tw = min(kCcTX, Wc - x0), th = min(kCcTY, a.H - y0);
     for (int i = threadIdx.x; i < kCcTX * kCcTY; i += 256) {
         const int ly = i / kCcTX, lx = i - ly * kCcTX;
-        int16_t d16 = 0;
+        int16_t d16 = (int16_t)a.newv;
         if (lx < tw && ly < th) {
-            const float v = a.disp[(int64_t)(y0 + ly) * a.in_pitch + a.crop + x0 + lx];
-            d16 = (int16_t)(int)__builtin_truncf(v * 16.0f);
+            const int64_t q = (int64_t)(y0 + ly) * a.in_pitch + a.crop + x0 + lx;
+            if (a.in16) {
+                d16 = a.in16[q];
+            } else {
+                const float v = a.disp[q];
+                d16 = (int16_t)(int)__builtin_truncf(v * 16.0f);
+            }
             a.v16[(int64_t)(y0 + ly) * Wc + x0 + lx] = d16;
         }
         vl[i] = d16;
-        pl[i] = d16 != 0 ? i : -1;
+        pl[i] = d16 != a.newv ? i : -1;
         cl[i] = 0;
     }
     __syncthreads();
     for (int i = threadIdx.x; i < kCcTX * kCcTY; i += 256) {
         const int ly = i / kCcTX, lx = i - ly * kCcTX;
         const int v = vl[i];
-        if (v == 0) continue;
-        if (lx > 0 && joins(vl[i - 1], v, a.max_diff16)) ufl_unite(pl, i, i - 1);
-        if (ly > 0 && joins(vl[i - kCcTX], v, a.max_diff16)) ufl_unite(pl, i, i - kCcTX);
+        if (v == a.newv) continue;
+        if (lx > 0 && joins(vl[i - 1], v, a.max_diff16, a.newv)) ufl_unite(pl, i, i - 1);
+        if (ly > 0 && joins(vl[i - kCcTX], v, a.max_diff16, a.newv)) ufl_unite(pl, i, i - kCcTX);
     }
     __syncthreads();
     for (int i = threadIdx.x; i < kCcTX * kCcTY; i += 256) {
         const int ly = i / kCcTX, lx = i - ly * kCcTX;
         if (lx >= tw || ly >= th) continue;
         const int64_t p = (int64_t)(y0 + ly) * Wc + x0 + lx;
-        if (vl[i] == 0) {
+        if (vl[i] == a.newv) {
             a.root[p] = -1;
         } else {
             const int r = ufl_find(pl, i);
@@ -199,7 +204,7 @@ __global__ __launch_bounds__(256) void speckle_local(PostFullArgs a) {
     }
     __syncthreads();
     for (int i = threadIdx.x; i < kCcTX * kCcTY; i += 256) {
-        if (pl[i] != i) continue;  // local roots only (vl != 0)
+        if (pl[i] != i) continue;  // local roots only (vl != newv)
         const int ly = i / kCcTX, lx = i - ly * kCcTX;
         const int g = (int)((int64_t)(y0 + ly) * Wc + x0 + lx);
         a.parent[g] = g;
@@ -214,7 +219,7 @@ __global__ __launch_bounds__(256) void speckle_local(PostFullArgs a) {
 __global__ __launch_bounds__(256) void speckle_merge(PostFullArgs a, int ntx, int nty) {
     const int Wc = a.W - a.crop;
     const int64_t nv = (int64_t)a.H * (ntx - 1), nh = (int64_t)(nty - 1) * Wc;
-    const int md = a.max_diff16;
+    const int md = a.max_diff16, newv = a.newv;
     for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < nv + nh; i += (int64_t)gridDim.x * 256) {
         int y, x, q, s;  // edge p - q -> p; s = step to the previous edge along the border
         if (i < nv) {
@@ -230,8 +235,8 @@ __global__ __launch_bounds__(256) void speckle_merge(PostFullArgs a, int ntx, in
             s = x > 0 ? 1 : 0;
         }
         const int p = y * Wc + x;
-        if (!joins(a.v16[p], a.v16[p - q], md)) continue;
-        if (s && joins(a.v16[p - s], a.v16[p - s - q], md) && a.root[p] == a.root[p - s] &&
+        if (!joins(a.v16[p], a.v16[p - q], md, newv)) continue;
+        if (s && joins(a.v16[p - s], a.v16[p - s - q], md, newv) && a.root[p] == a.root[p - s] &&
             a.root[p - q] == a.root[p - s - q])
             continue;  // same pair as the previous edge: already united there
         uf_unite(a.parent, a.root[p], a.root[p - q]);  // parents exist for local roots only
@@ -256,16 +261,43 @@ __global__ __launch_bounds__(256) void speckle_resolve(PostFullArgs a) {
     }
 }
 
-// size of pixel p's component (after speckle_resolve); p must be live (v16 != 0)
+// size of pixel p's component (after speckle_resolve); p must be live (v16 != newv)
 __device__ __forceinline__ int comp_size(const PostFullArgs &a, int64_t p) { return a.count[a.parent[a.root[p]]]; }
 
 __global__ __launch_bounds__(256) void speckle_apply(PostFullArgs a) {
     const int64_t n = (int64_t)a.H * (a.W - a.crop);
     for (int64_t p = (int64_t)blockIdx.x * 256 + threadIdx.x; p < n; p += (int64_t)gridDim.x * 256) {
         int v = a.v16[p];
-        if (v != 0 && comp_size(a, p) <= a.max_speckle) v = 0;
+        if (v != a.newv && comp_size(a, p) <= a.max_speckle) v = a.newv;
         a.t0[p] = (float)v / 16.0f;
     }
+}
+
+// int16 form (launch_sgbm_post): small components -> newv; out_disp (optional) = out16 / 16
+__global__ __launch_bounds__(256) void speckle_apply16(PostFullArgs a) {
+    const int64_t n = (int64_t)a.H * a.W;
+    for (int64_t p = (int64_t)blockIdx.x * 256 + threadIdx.x; p < n; p += (int64_t)gridDim.x * 256) {
+        int v = a.v16[p];
+        if (v != a.newv && comp_size(a, p) <= a.max_speckle) v = a.newv;
+        if (a.out16) a.out16[p] = (int16_t)v;
+        if (a.out_disp) a.out_disp[p] = (float)v * 0.0625f;
+    }
+}
+
+// 3x3 median of an int16 map, BORDER_REPLICATE (cv2.medianBlur(disp, disp, 3) in
+// StereoSGBM::compute); int16 values are exact in float, so the float network's median is exact
+__global__ __launch_bounds__(256) void median3_i16(const int16_t *in, int H, int W, int16_t *out, float *outf) {
+    const int x = blockIdx.x * 256 + threadIdx.x, y = blockIdx.y;
+    if (x >= W) return;
+    auto tap = [&](int dy, int dx) __attribute__((always_inline)) -> float {
+        const int yy = min(max(y + dy, 0), H - 1), xx = min(max(x + dx, 0), W - 1);
+        return (float)in[(int64_t)yy * W + xx];
+    };
+    const float med = median9(tap(-1, -1), tap(-1, 0), tap(-1, 1), tap(0, -1), tap(0, 0), tap(0, 1), tap(1, -1),
+                              tap(1, 0), tap(1, 1));
+    const int64_t o = (int64_t)y * W + x;
+    if (out) out[o] = (int16_t)med;
+    if (outf) outf[o] = med * 0.0625f;
 }
 
 __device__ __forceinline__ int reflect101(int i, int n) {
@@ -326,7 +358,7 @@ __global__ __launch_bounds__(kTailTX *kTailTY) void post_tail(PostFullArgs a) {
         const int yy = reflect101(y0 - 1 - r + ty, H), xx = reflect101(x0 - 1 - r + tx, Wc);
         const int64_t p = (int64_t)yy * Wc + xx;
         int v = a.v16[p];
-        if (v != 0 && comp_size(a, p) <= a.max_speckle) v = 0;
+        if (v != a.newv && comp_size(a, p) <= a.max_speckle) v = a.newv;
         t0[ty][tx] = (float)v / 16.0f;
     }
     __syncthreads();
@@ -459,6 +491,52 @@ hipError_t launch_post_full(PostFullArgs a, void *ws, hipStream_t st) {
     m.max_depth = a.max_depth;
     m.has_max = a.has_max;
     return launch_post_fast(m, st);
+}
+
+size_t sgbm_post_workspace(int H, int W) {
+    const size_t n = (size_t)H * W;
+    const auto r = [](size_t b) { return (b + 255) & ~(size_t)255; };
+    return r(n * 2) + r(n * 4) * 4 + r(n * 2);  // median | parent, count, root, lsz | v16
+}
+
+hipError_t launch_sgbm_post(const int16_t *in, int H, int W, int newv, int max_speckle, int max_diff16, int16_t *out16,
+                            float *outf, void *ws, hipStream_t st) {
+    const size_t n = (size_t)H * W;
+    const auto r = [](size_t b) { return (b + 255) & ~(size_t)255; };
+    uint8_t *w = static_cast<uint8_t *>(ws);
+    const bool speckles = max_speckle > 0;
+    int16_t *med = reinterpret_cast<int16_t *>(w);
+    hipLaunchKernelGGL(median3_i16, dim3((W + 255) / 256, H), dim3(256), 0, st, in, H, W, speckles ? med : out16,
+                       speckles ? nullptr : outf);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess || !speckles) return e;
+    PostFullArgs a{};
+    a.in16 = med;
+    a.in_pitch = W;
+    a.H = H;
+    a.W = W;
+    a.crop = 0;
+    a.max_speckle = max_speckle;
+    a.max_diff16 = max_diff16;
+    a.newv = newv;
+    a.out16 = out16;
+    a.out_disp = outf;
+    a.parent = reinterpret_cast<int *>(w + r(n * 2));
+    a.count = reinterpret_cast<int *>(w + r(n * 2) + r(n * 4));
+    a.root = reinterpret_cast<int *>(w + r(n * 2) + 2 * r(n * 4));
+    a.lsz = reinterpret_cast<int *>(w + r(n * 2) + 3 * r(n * 4));
+    a.v16 = reinterpret_cast<int16_t *>(w + r(n * 2) + 4 * r(n * 4));
+    const int grid = (int)std::min<size_t>((n + 255) / 256, 4096);
+    const int ntx = (W + kCcTX - 1) / kCcTX, nty = (H + kCcTY - 1) / kCcTY;
+    hipLaunchKernelGGL(speckle_local, dim3(ntx, nty), dim3(256), 0, st, a);
+    if (ntx > 1 || nty > 1) {
+        const int64_t nb = (int64_t)H * (ntx - 1) + (int64_t)(nty - 1) * W;
+        hipLaunchKernelGGL(speckle_merge, dim3((unsigned)std::min<int64_t>((nb + 255) / 256, 4096)), dim3(256), 0, st, a,
+                           ntx, nty);
+    }
+    hipLaunchKernelGGL(speckle_resolve, dim3(grid), dim3(256), 0, st, a);
+    hipLaunchKernelGGL(speckle_apply16, dim3(grid), dim3(256), 0, st, a);
+    return hipGetLastError();
 }
 
 }  // namespace dsx

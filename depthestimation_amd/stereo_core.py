@@ -10,6 +10,10 @@ Keys added to ``sgbm_params`` (accepted by ``configure_sgbm`` like the reference
   'cost'     : 'sad' | 'ssd' | 'bt'   (block cost; north_star SAD/SSD; 'bt' is OpenCV SGBM's
                                        Birchfield-Tomasi pixel cost on the 'prefilter_cap'-clipped
                                        x-derivative plus intensity, summed over the same block)
+  'sgbm_post': bool                   (False; True runs cv2.StereoSGBM::compute's own tail on the
+                                       int16 map: 3x3 median, then filterSpeckles with
+                                       'speckle_window_size' / 'speckle_range' and newVal
+                                       (min_disp - 1) * 16)
   'subpixel' : bool                   (1/16-px parabola refinement, on by default)
   'device'   : int                    (HIP device of the matcher)
   'aggregation': 'none' | 'sgm'       ('none', the default, is the north-star block matching;
@@ -17,8 +21,10 @@ Keys added to ``sgbm_params`` (accepted by ``configure_sgbm`` like the reference
                                        the path set of 'sgbm_mode' and P1 = 8 bs^2, P2 = 32 bs^2 as
                                        _build_sgbm derives them, stereo_core.py:51-61)
 Keys of the reference that have no block-matching meaning are kept, validated and reported
-but do not change the result: 'prefilter_cap' unless 'cost' is 'bt', 'speckle_window_size',
-'speckle_range', and 'sgbm_mode' / P1 / P2 while 'aggregation' is 'none' (SURVEY.md 8a A5').
+but do not change the result: 'prefilter_cap' unless 'cost' is 'bt', 'speckle_window_size' /
+'speckle_range' unless 'sgbm_post' is set, and 'sgbm_mode' / P1 / P2 while 'aggregation' is 'none'
+(SURVEY.md 8a A5').  cost='bt' + aggregation='sgm' + sgbm_post=True is this build's closest form
+of the reference's cv2.StereoSGBM (its LR check stays the A5' one).
 
 There is no CPU fallback: without libdsx.so or a HIP device ``compute_disparity`` raises.
 """
@@ -106,6 +112,7 @@ class StereoCore:
             'subpixel': True,
             'device': 0,
             'aggregation': 'none',
+            'sgbm_post': False,
         }
         self._build_sgbm()
         self.disparity_map = None
@@ -135,6 +142,9 @@ class StereoCore:
             p1=self.P1,
             p2=self.P2,
             prefilter_cap=p['prefilter_cap'],
+            sgbm_post=bool(p.get('sgbm_post', False)),
+            speckle_window_size=p['speckle_window_size'],
+            speckle_range=p['speckle_range'],
         )
         if old is not None:
             old.close()

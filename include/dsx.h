@@ -81,7 +81,12 @@ typedef struct dsx_params {
                               /* SGM path set of 'sgbm_mode' (stereo_core.py:55-61), SAD only */
     int32_t p1, p2;           /* SGM penalties; <= 0 -> 8*bs^2 / 32*bs^2 (stereo_core.py:51-52) */
     int32_t prefilter_cap;    /* 'prefilter_cap'     (stereo_core.py:21), 1..63; DSX_COST_BT only */
-    int32_t reserved[1];
+    int32_t sgbm_post;        /* 1 = cv2.StereoSGBM::compute's own tail on the int16 map: 3x3     */
+                              /* median, then filterSpeckles(newVal (min_disp-1)*16) when          */
+                              /* speckle_window_size > 0; needs float_mode DSX_FLOAT_FIXED         */
+    int32_t speckle_window_size; /* 'speckle_window_size' (stereo_core.py:23), >= 0              */
+    int32_t speckle_range;    /* 'speckle_range'     (stereo_core.py:24), maxDiff = 16 * range   */
+    int32_t reserved[4];
 } dsx_params;
 
 typedef struct dsx_handle dsx_handle;
@@ -94,7 +99,7 @@ int dsx_device_count(int *n);
 
 /* Fill *p with the defaults of StereoCore.sgbm_params (stereo_core.py:16-39) plus the build
  * keys: min 0, num 128, block 5, SAD, uniqueness 10, disp12 1, subpixel 1, fixed floats,
- * fused path, prefilter_cap 31. */
+ * fused path, prefilter_cap 31, sgbm_post 0, speckle window 50 / range 2. */
 void dsx_default_params(dsx_params *p);
 
 /* Validate parameters without creating a handle (DSX_EINVAL + message if unsupported). */

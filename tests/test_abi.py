@@ -44,7 +44,7 @@ def test_header_compiles_as_c(tmp_path):
 
 
 def test_params_struct_layout():
-    assert ctypes.sizeof(_dsx.DsxParams) == 16 * 4
+    assert ctypes.sizeof(_dsx.DsxParams) == 22 * 4
 
 
 def test_version_and_defaults():

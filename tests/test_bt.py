@@ -1,9 +1,11 @@
-"""OpenCV SGBM's Birchfield-Tomasi pixel cost ('cost': 'bt'; VERDICT r1 missing item 6).
+"""OpenCV SGBM semantics (VERDICT r1 missing item 6): the Birchfield-Tomasi pixel cost ('cost':
+'bt') and StereoSGBM::compute's own median + speckle tail ('sgbm_post').
 
-The reference's matcher is cv2.StereoSGBM with preFilterCap = sgbm_params['prefilter_cap']
-(depthlib/stereo_core.py:63-75).  OpenCV is absent, so parity against it is unpinned: the NumPy
-restatement (oracle/bt_cost.py) is pinned by an independent loop restatement and by known answers,
-and the HIP volume (dsx_bt.hip) is checked bit-exactly against it, alone and under SGM."""
+The reference's matcher is cv2.StereoSGBM with preFilterCap = sgbm_params['prefilter_cap'] and
+speckleWindowSize / speckleRange (depthlib/stereo_core.py:63-75).  OpenCV is absent, so parity
+against it is unpinned: the NumPy restatements (oracle/bt_cost.py, oracle/sgbm_post.py) are pinned
+by independent loop restatements and known answers, and the HIP paths (dsx_bt.hip, dsx_post.hip
+launch_sgbm_post) are checked bit-exactly against them, alone and under SGM."""
 from __future__ import annotations
 
 import numpy as np
@@ -12,8 +14,9 @@ import pytest
 from depthestimation_amd import _dsx
 from depthestimation_amd.synthetic import stereo_pair
 from oracle.bt_cost import bt_bruteforce, channels, cost_volume_bt, ftzero, max_cost_bt
+from oracle.sgbm_post import filter_speckles_flood, median3_int16, sgbm_post
 from oracle.sgm import aggregate
-from oracle.stereo_bm import wta_epilogue
+from oracle.stereo_bm import stereo_bm, wta_epilogue
 
 
 @pytest.mark.parametrize("H,W,m,D,bs,cap", [
@@ -74,6 +77,41 @@ def test_stereo_core_bt_key():
     assert core.sgbm.params["cost"] == "bt" and core.sgbm.params["prefilter_cap"] == 15
     with pytest.raises(ValueError):
         core.configure_sgbm(cost="bt", prefilter_cap=99)
+
+
+def _speckly_map(H, W, seed, m=0):
+    rng = np.random.default_rng(seed)
+    d = (rng.integers(0, 6, (H, W)) * 16 + m * 16).astype(np.int16)
+    d[rng.random((H, W)) < 0.15] = (m - 1) * 16
+    d[:, : W // 5] = np.int16(m * 16 + 40)  # one large flat region
+    return d
+
+
+@pytest.mark.parametrize("seed", [0, 1, 2])
+def test_sgbm_post_oracle_pins(seed):
+    from scipy import ndimage
+    from depthestimation_amd.postprocess import filter_speckles_int16
+    d = _speckly_map(23, 41, seed)
+    np.testing.assert_array_equal(median3_int16(d), ndimage.median_filter(d, size=3, mode="nearest"))
+    for nv, size, diff in ((-16, 4, 16), (-16, 1, 0), (0, 30, 32), (-16, 0, 16)):
+        want = filter_speckles_int16(d.copy(), nv, size, diff)
+        np.testing.assert_array_equal(filter_speckles_flood(d, nv, size, diff), want)
+    # known answer: an isolated pixel of a different value is a 1-pixel speckle
+    k = np.full((5, 5), 64, np.int16)
+    k[2, 2] = 160
+    out = filter_speckles_flood(k, -16, 1, 16)
+    assert out[2, 2] == -16 and (np.delete(out.ravel(), 12) == 64).all()
+
+
+def test_sgbm_post_params():
+    p = _dsx.make_params(sgbm_post=True, speckle_window_size=100, speckle_range=32)
+    _dsx.check_params(p)
+    assert (p.sgbm_post, p.speckle_window_size, p.speckle_range) == (1, 100, 32)
+    d = _dsx.default_params()
+    assert (d.sgbm_post, d.speckle_window_size, d.speckle_range) == (0, 50, 2)
+    for kw in (dict(sgbm_post=True, float_mode="parabola"), dict(sgbm_post=True, speckle_window_size=-1)):
+        with pytest.raises(ValueError):
+            _dsx.check_params(_dsx.make_params(**kw))
 
 
 # ---------------------------------------------------------------- GPU -------------------
@@ -179,3 +217,59 @@ def test_gpu_bt_c2_size_properties():
             yy = y - lo
             if (y - 5 >= lo or lo == 0) and (y + 5 < hi or hi == 1080):
                 np.testing.assert_array_equal(got[y], ref[yy], err_msg=f"row {y}")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cost,agg,m,win,rng", [
+    ("sad", None, 0, 50, 2), ("bt", "sgbm_3way", 0, 50, 2), ("bt", "hh", 2, 20, 1), ("ssd", None, -3, 0, 2),
+    ("sad", None, 0, 400, 0),
+])
+def test_gpu_sgbm_post_matches_oracle(cost, agg, m, win, rng):
+    """The full cv2.StereoSGBM-shaped call: BT (or SAD/SSD) -> [SGM] -> epilogue -> median -> speckles."""
+    _gpu()
+    import torch
+    from depthestimation_amd.matcher import HipBlockMatcher
+    H, W, D, bs = 48, 160, 32, 5
+    L, R, _ = stereo_pair(H, W, m, D, seed=21 + win)
+    if cost == "bt":
+        C = cost_volume_bt(L, R, m, D, bs, 31)
+        if agg:
+            C = aggregate(C, agg, 8 * bs * bs, 32 * bs * bs)
+        fixed = wta_epilogue(C, m, 10, 1, True)["fixed"]
+    else:
+        fixed = stereo_bm(L, R, m, D, bs, cost, 10, 1, True)["fixed"]
+    want = sgbm_post(fixed, m, win, rng)
+    mm = HipBlockMatcher(min_disp=m, num_disp=D, block_size=bs, cost=cost, uniqueness_ratio=10, disp12_max_diff=1,
+                         aggregation=agg, p1=8 * bs * bs, p2=32 * bs * bs, sgbm_post=True,
+                         speckle_window_size=win, speckle_range=rng)
+    flt = np.empty((H, W), np.float32)
+    got = mm.compute(L, R, out_float=flt)
+    np.testing.assert_array_equal(got, want)
+    np.testing.assert_array_equal(flt, want.astype(np.float32) / 16)
+    # batch path: the tail runs per frame
+    Ld = torch.from_numpy(np.stack([L, L[::-1].copy()])).cuda()
+    Rd = torch.from_numpy(np.stack([R, R[::-1].copy()])).cuda()
+    out = torch.empty((2, H, W), dtype=torch.int16, device="cuda")
+    mm.compute_batch_device(Ld, Rd, out_fixed=out)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(out[0].cpu().numpy(), want)
+    mm.close()
+
+
+@pytest.mark.gpu
+def test_gpu_sgbm_post_stereo_core_and_large():
+    """StereoCore keys (cost 'bt', aggregation 'sgm', sgbm_post) at 720p: the tail against the
+    oracle tail applied to the same device matcher's untailed output (the flood fill is exact, only
+    slow in Python, so it runs once)."""
+    _gpu()
+    from depthestimation_amd.matcher import HipBlockMatcher
+    from depthestimation_amd.stereo_core import StereoCore
+    L, R, _ = stereo_pair(720, 1280, 0, 128, seed=4)
+    base = HipBlockMatcher(num_disp=128, block_size=5, cost="bt", aggregation="sgbm_3way", p1=200, p2=800)
+    raw = base.compute(L, R)
+    base.close()
+    core = StereoCore()
+    core.configure_sgbm(cost="bt", aggregation="sgm", sgbm_mode="sgbm_3way", sgbm_post=True)
+    got = core.compute_disparity(L, R)
+    want = sgbm_post(raw, 0, 50, 2)
+    np.testing.assert_array_equal(got, want.astype(np.float32) / 16.0)

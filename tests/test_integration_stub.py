@@ -14,7 +14,8 @@ import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 FIELDS = ("min_disp", "num_disp", "block_size", "cost", "uniqueness_ratio", "disp12_max_diff", "subpixel",
-          "float_mode", "path", "timing", "grid_blocks", "aggregation", "p1", "p2", "prefilter_cap", "reserved")
+          "float_mode", "path", "timing", "grid_blocks", "aggregation", "p1", "p2", "prefilter_cap", "sgbm_post",
+          "speckle_window_size", "speckle_range", "reserved")
 
 
 @pytest.fixture(scope="module")
