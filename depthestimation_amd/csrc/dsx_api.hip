@@ -475,7 +475,8 @@ int run(dsx_handle *h, const void *dL, const void *dR, int H, int W, int64_t str
                 b.Dp = h->g.Dp;
                 b.R = radius;
                 b.padv = pad_value(h);
-                DSX_LAUNCH(h, "cost_volume", st, dsx::launch_bt_volume(b, st));
+                DSX_LAUNCH(h, "bt_hsum", st, dsx::launch_bt_volume(b, 0, st));
+                DSX_LAUNCH(h, "bt_vsum", st, dsx::launch_bt_volume(b, 1, st));
             } else {
                 dsx::Bm2Args a = base_args(h, H, W, stride);
                 a.side = dsx::SIDE_VOLUME;

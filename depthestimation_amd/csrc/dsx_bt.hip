@@ -8,7 +8,7 @@
 // Three launches, all streaming:
 //   bt_prep : per pixel of each view, the 6 bytes BT needs - per channel the value and the min/max
 //             of it and its two half-pixel midpoints (8-B record; 16 B per pixel pair).
-//   bt_hsum : horizontal window sums of the pixel cost, Hs[y][x][d] u16: one wave per (row, 32
+//   bt_hsum : horizontal window sums of the pixel cost, Hs[y][x][d] u16: one wave per (row, 64
 //             columns, 64 disparities), lane = d; a running sum along x with the window's
 //             2R+1 pixel costs in registers (unrolled, so the ring index is a constant), the left
 //             record a scalar load, the right records one coalesced 512-B line per column.
@@ -24,7 +24,7 @@ namespace dsx {
 
 namespace {
 
-constexpr int kBtTX = 32;   // columns per bt_hsum wave
+constexpr int kBtTX = 64;   // columns per bt_hsum wave
 constexpr int kBtSeg = 32;  // rows per bt_vsum segment
 
 __device__ __forceinline__ int clampi(int v, int lo, int hi) { return v < lo ? lo : (v > hi ? hi : v); }
@@ -120,6 +120,11 @@ __global__ __launch_bounds__(256) void bt_vsum(const uint16_t *hs, int H, int W,
     const uint4 *src = reinterpret_cast<const uint4 *>(hs) + g;
     uint4 *dst = reinterpret_cast<uint4 *>(vol) + g;
     const int y0 = blockIdx.y * kBtSeg, y1 = min(H, y0 + kBtSeg);
+    if (d0 >= D) {  // padding only: nothing to read
+        const uint32_t pv = (padv & 0xFFFFu) | (padv & 0xFFFFu) << 16;
+        for (int y = y0; y < y1; ++y) dst[(int64_t)y * groups] = make_uint4(pv, pv, pv, pv);
+        return;
+    }
     u16x2 s[4] = {u16x2{0, 0}, u16x2{0, 0}, u16x2{0, 0}, u16x2{0, 0}};
 #pragma unroll
     for (int j = -R; j <= R; ++j) {
@@ -152,15 +157,17 @@ __global__ __launch_bounds__(256) void bt_vsum(const uint16_t *hs, int H, int W,
 }
 
 template <int R>
-hipError_t launch_bt_r(const BtArgs &a, hipStream_t st) {
-    const dim3 hg((a.W + kBtTX - 1) / kBtTX, a.H, a.Dp / 64);
-    hipLaunchKernelGGL(bt_hsum<R>, hg, dim3(64), 0, st, a.prepL, a.prepR, a.W, a.m, a.D, a.Dp, a.hs);
-    hipError_t e = hipGetLastError();
-    if (e != hipSuccess) return e;
-    const int64_t groups = (int64_t)a.W * (a.Dp / 8);
-    const dim3 vg((unsigned)((groups + 255) / 256), (a.H + kBtSeg - 1) / kBtSeg);
-    hipLaunchKernelGGL(bt_vsum<R>, vg, dim3(256), 0, st, a.hs, a.H, a.W, a.D, a.Dp, a.padv,
-                       static_cast<uint16_t *>(a.vol));
+hipError_t launch_bt_r(const BtArgs &a, int part, hipStream_t st) {
+    if (part == 0) {
+        // waves whose 64 disparities all lie past D have nothing to sum (vsum writes their pads)
+        const dim3 hg((a.W + kBtTX - 1) / kBtTX, a.H, (a.D + 63) / 64);
+        hipLaunchKernelGGL(bt_hsum<R>, hg, dim3(64), 0, st, a.prepL, a.prepR, a.W, a.m, a.D, a.Dp, a.hs);
+    } else {
+        const int64_t groups = (int64_t)a.W * (a.Dp / 8);
+        const dim3 vg((unsigned)((groups + 255) / 256), (a.H + kBtSeg - 1) / kBtSeg);
+        hipLaunchKernelGGL(bt_vsum<R>, vg, dim3(256), 0, st, a.hs, a.H, a.W, a.D, a.Dp, a.padv,
+                           static_cast<uint16_t *>(a.vol));
+    }
     return hipGetLastError();
 }
 
@@ -176,17 +183,17 @@ hipError_t launch_bt_prep(const uint8_t *img, int64_t pitch, int H, int W, int f
     return hipGetLastError();
 }
 
-hipError_t launch_bt_volume(const BtArgs &a, hipStream_t st) {
-    if (a.Dp % 64 != 0 || a.H < 1 || a.W < 1) return hipErrorInvalidValue;
+hipError_t launch_bt_volume(const BtArgs &a, int part, hipStream_t st) {
+    if (a.Dp % 64 != 0 || a.H < 1 || a.W < 1 || a.D > a.Dp) return hipErrorInvalidValue;
     switch (a.R) {
-        case 0: return launch_bt_r<0>(a, st);
-        case 1: return launch_bt_r<1>(a, st);
-        case 2: return launch_bt_r<2>(a, st);
-        case 3: return launch_bt_r<3>(a, st);
-        case 4: return launch_bt_r<4>(a, st);
-        case 5: return launch_bt_r<5>(a, st);
-        case 6: return launch_bt_r<6>(a, st);
-        case 7: return launch_bt_r<7>(a, st);
+        case 0: return launch_bt_r<0>(a, part, st);
+        case 1: return launch_bt_r<1>(a, part, st);
+        case 2: return launch_bt_r<2>(a, part, st);
+        case 3: return launch_bt_r<3>(a, part, st);
+        case 4: return launch_bt_r<4>(a, part, st);
+        case 5: return launch_bt_r<5>(a, part, st);
+        case 6: return launch_bt_r<6>(a, part, st);
+        case 7: return launch_bt_r<7>(a, part, st);
         default: return hipErrorInvalidValue;
     }
 }

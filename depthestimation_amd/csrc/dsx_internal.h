@@ -172,7 +172,8 @@ struct BtArgs {
 };
 size_t bt_workspace(int H, int W, int Dp);
 hipError_t launch_bt_prep(const uint8_t *img, int64_t pitch, int H, int W, int ftz, uint2 *out, hipStream_t st);
-hipError_t launch_bt_volume(const BtArgs &a, hipStream_t st);
+// part 0: horizontal sums (bt_hsum), part 1: vertical sums into the volume (bt_vsum)
+hipError_t launch_bt_volume(const BtArgs &a, int part, hipStream_t st);
 
 // Rectification (dsx_rectify.hip): gray conversion fused with the fixed-point bilinear remap.
 struct RectArgs {
