@@ -73,6 +73,14 @@ __device__ __forceinline__ int mad_i24(int a, int b, int c) {
     asm("v_mad_i32_i24 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
     return r;
 }
+// min(src of lane l-1, key) with lane 0 keeping key: one v_min_u32_dpp wave_shr:1 whose disabled lane
+// (bound_ctrl off) keeps the tied key.  Written out because hipcc re-associates the builtin form into
+// v_mov -1 + v_mov_dpp + v_min3 (3 VALU for the pair of slot minima instead of 2).  s_nop 1: the DPP
+// source may have been written by the previous VALU (2 wait states on gfx9).
+__device__ __forceinline__ uint32_t min_shr1(uint32_t src, uint32_t key) {
+    asm("s_nop 1\n\tv_min_u32_dpp %0, %1, %0 wave_shr:1 row_mask:0xf bank_mask:0xf" : "+v"(key) : "v"(src));
+    return key;
+}
 __host__ __device__ constexpr int rnd16(int v) { return (v + 15) & ~15; }
 
 template <int R, bool SSD, int NW>
@@ -86,6 +94,7 @@ struct Geo {
     static constexpr int TPP = NT / TX;       // epilogue lanes per pixel (2*NW)
     static constexpr int DSL = Dp / TPP;      // disparities per epilogue lane (64 SAD, 32 SSD)
     static constexpr int CB = SSD ? 4 : 2;    // cost bytes
+    // 16 B of row padding (LDS banks; the SAD LR pass parks one exit key per wave there, NW <= 4)
     static constexpr int PITCH = Dp * CB + 16;
     static constexpr int NJ = NC + Dp;        // S entries per staged row
     static constexpr int REFW = rnd16(NC + 4);  // >= 4 * ceil(NC / 4)
@@ -605,16 +614,26 @@ __device__ __forceinline__ void bm2_segment(const Bm2Args &a, uint8_t *smem, int
                 // right pixel xr collects keys (C << s | d) from (x, d) with x - m - d = xr.  Each
                 // lane keeps the running key minimum of the diagonal through its slot(s); moving to
                 // pixel k+1 a diagonal moves one disparity up (SAD: odd slot <- even slot, even slot
-                // <- odd slot of lane-1).  One DPP wave_ror:1 does that move and hands the diagonal
-                // leaving the wave's top disparity to lane 0, from where a wave_shr:1 FIFO (E)
-                // collects it; after the row every partial minimum is combined across strips with a
-                // global atomicMin.  Keys of disparities >= D (Dp padding) are forced to ~0 through
-                // the byte-permute selector (selector byte 13 = 0xFF).
+                // <- odd slot of lane-1; SSD: the slot of lane-1).  After the row every partial
+                // minimum is combined across strips with a global atomicMin.  Keys of disparities
+                // >= D (Dp padding) are forced to ~0 through the byte-permute selector (selector
+                // byte 13 = 0xFF) / the d mask.
+                //   SAD: the move is one v_min_u32_dpp wave_shr:1 (min_shr1: lane 0 keeps the new
+                //        key) and the diagonal leaving the wave's top slot (lane 63) at pixel k is
+                //        parked by that lane in the padding of tile row k (single-lane LDS store, no
+                //        VALU); lanes 0..TX-2 pick the exits up after the row.  4 VALU per pixel
+                //        for the two slots, against 7 for the register FIFO below.
+                //   SSD: DPP wave_ror:1 hands the leaving diagonal to lane 0, from where a
+                //        wave_shr:1 FIFO (E) collects it.  (The LDS exits measured slower here: the
+                //        4-wave SSD pass is at its 128-VGPR budget and spilled more, C3 +9 %.)
+                static_assert(SSD || NW <= 4, "SAD exit slots: 16 B of padding per tile row");
                 const int ks = a.kshift;
                 const uint32_t selE = d0 < D ? 0x05040100u : 0x0D0D0D0Du;
                 const uint32_t selO = d0 + 1 < D ? 0x07060100u : 0x0D0D0D0Du;
                 const uint32_t dmE = d0 < D ? (uint32_t)d0 : 0xFFFFFFFFu;
                 const bool lane0 = ln == 0;
+                const bool top = ln == 63;
+                uint8_t *xq = tile + Dp * CB + 4 * wv;  // SAD: this wave's exit slot in each tile row's padding
                 uint32_t Ae = 0xFFFFFFFFu, Ao = 0xFFFFFFFFu, E = 0xFFFFFFFFu;
                 // FULL: the strip lies inside the image and every lane owns real disparities
                 // (D == Dp), so the per-pixel bounds / lane checks drop out of the unrolled loop
@@ -631,29 +650,53 @@ __device__ __forceinline__ void bm2_segment(const Bm2Args &a, uint8_t *smem, int
                             if constexpr (SSD) *reinterpret_cast<uint32_t *>(tb + k * PITCH) = abits(acc);
                             else *reinterpret_cast<uint32_t *>(tb + k * PITCH) = as1(acc);
                         }
-                        if (FULL || x0 + k < W) {
-                            if constexpr (SSD) {
-                                Ae = umin2(Ae, (abits(acc) << ks) | dmE);
-                            } else {  // (C << 16) | d by byte permute
-                                Ae = umin2(Ae, __builtin_amdgcn_perm(as1(acc), (uint32_t)d0, selE));
-                                Ao = umin2(Ao, __builtin_amdgcn_perm(as1(acc), (uint32_t)(d0 + 1), selO));
+                        if constexpr (SSD) {
+                            if (FULL || x0 + k < W) Ae = umin2(Ae, (abits(acc) << ks) | dmE);
+                            if (k < TX - 1) {
+                                const uint32_t F = (uint32_t)__builtin_amdgcn_mov_dpp((int)Ae, 0x13C, 0xF, 0xF, false);  // wave_ror:1
+                                E = (uint32_t)__builtin_amdgcn_update_dpp((int)F, (int)E, 0x138, 0xF, 0xF, false);  // wave_shr:1, lane 0 <- F
+                                Ae = lane0 ? 0xFFFFFFFFu : F;
                             }
-                        }
-                        if (k < TX - 1) {
-                            const uint32_t top = SSD ? Ae : Ao;
-                            const uint32_t F = (uint32_t)__builtin_amdgcn_mov_dpp((int)top, 0x13C, 0xF, 0xF, false);  // wave_ror:1
-                            E = (uint32_t)__builtin_amdgcn_update_dpp((int)F, (int)E, 0x138, 0xF, 0xF, false);  // wave_shr:1, lane 0 <- F
-                            if constexpr (!SSD) Ao = Ae;
-                            Ae = lane0 ? 0xFFFFFFFFu : F;
+                        } else {
+                            // (C << 16) | d by byte permute
+                            const uint32_t kE = __builtin_amdgcn_perm(as1(acc), (uint32_t)d0, selE);
+                            const uint32_t kO = __builtin_amdgcn_perm(as1(acc), (uint32_t)(d0 + 1), selO);
+                            if constexpr (FULL) {
+                                if (k > 0) {
+                                    const uint32_t nE = min_shr1(Ao, kE);
+                                    Ao = umin2(Ae, kO);
+                                    Ae = nE;
+                                } else {
+                                    Ae = kE;
+                                    Ao = kO;
+                                }
+                            } else {
+                                if (k > 0) {  // one disparity up: wave_shr:1, lane 0 <- ~0
+                                    const uint32_t sh = (uint32_t)__builtin_amdgcn_update_dpp(-1, (int)Ao, 0x138, 0xF, 0xF, false);
+                                    Ao = Ae;
+                                    Ae = sh;
+                                }
+                                if (x0 + k < W) {
+                                    Ae = umin2(Ae, kE);
+                                    Ao = umin2(Ao, kO);
+                                }
+                            }
+                            if (k < TX - 1 && top) *reinterpret_cast<uint32_t *>(xq + k * PITCH) = Ao;  // exit
                         }
                     }
                 };
                 if (x0 + TX <= W && D == Dp) diag_loop(std::true_type{});
                 else diag_loop(std::false_type{});
                 uint32_t *krow = a.lr_keys + fout + (long)y * W;
-                const int dtop = (wv + 1) * G::LDW - 1;            // disparity of the wave's top slot
-                const int xe = x0 + (TX - 2 - ln) - m - dtop;       // E lane j: exit of pixel TX-2-j
-                if (ln < TX - 1 && E != 0xFFFFFFFFu && xe >= 0 && xe < W) atomicMin(krow + xe, E);
+                const int dtop = (wv + 1) * G::LDW - 1;  // disparity of the wave's top slot
+                if constexpr (SSD) {
+                    const int xe = x0 + (TX - 2 - ln) - m - dtop;  // E lane j: exit of pixel TX-2-j
+                    if (ln < TX - 1 && E != 0xFFFFFFFFu && xe >= 0 && xe < W) atomicMin(krow + xe, E);
+                } else if (ln < TX - 1) {
+                    E = *reinterpret_cast<const uint32_t *>(xq + ln * PITCH);  // exit of pixel ln, parked in LDS
+                    const int xe = x0 + ln - m - dtop;
+                    if (E != 0xFFFFFFFFu && xe >= 0 && xe < W) atomicMin(krow + xe, E);
+                }
                 const int xa = x0 + TX - 1 - m - d0;
                 if (Ae != 0xFFFFFFFFu && xa >= 0 && xa < W) atomicMin(krow + xa, Ae);
                 if constexpr (!SSD) {
