@@ -35,6 +35,9 @@
 // Register budget (waves per SIMD) the fused pass is compiled for, measured per cost (r01e): SAD at 4
 // waves spills in the row loop (C2 +45 %); SSD blocks of >= 4 waves (D > 128) gain at 4 despite init
 // spills (C3 392 -> 350 us); other SSD shapes were not measured and keep 3.
+#ifndef DSX_LR_KEYS  // key-tree argmin on the LR pass (experiment switch)
+#define DSX_LR_KEYS 1
+#endif
 #ifndef DSX_WPE
 #define DSX_WPE 3
 #endif
@@ -766,7 +769,7 @@ __device__ __forceinline__ void bm2_segment(const Bm2Args &a, uint8_t *smem, int
             // Two argmin forms, chosen per instantiation from measurements (r01e): the key tree
             // wins on the LR pass (C3, C4) and 15x15 windows (C5); the compare/select scan keeps
             // the SIDE 0 pass at <= 11x11 at 151 VGPRs (the key tree costs C2 +7 %).
-            constexpr bool KEYS = SIDE == 3 || R >= 6;
+            constexpr bool KEYS = (SIDE == 3 && DSX_LR_KEYS) || R >= 6;
             uint32_t cb, dl;
             if constexpr (KEYS) {
                 // lowest-d argmin without compare/select scans: keys (cost << GB | global block) give
