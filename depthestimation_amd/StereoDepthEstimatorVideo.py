@@ -54,9 +54,12 @@ class StereoDepthEstimatorVideo:
         self.core.configure_sgbm(**kwargs)
 
     def _frames(self):
+        """This rank's frame pairs: the others are skipped at the source without being decoded
+        (every rank used to decode every frame and drop the ones it did not own)."""
+        r, n = (0, 1) if self.devices else (self.rank, self.world_size)
         if self.use_threading:
             cap = ThreadedStereoCapture(self.left_source, self.right_source, downscale_factor=self.downscale_factor,
-                                        drop_frames=self.drop_frames)
+                                        drop_frames=self.drop_frames, rank=r, world_size=n)
             cap.start()
             try:
                 while True:
@@ -67,7 +70,8 @@ class StereoDepthEstimatorVideo:
             finally:
                 cap.stop()
         else:
-            yield from stereo_stream(self.left_source, self.right_source, downscale_factor=self.downscale_factor)
+            yield from stereo_stream(self.left_source, self.right_source, downscale_factor=self.downscale_factor,
+                                     rank=r, world_size=n)
 
     def estimate_depth(self):
         """Yields depth_m per frame (this rank's frames when sharded)."""
@@ -80,9 +84,7 @@ class StereoDepthEstimatorVideo:
             yield from self._estimate_multi_device()
             return
         frame_start_time = time.time()
-        for i, (left_frame, right_frame) in enumerate(self._frames()):
-            if i % self.world_size != self.rank:
-                continue
+        for left_frame, right_frame in self._frames():  # this rank's frames only
             _, depth_m = self.core.estimate_depth(left_frame, right_frame)
             yield depth_m
             if self._frame_interval > 0:

@@ -3,7 +3,9 @@
 A background thread reads frame pairs into a bounded queue (maxsize ``buffer_size``); with
 ``drop_frames`` the oldest pair is discarded when the queue is full (live cameras), without
 it the producer blocks (files: every frame is processed). ``read()`` returns None once the
-stream has ended and the queue is drained.
+stream has ended and the queue is drained. ``rank`` / ``world_size`` (an extension for frame
+sharding): the producer decodes only pairs i with i % world_size == rank and skips
+the others with ``grab()``.
 """
 from __future__ import annotations
 
@@ -17,7 +19,11 @@ from .input import open_capture, resize_area
 
 
 class ThreadedStereoCapture:
-    def __init__(self, left_source, right_source, downscale_factor=1.0, buffer_size=2, drop_frames=True):
+    def __init__(self, left_source, right_source, downscale_factor=1.0, buffer_size=2, drop_frames=True,
+                 rank=0, world_size=1):
+        if world_size < 1 or not 0 <= rank < world_size:
+            raise ValueError(f"rank {rank} outside world_size {world_size}")
+        self.rank, self.world_size = int(rank), int(world_size)
         self.left_source = left_source
         self.right_source = right_source
         self.downscale_factor = downscale_factor
@@ -45,10 +51,18 @@ class ThreadedStereoCapture:
         return frame
 
     def _capture_loop(self):
+        i = 0
         while not self._stop_event.is_set():
             if self._cap_L is None or self._cap_R is None:
                 self._stop_event.set()
                 break
+            if i % self.world_size != self.rank:  # another rank's pair: skip without decoding
+                i += 1
+                if not (self._cap_L.grab() and self._cap_R.grab()):
+                    self._stop_event.set()
+                    break
+                continue
+            i += 1
             left = self._read_frame(self._cap_L)
             right = self._read_frame(self._cap_R)
             if left is None or right is None:

@@ -267,6 +267,41 @@ def test_open_capture_errors_and_streams(tmp_path):
         list(stereo_stream(list(frames), list(frames), downscale_factor=2.0))
 
 
+def test_sharded_stream_skips_without_decoding(tmp_path, monkeypatch):
+    """Frame sharding at the source: rank r of N decodes only pairs i % N == r (the others are
+    grabbed, not decoded), for .npy stacks, image directories and plain iterables."""
+    from PIL import Image
+
+    import depthestimation_amd.input as inp
+
+    frames = np.stack([np.full((4, 6, 3), 10 * i, np.uint8) for i in range(7)])
+    np.save(tmp_path / "v.npy", frames)
+    d = tmp_path / "imgs"
+    d.mkdir()
+    for i, f in enumerate(frames):
+        Image.fromarray(f).save(d / f"{i:03d}.png")
+    calls = []
+    real = inp._imread_rgb
+    monkeypatch.setattr(inp, "_imread_rgb", lambda p: (calls.append(p), real(p))[1])
+    for rank in range(3):
+        for src in (str(tmp_path / "v.npy"), str(d), list(frames)):
+            calls.clear()
+            got = [int(l[0, 0, 0]) for l, _ in stereo_stream(src, src, rank=rank, world_size=3)]
+            assert got == [10 * i for i in range(rank, 7, 3)]
+            if src == str(d):  # left + right decoded for own frames only
+                assert len(calls) == 2 * len(got)
+    with pytest.raises(ValueError):
+        list(stereo_stream(list(frames), list(frames), rank=2, world_size=2))
+    cap = ThreadedStereoCapture(str(d), str(d), drop_frames=False, rank=1, world_size=2)
+    calls.clear()
+    cap.start()
+    got = []
+    while (p := cap.read()) is not None:
+        got.append(int(p[0][0, 0, 0]))
+    cap.stop()
+    assert got == [10, 30, 50] and len(calls) == 6
+
+
 @pytest.mark.parametrize("drop", [False, True])
 def test_threaded_capture_order(drop):
     frames = [np.full((4, 4), i, np.uint8) for i in range(20)]
