@@ -37,9 +37,20 @@ int bits_for(int n) {  // smallest b with (1 << b) >= n
 
 // bm2 geometry: SAD lanes own disparity pairs (Dp = 128 * nw, nw in {1,2,4}); SSD lanes own
 // one disparity (Dp = 64 * nw, nw in {1,2,4,8}).  K2 (vol_wta) reuses Dp with 32-d slices.
-bool pick_geometry(int D, int cost, dsx::Geometry &g) {
-    const int unit = cost == DSX_COST_SSD ? 64 : 128;
-    const int maxnw = cost == DSX_COST_SSD ? 8 : 4;
+// SAD with D <= 64 on the fused path takes the SSD layout with u32 |.| sums (BM_SAD1, Dp = 64): the
+// pair layout would spend half of every wave on padding disparities.  DSX_NO_SAD1=1 disables it.
+bool pick_geometry(const dsx_params &p, dsx::Geometry &g) {
+    const int D = p.num_disp, cost = p.cost;
+    static const bool no_sad1 = [] {
+        const char *e = getenv("DSX_NO_SAD1");
+        return e && *e == '1';
+    }();
+    const bool sad1 = !no_sad1 && cost == DSX_COST_SAD && D <= 64 && p.path == DSX_PATH_FUSED &&
+                      p.aggregation == DSX_AGG_NONE;
+    const bool lane1 = cost == DSX_COST_SSD || sad1;  // one disparity per lane
+    g.kind = cost == DSX_COST_SSD ? dsx::BM_SSD : (sad1 ? dsx::BM_SAD1 : dsx::BM_SAD);
+    const int unit = lane1 ? 64 : 128;
+    const int maxnw = lane1 ? 8 : 4;
     int nw = 1;
     while (nw * unit < D) nw *= 2;
     if (nw > maxnw) return false;
@@ -105,7 +116,7 @@ int check(const dsx_params *p) {
             return fail(DSX_EINVAL, "SGM penalties must satisfy 0 < P1 <= P2 <= 65535");
     }
     dsx::Geometry g;
-    if (!pick_geometry(p->num_disp, p->cost, g)) return fail(DSX_EINVAL, "num_disp too large");
+    if (!pick_geometry(*p, g)) return fail(DSX_EINVAL, "num_disp too large");
     if (max_cost(*p) >= (1ull << (32 - g.DB)) - 1)
         return fail(DSX_EINVAL, "block_size/cost/num_disp combination exceeds the 32-bit (cost<<DB|d) key");
     return DSX_OK;
@@ -371,7 +382,7 @@ int run_right_pass(dsx_handle *h, const void *dL, const void *dR, int H, int W, 
     a.src = static_cast<const uint8_t *>(dL);
     a.out_dR = out;
     const int radius = h->p.block_size / 2;
-    DSX_LAUNCH(h, "bm_pass_right", st, dsx::launch_bm2(radius, h->p.cost == DSX_COST_SSD, h->g.NW, a, st));
+    DSX_LAUNCH(h, "bm_pass_right", st, dsx::launch_bm2(radius, h->g.kind, h->g.NW, a, st));
     return DSX_OK;
 }
 
@@ -404,7 +415,7 @@ int run(dsx_handle *h, const void *dL, const void *dR, int H, int W, int64_t str
             a.side = dsx::SIDE_LEFT_LR;
             a.lr_keys = h->lrKeys + (size_t)h->lrParity * H * W * h->lrFrames;
             a.dstar = h->dStar;
-            a.kshift = ssd ? h->g.DB : 16;
+            a.kshift = h->g.kind != dsx::BM_SAD ? h->g.DB : 16;  // u32 layouts: (C << DB) | d
         } else {
             // only strips meeting the valid band [m + D - 1, W - 1 + m] need a search
             // (stereo_core.py:168 crops the rest)
@@ -423,7 +434,7 @@ int run(dsx_handle *h, const void *dL, const void *dR, int H, int W, int64_t str
         if (tlpath && *tlpath) DSX_HIP(hipMalloc(&tl, 12 * 8 * 65536));
         if (tl) DSX_HIP(hipMemsetAsync(tl, 0, 12 * 8 * 65536, st));
         a.timeline = tl;
-        DSX_LAUNCH(h, "bm_pass_left", st, dsx::launch_bm2(radius, ssd, h->g.NW, a, st));
+        DSX_LAUNCH(h, "bm_pass_left", st, dsx::launch_bm2(radius, h->g.kind, h->g.NW, a, st));
         if (lr) {
             // this call dirties nframes frames of half P; lr_fixup resets every dirty frame of
             // the other half (consumed by the previous call), however many frames that call had
@@ -483,7 +494,7 @@ int run(dsx_handle *h, const void *dL, const void *dR, int H, int W, int64_t str
                 a.ref = static_cast<const uint8_t *>(dL) + f * frame_stride;
                 a.src = static_cast<const uint8_t *>(dR) + f * frame_stride;
                 a.vol = h->vol;
-                DSX_LAUNCH(h, "cost_volume", st, dsx::launch_bm2(radius, ssd, h->g.NW, a, st));
+                DSX_LAUNCH(h, "cost_volume", st, dsx::launch_bm2(radius, ssd ? dsx::BM_SSD : dsx::BM_SAD, h->g.NW, a, st));
             }
             const bool agg = h->p.aggregation != DSX_AGG_NONE;
             const bool agg_all = agg && sgm_concurrent(h);
@@ -632,7 +643,7 @@ int dsx_create(int device, const dsx_params *p, dsx_handle **out) {
     dsx_handle *h = new dsx_handle();
     h->device = device;
     h->p = *p;
-    pick_geometry(p->num_disp, p->cost, h->g);
+    pick_geometry(*p, h->g);
     hipError_t e = hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking);
     if (e != hipSuccess) {
         delete h;
@@ -650,7 +661,7 @@ int dsx_set_params(dsx_handle *h, const dsx_params *p) {
     DSX_HIP(hipSetDevice(h->device));
     DSX_HIP(hipStreamSynchronize(h->stream));
     h->p = *p;
-    pick_geometry(p->num_disp, p->cost, h->g);
+    pick_geometry(*p, h->g);
     return DSX_OK;
 }
 

@@ -163,7 +163,7 @@ typedef const __attribute__((address_space(4))) uint32_t cu32;
 // image (one unaligned dword + one byte load per lane and row); otherwise replicate-clamped
 // byte loads. All per-row state is in plain registers (no structs / arrays with runtime
 // indices, which hipcc would demote to scratch).
-template <int R, bool SSD, int NW, int SIDE, bool FAST>
+template <int R, bool SSD, int NW, int SIDE, bool FAST, bool ABS>
 __device__ __forceinline__ void bm2_segment(const Bm2Args &a, uint8_t *smem, int x0, int yb, int ye, long fin, long fout,
                                             bool lr_on, int done0, const int (&pe)[3], int &qcur
 #ifdef DSX_STAMPS
@@ -181,7 +181,9 @@ __device__ __forceinline__ void bm2_segment(const Bm2Args &a, uint8_t *smem, int
     // (SSD R <= 5: 121 * 255^2 = 7.87M) the f32 value 2^23 + box has ulp 1 and its bit pattern is
     // OFF + box, monotone as u32, so the tile and the LR keys take the raw bits (OFF's set bits
     // lie above 23 + DB and leave the (C << DB | d) order intact); the epilogue subtracts OFF.
-    constexpr bool FSS = SSD && R <= 5 && (SIDE == 0 || SIDE == 3);
+    // ABS (SAD1): SAD with the SSD layout (one disparity per lane, u32 column / box sums) for D <= 64,
+    // where the packed pairs would leave half of the wave on padding disparities
+    constexpr bool FSS = SSD && !ABS && R <= 5 && (SIDE == 0 || SIDE == 3);
     constexpr uint32_t OFF = FSS ? 0x4B000000u : 0u;
     typedef typename std::conditional<FSS, float, typename std::conditional<SSD, uint32_t, u16x2>::type>::type acc_t;
     uint8_t *tile = smem + 4 * SLOT;
@@ -488,6 +490,8 @@ __device__ __forceinline__ void bm2_segment(const Bm2Args &a, uint8_t *smem, int
                     if constexpr (FSS) {
                         const float t = rf8[c] - __uint_as_float(sw[c]);
                         cs[c0 + c] = __builtin_fmaf(t, t, cs[c0 + c]);
+                    } else if constexpr (ABS) {
+                        cs[c0 + c] = __builtin_amdgcn_sad_u16(refv(rw, c), sw[c], cs[c0 + c]);  // + |ref - src|
                     } else if constexpr (SSD) {
                         const int t = (int)refv(rw, c) - (int)sw[c];
                         cs[c0 + c] += (uint32_t)__mul24(t, t);  // v_mul_i32_i24: |t| <= 255
@@ -579,7 +583,10 @@ __device__ __forceinline__ void bm2_segment(const Bm2Args &a, uint8_t *smem, int
 #pragma unroll
                 for (int c = 0; c < 8; ++c) {
                     if (c0 + c < NC) {
-                        if constexpr (SSD) {  // u32 SSD (R > 5 or the right / volume passes)
+                        if constexpr (ABS) {  // cs + |tn| - |to|: two v_sad_u16 (bytes) + one v_sub
+                            cs[c0 + c] = __builtin_amdgcn_sad_u16(refv(rn, c), sn[c], cs[c0 + c]) -
+                                         __builtin_amdgcn_sad_u16(refv(ro, c), so[c], 0u);
+                        } else if constexpr (SSD) {  // u32 SSD (R > 5 or the right / volume passes)
                             const int tn = (int)refv(rn, c) - (int)sn[c];
                             const int to = (int)refv(ro, c) - (int)so[c];
                             const int nto = (int)so[c] - (int)refv(ro, c);
@@ -912,7 +919,7 @@ __device__ __forceinline__ void bm2_segment(const Bm2Args &a, uint8_t *smem, int
     }
 }
 
-template <int R, bool SSD, int NW, int SIDE>
+template <int R, bool SSD, int NW, int SIDE, bool ABS>
 __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu((SSD && NW >= 4) ? DSX_WPE_SSD : DSX_WPE))) void bm2(Bm2Args a) {
     using G = Geo<R, SSD, NW>;
     constexpr int TX = G::TX, NT = G::NT, NC = G::NC, NJ = G::NJ;
@@ -971,13 +978,13 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu((SSD &&
         const bool fast = (side == 1 ? (PB >= 0 && PB + 4 * NJ4 <= W - 1) : (PB - 4 * NJ4 >= 0 && PB <= W - 1)) &&
                           x0 - R >= 0 && x0 - R + 4 * ((NC + 3) / 4) - 1 <= W - 1;
         if (fast)
-            bm2_segment<R, SSD, NW, SIDE, true>(a, smem, x0, yb, ye, fin, fout, lr_on, done0, pe, qcur
+            bm2_segment<R, SSD, NW, SIDE, true, ABS>(a, smem, x0, yb, ye, fin, fout, lr_on, done0, pe, qcur
 #ifdef DSX_STAMPS
                                                 , ph, t_prev, nsteps
 #endif
             );
         else
-            bm2_segment<R, SSD, NW, SIDE, false>(a, smem, x0, yb, ye, fin, fout, lr_on, done0, pe, qcur
+            bm2_segment<R, SSD, NW, SIDE, false, ABS>(a, smem, x0, yb, ye, fin, fout, lr_on, done0, pe, qcur
 #ifdef DSX_STAMPS
                                                  , ph, t_prev, nsteps
 #endif
@@ -1055,10 +1062,10 @@ static hipError_t bm2_partition_dev(const PartKey &k, int TX, const int **out) {
     return hipSuccess;
 }
 
-template <int R, bool SSD, int NW, int SIDE>
+template <int R, bool SSD, int NW, int SIDE, bool ABS = false>
 static hipError_t launch_bm2_side(const Bm2Args &a, hipStream_t st) {
     using G = Geo<R, SSD, NW>;
-    const void *fn = (const void *)bm2<R, SSD, NW, SIDE>;
+    const void *fn = (const void *)bm2<R, SSD, NW, SIDE, ABS>;
     static int blocks_per_cu[64] = {};
     static int num_cu[64] = {};
     int dev = 0;
@@ -1128,7 +1135,7 @@ static hipError_t launch_bm2_side(const Bm2Args &a, hipStream_t st) {
         e = bm2_partition_dev(k, G::TX, &la.part);
         if (e != hipSuccess) return e;
     }
-    hipLaunchKernelGGL((bm2<R, SSD, NW, SIDE>), dim3((unsigned)grid), dim3(G::NT), G::SMEM, st, la);
+    hipLaunchKernelGGL((bm2<R, SSD, NW, SIDE, ABS>), dim3((unsigned)grid), dim3(G::NT), G::SMEM, st, la);
     return hipGetLastError();
 }
 
@@ -1142,9 +1149,21 @@ static hipError_t launch_bm2_one(const Bm2Args &a, hipStream_t st) {
     }
 }
 
+// SAD1 (kind BM_SAD1): fused left / right passes only (pick_geometry never selects it for the volume)
 template <int R>
-static hipError_t launch_bm2_r(bool ssd, int nw, const Bm2Args &a, hipStream_t st) {
-    if (!ssd) {
+static hipError_t launch_bm2_sad1(const Bm2Args &a, hipStream_t st) {
+    switch (a.side) {
+        case 0: return launch_bm2_side<R, true, 1, 0, true>(a, st);
+        case 1: return launch_bm2_side<R, true, 1, 1, true>(a, st);
+        case 3: return launch_bm2_side<R, true, 1, 3, true>(a, st);
+        default: return hipErrorInvalidValue;
+    }
+}
+
+template <int R>
+static hipError_t launch_bm2_r(int kind, int nw, const Bm2Args &a, hipStream_t st) {
+    if (kind == BM_SAD1) return nw == 1 ? launch_bm2_sad1<R>(a, st) : hipErrorInvalidValue;
+    if (kind == BM_SAD) {
         switch (nw) {
             case 1: return launch_bm2_one<R, false, 1>(a, st);
             case 2: return launch_bm2_one<R, false, 2>(a, st);
@@ -1161,27 +1180,27 @@ static hipError_t launch_bm2_r(bool ssd, int nw, const Bm2Args &a, hipStream_t s
     return hipErrorInvalidValue;
 }
 
-#define DSX_DECL_BM2(r) hipError_t launch_bm2_radius_##r(bool, int, const Bm2Args &, hipStream_t);
+#define DSX_DECL_BM2(r) hipError_t launch_bm2_radius_##r(int, int, const Bm2Args &, hipStream_t);
 DSX_DECL_BM2(0) DSX_DECL_BM2(1) DSX_DECL_BM2(2) DSX_DECL_BM2(3)
 DSX_DECL_BM2(4) DSX_DECL_BM2(5) DSX_DECL_BM2(6) DSX_DECL_BM2(7)
 
 #ifdef DSX_RADIUS
 #define DSX_CAT2(x, y) x##y
 #define DSX_CAT(x, y) DSX_CAT2(x, y)
-hipError_t DSX_CAT(launch_bm2_radius_, DSX_RADIUS)(bool ssd, int nw, const Bm2Args &a, hipStream_t st) {
-    return launch_bm2_r<DSX_RADIUS>(ssd, nw, a, st);
+hipError_t DSX_CAT(launch_bm2_radius_, DSX_RADIUS)(int kind, int nw, const Bm2Args &a, hipStream_t st) {
+    return launch_bm2_r<DSX_RADIUS>(kind, nw, a, st);
 }
 #else
-hipError_t launch_bm2(int radius, bool ssd, int nw, const Bm2Args &a, hipStream_t st) {
+hipError_t launch_bm2(int radius, int kind, int nw, const Bm2Args &a, hipStream_t st) {
     switch (radius) {
-        case 0: return launch_bm2_radius_0(ssd, nw, a, st);
-        case 1: return launch_bm2_radius_1(ssd, nw, a, st);
-        case 2: return launch_bm2_radius_2(ssd, nw, a, st);
-        case 3: return launch_bm2_radius_3(ssd, nw, a, st);
-        case 4: return launch_bm2_radius_4(ssd, nw, a, st);
-        case 5: return launch_bm2_radius_5(ssd, nw, a, st);
-        case 6: return launch_bm2_radius_6(ssd, nw, a, st);
-        case 7: return launch_bm2_radius_7(ssd, nw, a, st);
+        case 0: return launch_bm2_radius_0(kind, nw, a, st);
+        case 1: return launch_bm2_radius_1(kind, nw, a, st);
+        case 2: return launch_bm2_radius_2(kind, nw, a, st);
+        case 3: return launch_bm2_radius_3(kind, nw, a, st);
+        case 4: return launch_bm2_radius_4(kind, nw, a, st);
+        case 5: return launch_bm2_radius_5(kind, nw, a, st);
+        case 6: return launch_bm2_radius_6(kind, nw, a, st);
+        case 7: return launch_bm2_radius_7(kind, nw, a, st);
         default: return hipErrorInvalidValue;
     }
 }

@@ -15,6 +15,7 @@ constexpr int kVolThreads = 256;    // K2 (volume WTA) block size
 //   DB : key shift bits for K2's packed (cost << DB | d) keys
 struct Geometry {
     int NW, Dp, TX, TPP, DB;
+    int kind;  // BM_SAD / BM_SSD / BM_SAD1 (the fused passes' cost layout)
 };
 
 // Arguments of the fused pass kernel bm2 (dsx_bm.hip).
@@ -77,7 +78,10 @@ __device__ __forceinline__ int div_trunc_small(int num, int den2) {
 }
 
 // nw = waves per block: SAD Dp = 128*nw (nw in {1,2,4}), SSD Dp = 64*nw (nw in {1,2,4,8}).
-hipError_t launch_bm2(int radius, bool ssd, int nw, const Bm2Args &a, hipStream_t st);
+// bm2 cost layouts: SAD disparity pairs (u16), SSD one disparity per lane (u32), SAD1 = SAD in the SSD
+// layout (u32 sums, one disparity per lane; fused passes with D <= 64, pick_geometry in dsx_api.hip)
+enum { BM_SAD = 0, BM_SSD = 1, BM_SAD1 = 2 };
+hipError_t launch_bm2(int radius, int kind, int nw, const Bm2Args &a, hipStream_t st);
 hipError_t launch_volume_wta(int TX, bool ssd, const VolArgs &a, hipStream_t st);
 // LR check after the left pass: invalidate x where |dR(x - m - d*) - d*| > lr over `rows` rows
 // (frames stacked), reading this call's key buffer and resetting the first `reset_rows` rows of

@@ -35,14 +35,19 @@ MIX = os.path.join(ROOT, "profiles", "valu_mix.json")
 N_SIMD = 1024  # 256 CUs x 4 SIMDs (MI355X)
 
 # the instantiations bench.py runs (BASELINE configs, fused path): (radius, SSD, NW, SIDE)
+# (radius, SSD layout, NW, SIDE, ABS): ABS = SAD in the one-disparity-per-lane u32 layout (BM_SAD1, D <= 64)
 BENCH_KERNELS = {
-    "c1": (2, False, 1, 0), "c2": (4, False, 1, 0), "c3": (5, True, 4, 3), "c4": (2, False, 1, 3),
-    "c5": (7, False, 2, 0), "c2r": (4, False, 1, 3),
+    "c1": (2, True, 1, 0, True), "c2": (4, False, 1, 0, False), "c3": (5, True, 4, 3, False),
+    "c4": (2, False, 1, 3, False), "c5": (7, False, 2, 0, False), "c2r": (4, False, 1, 3, False),
 }
 
 
-def symbol(r, ssd, nw, side):
-    return f"_ZN3dsx3bm2ILi{r}ELb{int(ssd)}ELi{nw}ELi{side}EEEvNS_7Bm2ArgsE"
+def symbol(r, ssd, nw, side, abs_=False):
+    return f"_ZN3dsx3bm2ILi{r}ELb{int(ssd)}ELi{nw}ELi{side}ELb{int(abs_)}EEEvNS_7Bm2ArgsE"
+
+
+def kernel_label(r, ssd, nw, side, abs_=False):
+    return f"bm2<R={r},{'SAD1' if abs_ else ('SSD' if ssd else 'SAD')},NW={nw},SIDE={side}>"
 
 
 def base_op(op: str) -> str:
@@ -172,15 +177,15 @@ def cmd_build():
     tmp = os.path.join("/tmp", "dsx_valu_mix")
     os.makedirs(tmp, exist_ok=True)
     out = {}
-    for name, (r, ssd, nw, side) in BENCH_KERNELS.items():
+    for name, (r, ssd, nw, side, abs_) in BENCH_KERNELS.items():
         s_path = os.path.join(tmp, f"r{r}.s")
         if not os.path.exists(s_path) or os.path.getmtime(s_path) < os.path.getmtime(src):
             subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", f"-DDSX_RADIUS={r}",
                             "--cuda-device-only", "-S", "-o", s_path, src], check=True)
-        sym = symbol(r, ssd, nw, side)
+        sym = symbol(r, ssd, nw, side, abs_)
         mix, loops = loop_mix(s_path, sym)
         c, unpriced = weigh(mix, costs, fam)
-        out[name] = {"kernel": f"bm2<R={r},{'SSD' if ssd else 'SAD'},NW={nw},SIDE={side}>", "symbol": sym,
+        out[name] = {"kernel": kernel_label(r, ssd, nw, side, abs_), "symbol": sym,
                      "mean_issue_cycles": round(c, 4), "loop_valu_ops": sum(mix.values()),
                      "loops": [list(x) for x in loops],
                      "unpriced_ops": dict(unpriced),
