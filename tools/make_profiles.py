@@ -13,20 +13,22 @@ import csv
 import glob
 import json
 import os
+import re
 import shutil
 import sys
 from collections import defaultdict
 
-# kernel-name patterns, most specific first (vol_wta's template list also ends in ", 3>")
-NAMES = {"vol_wta": "volume_wta", "lr_fixup": "lr_fixup", ", 0>": "bm_pass_left", ", 3>": "bm_pass_left",
-         ", 1>": "bm_pass_right", ", 2>": "cost_volume"}
+# kernel names: vol_wta / lr_fixup by name, bm2<R, SSD, NW, SIDE[, ABS]> by its SIDE argument
+SIDES = {"0": "bm_pass_left", "3": "bm_pass_left", "1": "bm_pass_right", "2": "cost_volume"}
 
 
 def short(k):
-    for pat, n in NAMES.items():
-        if pat in k:
-            return n
-    return k
+    if "vol_wta" in k:
+        return "volume_wta"
+    if "lr_fixup" in k:
+        return "lr_fixup"
+    m = re.search(r"bm2<\s*\d+,\s*\w+,\s*\d+,\s*(\d)", k)
+    return SIDES[m.group(1)] if m else k
 
 
 def main(src, tag, config, path):
