@@ -201,15 +201,66 @@ def selftest_launch(args):
         dist.destroy_process_group()
 
 
+class Ranks:
+    """The job's ranks: one process per GPU over RCCL (backend "nccl", the driver's mode), or the
+    labelled oversubscribed rehearsal (backend "gloo": ranks share the visible GPUs, rank r on
+    device local_rank % device_count, collectives on host tensors) that runs the whole N-rank body
+    on a box with fewer GPUs (tests/test_bench_multirank.py)."""
+
+    def __init__(self, backend: str):
+        import torch
+        import torch.distributed as dist
+        from depthestimation_amd import sharding
+        self.torch, self.dist = torch, dist
+        self.backend = backend
+        env = sharding.init_distributed(backend)
+        self.ws, self.rank, self.local = env.world_size, env.rank, env.local_rank
+        self.ndev = torch.cuda.device_count()
+        if backend == "nccl" and self.ws > self.ndev:
+            raise SystemExit(f"bench.py: {self.ws} ranks but {self.ndev} visible GPUs (use --dist-backend gloo "
+                             "for the oversubscribed rehearsal)")
+        self.dev_index = self.local % self.ndev
+        torch.cuda.set_device(self.dev_index)
+        self.dev = torch.device("cuda", self.dev_index)
+        self.coll_dev = self.dev if backend == "nccl" else torch.device("cpu")
+
+    def barrier(self):
+        if self.ws > 1:
+            self.dist.barrier()
+
+    def allreduce(self, x, op="max"):
+        """max / sum of a scalar over ranks (float64 for times, int64 for counts)."""
+        if self.ws == 1:
+            return x
+        torch, dist = self.torch, self.dist
+        t = torch.tensor([x], dtype=torch.int64 if isinstance(x, int) else torch.float64, device=self.coll_dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX if op == "max" else dist.ReduceOp.SUM)
+        return type(x)(t.item())
+
+    def gather(self, obj):
+        if self.ws == 1:
+            return [obj]
+        out = [None] * self.ws
+        self.dist.all_gather_object(out, obj)
+        return out
+
+    def close(self):
+        if self.ws > 1:
+            self.dist.barrier()
+            self.dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=1000)
-    ap.add_argument("--warmup", type=int, default=500,
-                    help="untimed steps; the GPU needs ~20 ms of load to reach full clocks after host-side setup")
+    ap.add_argument("--warmup", type=int, default=500, help="untimed steps right before the timed region")
     ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
     ap.add_argument("--path", default="fused", choices=["fused", "volume"])
     ap.add_argument("--frames", type=int, default=4, help="distinct resident frame pairs per GPU")
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                    help="nccl: one rank per GPU over RCCL (the measured mode); gloo: oversubscribed rehearsal, "
+                         "ranks share the visible GPUs (labelled in the JSON line, not a scaling figure)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-volume-roofline", action="store_true")
     ap.add_argument("--no-parity", action="store_true", help="skip the oracle check of frame 0 (tuning runs)")
@@ -234,35 +285,47 @@ def main():
         return
 
     import torch
-    import torch.distributed as dist
     from depthestimation_amd import sharding
     from depthestimation_amd.matcher import HipBlockMatcher
     from depthestimation_amd.synthetic import stereo_pair
 
     if not torch.cuda.is_available():
         raise RuntimeError("bench.py needs a HIP device")
-    env = sharding.init_distributed("nccl")
-    ws, rank, local = env.world_size, env.rank, env.local_rank
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+    rk = Ranks(args.dist_backend)
+    ws, rank, local, dev = rk.ws, rk.rank, rk.dev_index, rk.dev
 
     cfg = CONFIGS[args.config]
     H, W = cfg["H"], cfg["W"]
 
-    # one-time RCCL broadcast of the calibration block from rank 0 (no per-frame collectives)
-    calib = sharding.broadcast_calibration(calibration_params() if rank == 0 else None, device=dev)
-    assert calib["image_width"] == 2964, "calibration broadcast failed"
+    # one-time broadcast of the calibration block from rank 0 (RCCL; no per-frame collectives); every
+    # rank checks what it received against the calibration it would have built itself
+    calib = sharding.broadcast_calibration(calibration_params() if rank == 0 else None,
+                                           device=dev if args.dist_backend == "nccl" else None)
+    want_calib = sharding.unpack_calibration(sharding.pack_calibration(calibration_params()))
+    calib_bad = sum(int(not np.array_equal(np.asarray(calib[k], np.float64), np.asarray(want_calib[k], np.float64)))
+                    for k in want_calib)
+    calib_bad = rk.allreduce(calib_bad, "sum")
+    if calib_bad:
+        raise RuntimeError(f"calibration broadcast: {calib_bad} fields differ on some rank")
 
     # frame-sharded synthetic stream: global frame g = rank + ws * i, generated by its own rank
     # only; a step is one launch over `batch` resident frame pairs (batch 1: one compute_device call)
     B = max(1, args.batch)
     nres = max(args.frames, B)
+    gframes = [rank + ws * i for i in range(nres)]
     hostL, hostR = [], []
-    for i in range(nres):
-        g = rank + ws * i
+    for g in gframes:
         L, R, _ = stereo_pair(H, W, 0, cfg["num_disp"], seed=1234 + g)
         hostL.append(L)
         hostR.append(R)
+    owned = rk.gather(gframes)
+    flat = sorted(g for o in owned for g in o)
+    sharding_info = {"frames_per_rank": nres, "global_frames": len(flat),
+                     "disjoint_and_complete": flat == list(range(ws * nres)),
+                     "assignment": "global frame g on rank g mod N", "calibration_broadcast": "verified on every rank",
+                     "backend": "RCCL (torch.distributed nccl)" if args.dist_backend == "nccl" else "gloo"}
+    if not sharding_info["disjoint_and_complete"]:
+        raise RuntimeError("frame sharding is not a partition of the global frame set")
     allL = torch.from_numpy(np.stack(hostL)).to(dev)
     allR = torch.from_numpy(np.stack(hostR)).to(dev)
     groups = [(allL[i:i + B], allR[i:i + B]) for i in range(0, nres - B + 1, B)]
@@ -293,11 +356,34 @@ def main():
             gl, gr = groups[i % len(groups)]
             m.compute_batch_device(gl, gr, out_fixed=out_fixed, out_float=out_float, stream=stream)
 
+    # parity of the timed matcher: every rank's frame 0 against the C restatement of the contract
+    # (oracle/bm_ref.c, the checker; never on the measured path), before the timed region; after it
+    # the same handle's frame-0 map is compared with this one again on the device
+    parity, ref0 = None, None
+    if not args.no_parity and not args.sgm:
+        from oracle.cref import CRef
+        step(0)
+        torch.cuda.synchronize(dev)
+        got = out_fixed[0].cpu().numpy()
+        th = max(1, min(16, cpu_threads_available() // ws))  # the ranks share this host's CPUs
+        want = CRef()(hostL[0], hostR[0], nthreads=th, **kw)["fixed"]
+        mism = rk.allreduce(int(np.count_nonzero(got != want)), "sum")
+        ref0 = torch.from_numpy(want).to(dev)
+        parity = {"mismatches": mism, "frames_checked": ws, "pixels_checked": ws * H * W,
+                  "compared": "int16 x16 map of each rank's frame 0 from the timed matcher, bit for bit, before the "
+                              "timed region and again (on the device) after it",
+                  "oracle": "oracle/bm_ref.c (C restatement of the A5' contract; tests/test_oracle.py pins it)"}
+
+    # secondary measurements (never `value`) run BEFORE the headline's warmup, so the timed region
+    # starts on a GPU that has been busy for seconds (clocks settled) and the long CPU baseline
+    # runs after it
+    sec = secondaries(args, cfg, rk, matcher, frames, hostL, hostR, allL, allR, out_fixed, out_float, stream, nres, B,
+                      kw)
+
     for i in range(args.warmup):
         step(i)
     torch.cuda.synchronize(dev)
-    if ws > 1:
-        dist.barrier()
+    rk.barrier()
     torch.cuda.synchronize(dev)
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
@@ -306,14 +392,18 @@ def main():
         step(i)
     ev1.record(stream)
     torch.cuda.synchronize(dev)
-    if ws > 1:
-        dist.barrier()
+    rk.barrier()
     elapsed = time.perf_counter() - t0
     region_ms = ev0.elapsed_time(ev1) / args.steps  # GPU time per step over the timed region
-    if ws > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    elapsed = rk.allreduce(float(elapsed), "max")
+
+    if ref0 is not None:
+        step(0)
+        torch.cuda.synchronize(dev)
+        after = rk.allreduce(int(torch.count_nonzero(out_fixed[0] != ref0).item()), "sum")
+        parity["mismatches_after_timed_region"] = after
+        parity["mismatches"] += after
+
     # breakdown pass: per-kernel HIP events on the same stream (outside the timed region), only for
     # paths with several kernels per step; the fused pass without the LR check is one kernel, whose
     # launch duration is the timed region's per-step GPU time
@@ -330,143 +420,6 @@ def main():
         torch.cuda.synchronize(dev)
         ktimes = tmatcher.kernel_times()
 
-    # parity of the timed matcher (after the timed region): every rank's frame 0 against the C
-    # restatement of the contract (oracle/bm_ref.c, the checker; never on the measured path)
-    parity = None
-    if not args.no_parity and not args.sgm:
-        from oracle.cref import CRef
-        step(0)
-        torch.cuda.synchronize(dev)
-        got = out_fixed[0].cpu().numpy()
-        th = max(1, min(16, cpu_threads_available() // ws))
-        want = CRef()(hostL[0], hostR[0], nthreads=th, **kw)["fixed"]
-        mism = torch.tensor([int(np.count_nonzero(got != want))], dtype=torch.int64, device=dev)
-        if ws > 1:
-            dist.all_reduce(mism)
-        parity = {"mismatches": int(mism.item()), "frames_checked": ws, "pixels_checked": ws * H * W,
-                  "compared": "int16 x16 map of each rank's frame 0 from the timed matcher, bit for bit",
-                  "oracle": "oracle/bm_ref.c (C restatement of the A5' contract; tests/test_oracle.py pins it)"}
-
-    # secondary, never `value`: host frames -> H2D -> matcher -> D2H of the int16 map on every rank's
-    # GPU (multigpu.HostPipeline: 3 frames in flight over 2 streams, no per-frame host sync), whole-job
-    # rate over the slowest rank (SURVEY 8e / BASELINE.md: end-to-end next to the device-resident
-    # `value`).  Two sources: pinned frame buffers (a decoder writing into a pinned ring) and
-    # pageable numpy arrays (one host copy into the pinned slot per frame).
-    e2e = None
-    if not args.no_e2e and args.path == "fused" and not args.sgm:
-        from depthestimation_amd.multigpu import HostPipeline
-        pipe = HostPipeline(local, depth=3, streams=2, copy=False, **kw)
-        pinned = []
-        for i in range(nres):
-            t = torch.empty((2, H, W), dtype=torch.uint8, pin_memory=True)
-            t[0].numpy()[...] = hostL[i]
-            t[1].numpy()[...] = hostR[i]
-            pinned.append(t)
-        ne = 256
-        rates = {}
-        for name, src in (("pinned", [pinned[i % nres] for i in range(ne)]),
-                          ("pageable", [(hostL[i % nres], hostR[i % nres]) for i in range(ne)])):
-            for _ in pipe.run(iter(src[:16])):
-                pass
-            if ws > 1:
-                dist.barrier()
-            t1 = time.perf_counter()
-            n_done = sum(1 for _ in pipe.run(iter(src)))
-            et = time.perf_counter() - t1
-            if ws > 1:
-                t = torch.tensor([et], dtype=torch.float64, device=dev)
-                dist.all_reduce(t, op=dist.ReduceOp.MAX)
-                et = float(t.item())
-            rates[name] = (round(H * W * n_done * ws / et / 1e6, 1), round(et / n_done * 1e3, 4))
-        pipe.close()
-        # 2 B/px up (L + R) and 2 B/px down (int16) at ~50 GB/s per direction (PCIe 5 x16), the two
-        # directions overlapping: the floor is the larger of the two transfers
-        pcie_floor_ms = H * W * 2 / 50e9 * 1e3
-        e2e = {"value": rates["pinned"][0], "unit": "Mpix/s", "frames_per_gpu": ne,
-               "ms_per_frame_per_gpu": rates["pinned"][1], "pcie_floor_ms_per_frame": round(pcie_floor_ms, 4),
-               "pcie_floor_serial_ms_per_frame": round(2 * pcie_floor_ms, 4),
-               "pageable_source": {"value": rates["pageable"][0], "ms_per_frame_per_gpu": rates["pageable"][1]},
-               "note": "secondary, PCIe-inclusive: host uint8 pairs in (pinned frame ring; pageable_source: numpy "
-                       "arrays copied into the pinned slot), int16 x16 out in pinned memory, 3 frames in flight over "
-                       "2 streams (multigpu.HostPipeline), all ranks, max time over ranks"}
-
-    # secondary: the C2 shape with the reference's own uniqueness 10 / disp12MaxDiff 1 defaults
-    # (stereo_core.py:20,22), which add the LR pass (side 3 + lr_fixup)
-    refdef = None
-    if args.config == "c2" and args.path == "fused" and B == 1 and not args.sgm and not args.no_ref_defaults:
-        kwr = matcher_kwargs(CONFIGS["c2r"])
-        mr = HipBlockMatcher(device=local, path="fused", **kwr)
-        mrt = HipBlockMatcher(device=local, path="fused", timing=True, **kwr)
-        for i in range(100):
-            fl, fr = frames[i % len(frames)]
-            mr.compute_device(fl, fr, out_fixed=out_fixed[0], out_float=out_float[0], stream=stream)
-        torch.cuda.synchronize(dev)
-        nr = 300
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        t1 = time.perf_counter()
-        e0.record(stream)
-        for i in range(nr):
-            fl, fr = frames[i % len(frames)]
-            mr.compute_device(fl, fr, out_fixed=out_fixed[0], out_float=out_float[0], stream=stream)
-        e1.record(stream)
-        torch.cuda.synchronize(dev)
-        rt = time.perf_counter() - t1
-        for i in range(30):
-            fl, fr = frames[i % len(frames)]
-            mrt.compute_device(fl, fr, out_fixed=out_fixed[0], out_float=out_float[0], stream=stream)
-        torch.cuda.synchronize(dev)
-        kr = mrt.kernel_times()
-        refdef = {"value": round(H * W * nr / rt / 1e6, 1), "unit": "Mpix/s", "ms_per_step": round(rt / nr * 1e3, 5),
-                  "gpu_ms_per_step": round(e0.elapsed_time(e1) / nr, 5),
-                  "kernels_ms": {k: round(v[0], 5) for k, v in kr.items()},
-                  "config": dict(uniqueness_ratio=10, disp12_max_diff=1),
-                  "note": "secondary: C2 with the reference's default uniqueness_ratio=10, disp12_max_diff=1 "
-                          "(left pass with right-view winners + lr_fixup)"}
-        if "bm_pass_left" in kr:
-            vr = valu_roofline("c2r", "c2r:fused:bm_pass_left", kr["bm_pass_left"][0])
-            if vr:
-                refdef["roofline"] = vr
-        mr.close()
-        mrt.close()
-
-    # secondary: the reference's per-frame steps after the matcher on the device (SURVEY 8f F1/F2 and
-    # hole filling, stereo_core.py:168-196 / postprocess.py), on this rank's matcher output for frame 0:
-    # median of 30 stream-event timings each
-    post = None
-    if args.config in ("c2", "c4") and args.path == "fused" and not args.sgm and not args.no_post and B == 1:
-        from depthestimation_amd.matcher import fill_holes_device, postprocess_fast_device, postprocess_full_device
-        dsp = torch.empty((H, W), dtype=torch.float32, device=dev)
-        matcher.compute_device(frames[0][0], frames[0][1], out_float=dsp, stream=stream)
-        D = cfg["num_disp"]
-
-        def tmed(fn, n=30):
-            ts = []
-            for i in range(n + 3):
-                a_, b_ = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                a_.record(stream)
-                fn()
-                b_.record(stream)
-                b_.synchronize()
-                if i >= 3:
-                    ts.append(a_.elapsed_time(b_))
-            return round(float(np.median(ts)), 4)
-
-        with torch.cuda.stream(stream):
-            clean, _ = postprocess_full_device(dsp, D, max_speckle_size=100, max_diff=1.0, outlier_threshold=2.5,
-                                               stream=stream)
-            post = {"matcher_ms": tmed(lambda: matcher.compute_device(frames[0][0], frames[0][1], out_float=dsp,
-                                                                      stream=stream)),
-                    "fast_mode_ms": tmed(lambda: postprocess_fast_device(dsp, D, 700.0, 0.1, stream=stream)),
-                    "default_mode_ms": tmed(lambda: postprocess_full_device(
-                        dsp, D, max_speckle_size=100, max_diff=1.0, outlier_threshold=2.5, focal_length=700.0,
-                        baseline=0.1, stream=stream)),
-                    "hole_filling_ms": tmed(lambda: fill_holes_device(clean, radius=3, stream=stream), 10),
-                    "hole_pixels": int((clean <= 0).sum().item()),
-                    "note": "secondary: device post-processing of this frame's map (fast mode: crop + median + depth; "
-                            "default mode: speckles + outliers + median + depth; hole filling: Telea radius 3 on the "
-                            "default-mode map's holes), stream events, median of 30 (10)"}
-
-    result = None
     if rank == 0:
         px_total = H * W * B * args.steps * ws
         value = px_total / elapsed / 1e6
@@ -510,6 +463,10 @@ def main():
         else:
             roofline["algorithmic_bytes_per_launch"] = per_launch_bytes
             roofline["basis"] = "SURVEY 8(d) D3 per-frame bytes over the dominant kernel"
+        par = f"frame-sharded x{ws} (RCCL calibration broadcast, no per-frame collectives)"
+        if args.dist_backend == "gloo":
+            par = (f"frame-sharded x{ws} OVERSUBSCRIBED on {min(ws, rk.ndev)} GPU(s) (gloo rehearsal of the N-rank "
+                   "body; not a scaling figure)")
         result = {
             "metric": METRIC, "value": round(value, 1), "unit": "Mpix/s", "n_gpus": ws,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 5),
@@ -518,78 +475,205 @@ def main():
             "config": {"workload": cfg["desc"], "H": H, "W": W, "num_disp": cfg["num_disp"],
                        "block_size": cfg["block_size"], "cost": cfg["cost"],
                        "uniqueness_ratio": cfg["uniqueness_ratio"], "disp12_max_diff": cfg["disp12_max_diff"],
-                       "subpixel": True, "path": args.path, "aggregation": args.sgm or "none", "frames_per_step_per_gpu": B,
-                       "parallelism": f"frame-sharded x{ws} (RCCL calibration broadcast, no per-frame collectives)"},
+                       "subpixel": True, "path": args.path, "aggregation": args.sgm or "none",
+                       "frames_per_step_per_gpu": B, "parallelism": par},
             "roofline": roofline,
             "parity": parity,
+            "sharding": sharding_info,
+            "order": "parity check -> secondary measurements -> warmup -> timed region -> breakdown pass -> "
+                     "CPU baseline",
         }
-
-        if B == 1 and args.path == "fused" and not args.no_batched:
-            # secondary figure: the same workload with 4 frame pairs per launch (video streams)
-            Bb = 4
-            gL = allL[:Bb] if allL.shape[0] >= Bb else allL.repeat(Bb, 1, 1)[:Bb]
-            gR = allR[:Bb] if allR.shape[0] >= Bb else allR.repeat(Bb, 1, 1)[:Bb]
-            bf = torch.empty((Bb, H, W), dtype=torch.int16, device=dev)
-            bfl = torch.empty((Bb, H, W), dtype=torch.float32, device=dev)
-            for _ in range(3):
-                matcher.compute_batch_device(gL, gR, out_fixed=bf, out_float=bfl, stream=stream)
-            torch.cuda.synchronize(dev)
-            nb = 20
-            t1 = time.perf_counter()
-            for _ in range(nb):
-                matcher.compute_batch_device(gL, gR, out_fixed=bf, out_float=bfl, stream=stream)
-            torch.cuda.synchronize(dev)
-            bt = time.perf_counter() - t1
-            result["batched"] = {"frames_per_launch": Bb, "value": round(H * W * Bb * nb / bt / 1e6, 1),
-                                 "unit": "Mpix/s", "ms_per_frame": round(bt / (nb * Bb) * 1e3, 5),
-                                 "note": "secondary: dsx_compute_batch_device over 4 resident pairs per launch"}
-
-        if not args.no_volume_roofline and args.path == "fused":
-            vm = HipBlockMatcher(device=local, path="volume", timing=True, **kw)
-            for i in range(5):
-                fl, fr = frames[i % len(frames)]
-                vm.compute_device(fl, fr, out_fixed=out_fixed[0], out_float=out_float[0], stream=stream)
-            torch.cuda.synchronize(dev)
-            vm.reset_times()
-            t1 = time.perf_counter()
-            nv = 20
-            for i in range(nv):
-                fl, fr = frames[i % len(frames)]
-                vm.compute_device(fl, fr, out_fixed=out_fixed[0], out_float=out_float[0], stream=stream)
-            torch.cuda.synchronize(dev)
-            vt = time.perf_counter() - t1
-            kt = vm.kernel_times()
-            rv = {"value_mpix_s": round(H * W * nv / vt / 1e6, 1),
-                  "note": "the north-star two-kernel path (K1 writes the cost volume, K2 reduces it): HBM-bound, "
-                          "the HBM roofline evidence"}
-            for name, key in (("cost_volume", "k1"), ("volume_wta", "k2")):
-                if name in kt:
-                    ms = kt[name][0]
-                    a = ab[key] / (ms * 1e-3) / 1e9
-                    rv[name] = {"bound": "hbm", "kernel_ms": round(ms, 5), "algorithmic_bytes": ab[key],
-                                "achieved": round(a, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                                "frac": round(a / HBM_PEAK_GBS, 4),
-                                "traffic": (traffic.get(f"{args.config}:volume:{name}") or {}).get(
-                                    "hbm_bytes_per_launch")}
-            result["roofline_volume"] = rv
-            vm.close()
-
-        if e2e is not None:
-            result["e2e_host"] = e2e
-        if refdef is not None:
-            result["c2_reference_defaults"] = refdef
-        if post is not None:
-            result["post_processing"] = post
-
+        if args.dist_backend == "gloo":
+            result["oversubscribed"] = {"ranks": ws, "visible_gpus": rk.ndev,
+                                        "note": "ranks share GPUs: value is a rehearsal of the N-rank body, not "
+                                                "N-GPU throughput"}
+        result.update(sec)
         if not args.no_cpu_baseline and ws == 1:
             result["cpu_baseline"] = cpu_baseline(args, cfg, hostL[0], hostR[0])
         print(json.dumps(result), flush=True)
 
     matcher.close()
     tmatcher.close()
-    if ws > 1:
-        dist.barrier()
-        dist.destroy_process_group()
+    rk.close()
+
+
+def secondaries(args, cfg, rk, matcher, frames, hostL, hostR, allL, allR, out_fixed, out_float, stream, nres, B,
+                kw) -> dict:
+    """The secondary figures of the JSON line (never `value`): PCIe-inclusive host frames, the C2
+    shape with the reference's default checks, device post-processing, 4 frames per launch and the
+    two-kernel volume path's HBM roofline."""
+    import torch
+    from depthestimation_amd.matcher import HipBlockMatcher
+    ws, dev = rk.ws, rk.dev
+    H, W = cfg["H"], cfg["W"]
+    out = {}
+
+    # host frames -> H2D -> matcher -> D2H of the int16 map on every rank's GPU (multigpu.HostPipeline:
+    # 3 frames in flight over 2 streams, no per-frame host sync), whole-job rate over the slowest rank
+    # (SURVEY 8e / BASELINE.md: end-to-end next to the device-resident `value`).  Two sources: pinned
+    # frame buffers (a decoder writing into a pinned ring) and pageable numpy arrays (one host copy
+    # into the pinned slot per frame).
+    if not args.no_e2e and args.path == "fused" and not args.sgm:
+        from depthestimation_amd.multigpu import HostPipeline
+        pipe = HostPipeline(rk.dev_index, depth=3, streams=2, copy=False, **kw)
+        pinned = []
+        for i in range(nres):
+            t = torch.empty((2, H, W), dtype=torch.uint8, pin_memory=True)
+            t[0].numpy()[...] = hostL[i]
+            t[1].numpy()[...] = hostR[i]
+            pinned.append(t)
+        ne = 256
+        rates = {}
+        for name, src in (("pinned", [pinned[i % nres] for i in range(ne)]),
+                          ("pageable", [(hostL[i % nres], hostR[i % nres]) for i in range(ne)])):
+            for _ in pipe.run(iter(src[:16])):
+                pass
+            rk.barrier()
+            t1 = time.perf_counter()
+            n_done = sum(1 for _ in pipe.run(iter(src)))
+            et = rk.allreduce(float(time.perf_counter() - t1), "max")
+            rates[name] = (round(H * W * n_done * ws / et / 1e6, 1), round(et / n_done * 1e3, 4))
+        pipe.close()
+        # 2 B/px up (L + R) and 2 B/px down (int16) at ~50 GB/s per direction (PCIe 5 x16), the two
+        # directions overlapping: the floor is the larger of the two transfers
+        pcie_floor_ms = H * W * 2 / 50e9 * 1e3
+        out["e2e_host"] = {
+            "value": rates["pinned"][0], "unit": "Mpix/s", "frames_per_gpu": ne,
+            "ms_per_frame_per_gpu": rates["pinned"][1], "pcie_floor_ms_per_frame": round(pcie_floor_ms, 4),
+            "pcie_floor_serial_ms_per_frame": round(2 * pcie_floor_ms, 4),
+            "pageable_source": {"value": rates["pageable"][0], "ms_per_frame_per_gpu": rates["pageable"][1]},
+            "note": "secondary, PCIe-inclusive: host uint8 pairs in (pinned frame ring; pageable_source: numpy "
+                    "arrays copied into the pinned slot), int16 x16 out in pinned memory, 3 frames in flight over "
+                    "2 streams (multigpu.HostPipeline), all ranks, max time over ranks"}
+
+    # the C2 shape with the reference's own uniqueness 10 / disp12MaxDiff 1 defaults
+    # (stereo_core.py:20,22), which add the LR pass (side 3 + lr_fixup)
+    if args.config == "c2" and args.path == "fused" and B == 1 and not args.sgm and not args.no_ref_defaults:
+        kwr = matcher_kwargs(CONFIGS["c2r"])
+        mr = HipBlockMatcher(device=rk.dev_index, path="fused", **kwr)
+        mrt = HipBlockMatcher(device=rk.dev_index, path="fused", timing=True, **kwr)
+        for i in range(100):
+            fl, fr = frames[i % len(frames)]
+            mr.compute_device(fl, fr, out_fixed=out_fixed[0], out_float=out_float[0], stream=stream)
+        torch.cuda.synchronize(dev)
+        nr = 300
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        t1 = time.perf_counter()
+        e0.record(stream)
+        for i in range(nr):
+            fl, fr = frames[i % len(frames)]
+            mr.compute_device(fl, fr, out_fixed=out_fixed[0], out_float=out_float[0], stream=stream)
+        e1.record(stream)
+        torch.cuda.synchronize(dev)
+        rt = time.perf_counter() - t1
+        for i in range(30):
+            fl, fr = frames[i % len(frames)]
+            mrt.compute_device(fl, fr, out_fixed=out_fixed[0], out_float=out_float[0], stream=stream)
+        torch.cuda.synchronize(dev)
+        kr = mrt.kernel_times()
+        refdef = {"value": round(H * W * nr / rt / 1e6, 1), "unit": "Mpix/s", "ms_per_step": round(rt / nr * 1e3, 5),
+                  "gpu_ms_per_step": round(e0.elapsed_time(e1) / nr, 5),
+                  "kernels_ms": {k: round(v[0], 5) for k, v in kr.items()},
+                  "config": dict(uniqueness_ratio=10, disp12_max_diff=1),
+                  "note": "secondary: C2 with the reference's default uniqueness_ratio=10, disp12_max_diff=1 "
+                          "(left pass with right-view winners + lr_fixup)"}
+        if "bm_pass_left" in kr:
+            vr = valu_roofline("c2r", "c2r:fused:bm_pass_left", kr["bm_pass_left"][0])
+            if vr:
+                refdef["roofline"] = vr
+        mr.close()
+        mrt.close()
+        out["c2_reference_defaults"] = refdef
+
+    # the reference's per-frame steps after the matcher on the device (SURVEY 8f F1/F2 and hole
+    # filling, stereo_core.py:168-196 / postprocess.py), on this rank's matcher output for frame 0:
+    # median of 30 stream-event timings each
+    if args.config in ("c2", "c4") and args.path == "fused" and not args.sgm and not args.no_post and B == 1:
+        from depthestimation_amd.matcher import fill_holes_device, postprocess_fast_device, postprocess_full_device
+        dsp = torch.empty((H, W), dtype=torch.float32, device=dev)
+        matcher.compute_device(frames[0][0], frames[0][1], out_float=dsp, stream=stream)
+        D = cfg["num_disp"]
+
+        def tmed(fn, n=30):
+            ts = []
+            for i in range(n + 3):
+                a_, b_ = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                a_.record(stream)
+                fn()
+                b_.record(stream)
+                b_.synchronize()
+                if i >= 3:
+                    ts.append(a_.elapsed_time(b_))
+            return round(float(np.median(ts)), 4)
+
+        with torch.cuda.stream(stream):
+            clean, _ = postprocess_full_device(dsp, D, max_speckle_size=100, max_diff=1.0, outlier_threshold=2.5,
+                                               stream=stream)
+            out["post_processing"] = {
+                "matcher_ms": tmed(lambda: matcher.compute_device(frames[0][0], frames[0][1], out_float=dsp,
+                                                                  stream=stream)),
+                "fast_mode_ms": tmed(lambda: postprocess_fast_device(dsp, D, 700.0, 0.1, stream=stream)),
+                "default_mode_ms": tmed(lambda: postprocess_full_device(
+                    dsp, D, max_speckle_size=100, max_diff=1.0, outlier_threshold=2.5, focal_length=700.0,
+                    baseline=0.1, stream=stream)),
+                "hole_filling_ms": tmed(lambda: fill_holes_device(clean, radius=3, stream=stream), 10),
+                "hole_pixels": int((clean <= 0).sum().item()),
+                "note": "secondary: device post-processing of this frame's map (fast mode: crop + median + depth; "
+                        "default mode: speckles + outliers + median + depth; hole filling: Telea radius 3 on the "
+                        "default-mode map's holes), stream events, median of 30 (10)"}
+
+    if B == 1 and args.path == "fused" and not args.no_batched and rk.rank == 0:
+        # the same workload with 4 frame pairs per launch (video streams)
+        Bb = 4
+        gL = allL[:Bb] if allL.shape[0] >= Bb else allL.repeat(Bb, 1, 1)[:Bb]
+        gR = allR[:Bb] if allR.shape[0] >= Bb else allR.repeat(Bb, 1, 1)[:Bb]
+        bf = torch.empty((Bb, H, W), dtype=torch.int16, device=dev)
+        bfl = torch.empty((Bb, H, W), dtype=torch.float32, device=dev)
+        for _ in range(3):
+            matcher.compute_batch_device(gL, gR, out_fixed=bf, out_float=bfl, stream=stream)
+        torch.cuda.synchronize(dev)
+        nb = 20
+        t1 = time.perf_counter()
+        for _ in range(nb):
+            matcher.compute_batch_device(gL, gR, out_fixed=bf, out_float=bfl, stream=stream)
+        torch.cuda.synchronize(dev)
+        bt = time.perf_counter() - t1
+        out["batched"] = {"frames_per_launch": Bb, "value": round(H * W * Bb * nb / bt / 1e6, 1),
+                          "unit": "Mpix/s", "ms_per_frame": round(bt / (nb * Bb) * 1e3, 5),
+                          "note": "secondary: dsx_compute_batch_device over 4 resident pairs per launch"}
+
+    if not args.no_volume_roofline and args.path == "fused" and rk.rank == 0:
+        ab = algorithmic_bytes(cfg)
+        traffic = load_traffic()
+        vm = HipBlockMatcher(device=rk.dev_index, path="volume", timing=True, **kw)
+        for i in range(5):
+            fl, fr = frames[i % len(frames)]
+            vm.compute_device(fl, fr, out_fixed=out_fixed[0], out_float=out_float[0], stream=stream)
+        torch.cuda.synchronize(dev)
+        vm.reset_times()
+        t1 = time.perf_counter()
+        nv = 20
+        for i in range(nv):
+            fl, fr = frames[i % len(frames)]
+            vm.compute_device(fl, fr, out_fixed=out_fixed[0], out_float=out_float[0], stream=stream)
+        torch.cuda.synchronize(dev)
+        vt = time.perf_counter() - t1
+        kt = vm.kernel_times()
+        rv = {"value_mpix_s": round(H * W * nv / vt / 1e6, 1),
+              "note": "the north-star two-kernel path (K1 writes the cost volume, K2 reduces it): HBM-bound, "
+                      "the HBM roofline evidence"}
+        for name, key in (("cost_volume", "k1"), ("volume_wta", "k2")):
+            if name in kt:
+                ms = kt[name][0]
+                a = ab[key] / (ms * 1e-3) / 1e9
+                rv[name] = {"bound": "hbm", "kernel_ms": round(ms, 5), "algorithmic_bytes": ab[key],
+                            "achieved": round(a, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                            "frac": round(a / HBM_PEAK_GBS, 4),
+                            "traffic": (traffic.get(f"{args.config}:volume:{name}") or {}).get(
+                                "hbm_bytes_per_launch")}
+        out["roofline_volume"] = rv
+        vm.close()
+    return out
 
 
 def cpu_baseline(args, cfg, L, R) -> dict:
@@ -602,13 +686,10 @@ def cpu_baseline(args, cfg, L, R) -> dict:
     ref = CRef(so)
     allc = cpu_threads_available()
     legs = {"all_cores": allc, "single_core": 1}
-    secs = {"all_cores": 2.0, "single_core": 1.5, "cpu_count_threads": 1.5}
-    if allc != 16:
-        legs["threads_16"] = min(16, os.cpu_count() or 16)
+    secs = {"all_cores": 2.0, "single_core": 1.5}
+    if allc != 16 and (os.cpu_count() or 1) >= 16:
+        legs["threads_16"] = 16
         secs["threads_16"] = 1.0
-    if (os.cpu_count() or 1) != allc:
-        # os.cpu_count() OpenMP threads on the same CPU share (oversubscribed when a quota caps it)
-        legs["cpu_count_threads"] = os.cpu_count()
     table = {}
     for name in ("c1", "c2", "c5"):
         c = CONFIGS[name]
@@ -632,8 +713,8 @@ def cpu_baseline(args, cfg, L, R) -> dict:
                   f"oracle/bm_ref.c -O3 -march=native (C restatement of the same contract; OpenCV absent)",
         "host_cpus": os.cpu_count(), "usable_cpus": allc,
         "configs": table,
-        "note": "per-config legs are short samples (whole frames, >= 1 frame each); cores = OpenMP threads used; "
-                "cpu_count_threads runs os.cpu_count() threads on the usable CPUs (oversubscribed under a quota)",
+        "note": "per-config legs are short samples (whole frames, >= 1 frame each); cores = OpenMP threads used "
+                "(all_cores: every CPU this process may use; single_core: 1)",
     }
 
 

@@ -139,11 +139,13 @@ struct dsx_handle {
     int lrFrames = 0;  // frames the LR buffers hold
     int lrParity = 0;  // which half of lrKeys the next frame's left pass fills
     int lrDirty[2] = {0, 0};  // frames of each half holding keys that were not reset yet
-    // LR buffers are reused across calls: a call on another stream than the previous LR call
-    // waits for that call's lr_fixup (event) before its left pass writes the keys again
-    hipEvent_t lrDone = nullptr;
-    hipStream_t lrStream = nullptr;
-    bool lrPending = false;
+    // Handle-owned scratch (LR keys / left winners, cost volume, BT records, SGM sums, the
+    // sgbm_post input and workspace) is reused by every call: a call that touches it on another
+    // stream than the previous such call waits for that call's last kernel (event) first.  Only
+    // the plain fused pass (no LR check, no sgbm_post) owns no scratch and runs unordered.
+    hipEvent_t scratchDone = nullptr;
+    hipStream_t scratchStream = nullptr;
+    bool scratchPending = false;
     uint8_t *dL = nullptr, *dR = nullptr;
     int16_t *dFixed = nullptr;
     float *dFloat = nullptr;
@@ -196,7 +198,7 @@ void free_buffers(dsx_handle *h) {
     h->cH = h->cW = h->cDp = h->cCostBytes = 0;
     h->lrFrames = 0;
     h->lrDirty[0] = h->lrDirty[1] = 0;
-    h->lrPending = false;
+    h->scratchPending = false;
 }
 
 int sgm_p1(const dsx_handle *h) { return h->p.p1 > 0 ? h->p.p1 : 8 * h->p.block_size * h->p.block_size; }
@@ -239,7 +241,6 @@ int ensure_buffers(dsx_handle *h, int H, int W, bool host_staging, int nframes =
         h->lrFrames = nframes;
         h->lrParity = 0;
         h->lrDirty[0] = h->lrDirty[1] = 0;
-        h->lrPending = false;
     }
 
     const bool bt = h->p.cost == DSX_COST_BT;
@@ -394,6 +395,9 @@ int run(dsx_handle *h, const void *dL, const void *dR, int H, int W, int64_t str
     const bool bt = h->p.cost == DSX_COST_BT;  // BT costs exist only as a volume
     // sgbm_post: the matcher writes int16 maps into postIn, the tail then writes the outputs
     void *const finalFixed = outFixed, *const finalFloat = outFloat;
+    const bool scratch = h->p.disp12_max_diff >= 0 || h->p.path != DSX_PATH_FUSED || h->p.aggregation || bt ||
+                         h->p.sgbm_post;
+    if (scratch && h->scratchPending && h->scratchStream != st) DSX_HIP(hipStreamWaitEvent(st, h->scratchDone, 0));
     if (h->p.sgbm_post) {
         outFixed = h->postIn;
         outFloat = nullptr;
@@ -411,7 +415,6 @@ int run(dsx_handle *h, const void *dL, const void *dR, int H, int W, int64_t str
         if (lr) {
             // the left pass also builds the right-view winners (every strip: a right pixel's
             // diagonal starts left of the valid band); lr_fixup applies the check afterwards
-            if (h->lrPending && h->lrStream != st) DSX_HIP(hipStreamWaitEvent(st, h->lrDone, 0));
             a.side = dsx::SIDE_LEFT_LR;
             a.lr_keys = h->lrKeys + (size_t)h->lrParity * H * W * h->lrFrames;
             a.dstar = h->dStar;
@@ -446,10 +449,6 @@ int run(dsx_handle *h, const void *dL, const void *dR, int H, int W, int64_t str
             h->lrDirty[P ^ 1] = 0;
             h->lrDirty[P] = nframes;
             h->lrParity = P ^ 1;
-            if (!h->lrDone) DSX_HIP(hipEventCreateWithFlags(&h->lrDone, hipEventDisableTiming));
-            DSX_HIP(hipEventRecord(h->lrDone, st));
-            h->lrStream = st;
-            h->lrPending = true;
         }
         if (tl) {
             std::vector<uint64_t> host(12 * 65536);
@@ -571,6 +570,12 @@ int run(dsx_handle *h, const void *dL, const void *dR, int H, int W, int64_t str
                                              finalFloat ? static_cast<float *>(finalFloat) + fo : nullptr, h->postWs,
                                              st));
         }
+    }
+    if (scratch) {
+        if (!h->scratchDone) DSX_HIP(hipEventCreateWithFlags(&h->scratchDone, hipEventDisableTiming));
+        DSX_HIP(hipEventRecord(h->scratchDone, st));
+        h->scratchStream = st;
+        h->scratchPending = true;
     }
     return DSX_OK;
 }
@@ -917,7 +922,7 @@ int dsx_destroy(dsx_handle *h) {
         (void)hipEventDestroy(e.second);
     }
     free_buffers(h);
-    if (h->lrDone) (void)hipEventDestroy(h->lrDone);
+    if (h->scratchDone) (void)hipEventDestroy(h->scratchDone);
     (void)hipStreamDestroy(h->stream);
     delete h;
     return DSX_OK;

@@ -163,7 +163,7 @@ typedef const __attribute__((address_space(4))) uint32_t cu32;
 // image (one unaligned dword + one byte load per lane and row); otherwise replicate-clamped
 // byte loads. All per-row state is in plain registers (no structs / arrays with runtime
 // indices, which hipcc would demote to scratch).
-template <int R, bool SSD, int NW, int SIDE, bool FAST, bool ABS>
+template <int R, bool SSD, int NW, int SIDE, bool FAST, bool ABS, bool LRFULL>
 __device__ __forceinline__ void bm2_segment(const Bm2Args &a, uint8_t *smem, int x0, int yb, int ye, long fin, long fout,
                                             bool lr_on, int done0, const int (&pe)[3], int &qcur
 #ifdef DSX_STAMPS
@@ -695,7 +695,10 @@ __device__ __forceinline__ void bm2_segment(const Bm2Args &a, uint8_t *smem, int
                         }
                     }
                 };
-                if (x0 + TX <= W && D == Dp) diag_loop(std::true_type{});
+                // chosen per segment (template): with both forms in one row loop, hipcc hoisted the
+                // 31 per-pixel bounds of the partial form out of the loop as 62 SGPRs, which spilled
+                // through v_writelane / v_readlane in every row step of every strip
+                if constexpr (LRFULL) diag_loop(std::true_type{});
                 else diag_loop(std::false_type{});
                 uint32_t *krow = a.lr_keys + fout + (long)y * W;
                 const int dtop = (wv + 1) * G::LDW - 1;  // disparity of the wave's top slot
@@ -977,18 +980,22 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu((SSD &&
         const int NJ4 = (NJ + 3) / 4;
         const bool fast = (side == 1 ? (PB >= 0 && PB + 4 * NJ4 <= W - 1) : (PB - 4 * NJ4 >= 0 && PB <= W - 1)) &&
                           x0 - R >= 0 && x0 - R + 4 * ((NC + 3) / 4) - 1 <= W - 1;
-        if (fast)
-            bm2_segment<R, SSD, NW, SIDE, true, ABS>(a, smem, x0, yb, ye, fin, fout, lr_on, done0, pe, qcur
 #ifdef DSX_STAMPS
-                                                , ph, t_prev, nsteps
+#define DSX_SEG(FASTV, FULLV) \
+    bm2_segment<R, SSD, NW, SIDE, FASTV, ABS, FULLV>(a, smem, x0, yb, ye, fin, fout, lr_on, done0, pe, qcur, ph, t_prev, nsteps)
+#else
+#define DSX_SEG(FASTV, FULLV) bm2_segment<R, SSD, NW, SIDE, FASTV, ABS, FULLV>(a, smem, x0, yb, ye, fin, fout, lr_on, done0, pe, qcur)
 #endif
-            );
-        else
-            bm2_segment<R, SSD, NW, SIDE, false, ABS>(a, smem, x0, yb, ye, fin, fout, lr_on, done0, pe, qcur
-#ifdef DSX_STAMPS
-                                                 , ph, t_prev, nsteps
-#endif
-            );
+        // LR pass: strips inside the image with D == Dp take the check-free diagonal loop
+        const bool lrfull = side == 3 && x0 + TX <= W && a.D == G::Dp;
+        if (fast) {
+            if (lrfull) DSX_SEG(true, true);
+            else DSX_SEG(true, false);
+        } else {
+            if (lrfull) DSX_SEG(false, true);
+            else DSX_SEG(false, false);
+        }
+#undef DSX_SEG
     }
     if (a.timeline && tid == 0) {
         const uint64_t t_end = __builtin_amdgcn_s_memrealtime();

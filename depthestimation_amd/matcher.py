@@ -297,6 +297,18 @@ def rectify_device(img, mapx=None, mapy=None, out=None, stream=None):
     return out
 
 
+def _keep_until_done(t, stream):
+    """A workspace tensor dropped when the call returns is handed back to torch's caching
+    allocator at once; when the kernels run on another stream than torch's current one, mark it
+    used there so the block is not reused before they finish."""
+    import torch
+    if stream is None:
+        return
+    st = stream if isinstance(stream, torch.cuda.Stream) else torch.cuda.ExternalStream(int(stream), device=t.device)
+    if st.cuda_stream != torch.cuda.current_stream(t.device).cuda_stream:
+        t.record_stream(st)
+
+
 def postprocess_full_device(disp, crop, max_speckle_size=50, max_diff=1.0, apply_outlier_removal=True,
                             outlier_threshold=3.0, outlier_kernel=5, focal_length=None, baseline=None, doffs=0.0,
                             eps=1e-6, max_depth=None, stream=None, apply_hole_filling=False, fill_kernel=3):
@@ -328,6 +340,7 @@ def postprocess_full_device(disp, crop, max_speckle_size=50, max_diff=1.0, apply
         float(doffs or 0.0), float(eps), float(max_depth or 0.0), int(max_depth is not None), ws.data_ptr(),
         nbytes, sptr)
     _dsx.check(rc, "dsx_postprocess_full_ex_device")
+    _keep_until_done(ws, stream)
     return out_disp, out_depth
 
 
@@ -354,4 +367,5 @@ def fill_holes_device(disp, radius=5, out=None, stream=None):
     rc = L.dsx_fill_holes_device(disp.data_ptr(), H, W, disp.stride(0), int(radius), out.data_ptr(), ws.data_ptr(),
                                  nbytes, sptr)
     _dsx.check(rc, "dsx_fill_holes_device")
+    _keep_until_done(ws, stream)
     return out

@@ -111,8 +111,18 @@ def sharded_map(frames: Iterable, slots: Sequence[int], make_fn: Callable[[int],
     def worker(slot: int, dev: int):
         try:
             fn = make_fn(dev)
+            poll = getattr(fn, "poll", None) if pipelined else None
             while True:
-                item = inq[slot].get()
+                if poll is not None:
+                    # a live or slow source: publish frames whose GPU work has finished while
+                    # waiting for the next input, instead of when their ring slot comes round again
+                    try:
+                        item = inq[slot].get(timeout=0.002)
+                    except queue.Empty:
+                        publish(poll())
+                        continue
+                else:
+                    item = inq[slot].get()
                 if item is _STOP:
                     if pipelined:
                         publish(fn.drain_all())
@@ -203,7 +213,12 @@ class HostPipeline:
     (2, H, W) torch tensor (copied to the device straight from it, as a decoder writing into pinned
     buffers would hand frames over).  Results are int16 x16 maps (the cv2 StereoMatcher.compute
     contract, stereo_core.py:231) in pinned host memory: ``copy=False`` returns views that stay
-    valid until ``depth`` further frames are pushed."""
+    valid until ``depth`` further frames are pushed.
+
+    Buffer lifetime: a pinned tensor input is read by an asynchronous copy on the frame's stream,
+    so the caller must not modify it until that frame's result has been returned (by ``push``,
+    ``poll`` or ``drain_all``); a decoder reusing a pinned ring needs a ring at least ``depth + 1``
+    frames deep.  Numpy inputs are copied into the slot inside ``push`` and may be reused at once."""
 
     def __init__(self, device: int, depth: int = 3, streams: int = 2, copy: bool = True, **matcher_kw):
         import torch
@@ -237,8 +252,19 @@ class HostPipeline:
         out = self.hfx[i % (2 * self.depth)].numpy()
         return i, (out.copy() if self.copy else out)
 
+    def poll(self, keep: int = -1) -> List[Tuple[int, np.ndarray]]:
+        """The oldest frames in flight whose GPU work has already finished (no waiting), in frame
+        order up to the first unfinished one; frame ``keep`` stays in flight."""
+        out = []
+        for j, s in sorted((p[0], s) for s, p in enumerate(self.pending) if p is not None):
+            if j == keep or not self.pending[s][1].query():
+                break
+            out.append(self._finish(s))
+        return out
+
     def push(self, i: int, pair) -> List[Tuple[int, np.ndarray]]:
-        """Enqueue frame ``i``; returns the frames this completed (at most one), oldest first."""
+        """Enqueue frame ``i``; returns the frames that completed, oldest first: the one whose
+        ring slot this frame takes (waited for) and any other finished ones (not waited for)."""
         torch = self.torch
         if isinstance(pair, torch.Tensor):
             if pair.dtype != torch.uint8 or pair.dim() != 3 or pair.shape[0] != 2 or pair.is_cuda:
@@ -273,6 +299,7 @@ class HostPipeline:
             ev = torch.cuda.Event()
             ev.record(st)
         self.pending[slot] = (i, ev)
+        done.extend(self.poll(keep=i))
         return done
 
     def drain_all(self) -> List[Tuple[int, np.ndarray]]:
@@ -355,7 +382,18 @@ class DepthPipeline:
             ev = torch.cuda.Event()
             ev.record(st)
         self.pending[slot] = (i, ev, zshape)
+        done.extend(self.poll(keep=i))
         return done
+
+    def poll(self, keep: int = -1) -> List[Tuple[int, Optional[np.ndarray]]]:
+        """The oldest frames in flight whose GPU work has already finished (no waiting), in frame
+        order up to the first unfinished one; frame ``keep`` stays in flight."""
+        out = []
+        for j, s in sorted((p[0], s) for s, p in enumerate(self.pending) if p is not None):
+            if j == keep or not self.pending[s][1].query():
+                break
+            out.append(self._finish(s))
+        return out
 
     def drain_all(self) -> List[Tuple[int, Optional[np.ndarray]]]:
         live = sorted((p[0], s) for s, p in enumerate(self.pending) if p is not None)

@@ -121,7 +121,12 @@ int dsx_compute_host(dsx_handle *h, const uint8_t *L, const uint8_t *R, int32_t 
 /* Asynchronous device-pointer compute on `hip_stream` (hipStream_t, NULL = default stream).
  * dL, dR: device uint8 H x W, row stride `stride_bytes`.  d_out_fixed (int16) and
  * d_out_float (float32) are contiguous H x W device buffers; either may be NULL but not
- * both.  No host synchronisation, no allocation when the size matches the cached one. */
+ * both.  No host synchronisation, no allocation when the size matches the cached one.
+ * Calls on different streams through ONE handle are safe: a configuration that uses the handle's
+ * scratch (LR check, volume path, BT cost, SGM, sgbm_post) orders a call on a new stream after the
+ * previous call's last kernel (stream wait on an event, no host wait); the plain fused pass owns no
+ * scratch and runs concurrently.  Inputs and outputs are the caller's: they must stay valid and
+ * unmodified until the work on hip_stream has completed. */
 int dsx_compute_device(dsx_handle *h, const void *dL, const void *dR, int32_t H, int32_t W,
                        int64_t stride_bytes, void *d_out_fixed, void *d_out_float,
                        void *hip_stream);

@@ -72,6 +72,47 @@ def test_sharded_map_early_consumer_exit_does_not_hang():
     assert [r[2] for r in first] == [0, 1, 4, 9, 16]
 
 
+class _FakeStage:
+    """A pipelined stage shaped like HostPipeline: push keeps items in flight, poll publishes the
+    ones whose (simulated) GPU work has finished, drain_all waits for the rest."""
+
+    def __init__(self, dev, log):
+        self.dev, self.log, self.inflight = dev, log, []
+
+    def push(self, i, item):
+        self.inflight.append((i, item, time.monotonic() + 0.003))
+        return []
+
+    def poll(self):
+        now = time.monotonic()
+        done = [(i, (self.dev, x * x)) for i, x, t in self.inflight if t <= now]
+        self.inflight = [e for e in self.inflight if e[2] > now]
+        self.log.extend(i for i, _ in done)
+        return done
+
+    def drain_all(self):
+        done = [(i, (self.dev, x * x)) for i, x, _ in self.inflight]
+        self.inflight = []
+        return done
+
+
+def test_sharded_map_pipelined_polls_while_source_is_slow():
+    """A slow (live) source: finished frames are published by poll() while the worker waits for
+    input, not only when the stream ends (results waited depth*N frames)."""
+    log = []
+
+    def frames():
+        for i in range(12):
+            time.sleep(0.01)
+            yield i
+
+    gen = sharded_map(frames(), [0, 1], lambda dev: _FakeStage(dev, log), queue_depth=2, pipelined=True)
+    out = list(gen)
+    assert [r[1] for r in out] == [i * i for i in range(12)]
+    assert [r[0] for r in out] == [i % 2 for i in range(12)]
+    assert len(log) >= 8  # most frames came out through poll(), not drain_all at STOP
+
+
 def test_comm_rejects_invisible_devices(gpu_available):
     if gpu_available:
         pytest.skip("CPU-only check")
