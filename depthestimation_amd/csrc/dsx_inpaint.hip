@@ -9,17 +9,28 @@
 //   T(p)   = min over the 4 quadrants of Telea's upwind solve from earlier-layer neighbours' T;
 //   value  = sum w v / sum w over earlier-layer pixels q with 0 < |p-q|^2 <= r^2 (offset order),
 //            w = max(|(p-q).gradT| / |p-q| / |p-q|^2 / (1 + |T(q) - T(p)|), 1e-6).
-// One launch per layer: a layer only reads pixels whose layer is < k, which no thread of that
-// launch writes (a pixel being filled goes from "queued" straight to k), so a launch is race-free
-// and the kernel boundary orders the layers.  The frontiers are explicit lists: layer k's launch
-// walks list k and queues the still-untouched hole 4-neighbours of the pixels it fills (one CAS
-// unfilled -> queued each, so a pixel is listed once) as list k+1 - exactly layer k+1.  Layers run
-// in batches with one host read-back of the next frontier's size per batch; the loop ends at the
-// first empty frontier.
+//
+// The layers are known before the march: a hole pixel's layer is its 4-connected (BFS) distance
+// through holes to the nearest known pixel, and that equals its plain L1 distance to the nearest
+// known pixel (the known pixel q nearest in L1 is joined to p by a monotone lattice path whose inner
+// pixels are all holes, else one of them would be nearer).  So the layers come from a separable L1
+// distance transform (row scans, then column scans), the hole pixels are bucketed by layer with a
+// counting sort, and the march visits list k at step k.  Nothing is read back to the host:
+//   inp_rows     copy, T init, distance to the nearest known pixel of the row (block scans)
+//   inp_cols     column pass of the L1 transform (segment summaries + scans) -> layer map
+//   inp_hist     per-layer counts and the deepest layer K (LDS histograms)
+//   inp_scan     per-layer list offsets
+//   inp_scatter  hole pixels into their layer's list
+//   inp_layer    one launch per layer k = 1..L0, enqueued without waiting; a launch past K exits
+//   inp_rest     layers L0+1..K, if any, in ONE persistent launch with a grid barrier per layer
+// L0 follows the deepest layer of the previous call (written by the device into mapped host memory),
+// so a video stream normally finishes in the per-layer launches and the persistent kernel exits at
+// once.  A layer only reads pixels of earlier layers and writes its own, so the kernel boundary (or
+// the barrier) is the only ordering the march needs.
 #include "dsx_internal.h"
 
 #include <algorithm>
-#include <vector>
+#include <cstdlib>
 
 namespace dsx {
 
@@ -27,8 +38,12 @@ namespace dsx {
 
 namespace {
 
-constexpr int kUnfilled = 0x7FFFFFFF;  // hole pixel not yet in any frontier list
-constexpr int kQueued = 0x7FFFFFFE;    // listed for the next layer (still >= every layer index)
+constexpr int kFar = 1 << 28;             // "no known pixel" in the distance transform
+constexpr int kUnreached = 0x7FFFFFFF;    // layer of a hole no known pixel reaches
+constexpr int kCtlK = 0, kCtlBar = 1, kCtlTmo = 2;
+constexpr int kCtlWords = 64;
+constexpr int kHistBins = 2048;           // LDS histogram bins of inp_hist / inp_scatter
+constexpr int kChunk = 4096;              // pixels per block of inp_hist / inp_scatter
 
 __device__ __forceinline__ double telea_solve(double t1, double t2) {
     if (t1 < 1e6 && t2 < 1e6) {
@@ -42,92 +57,213 @@ __device__ __forceinline__ double telea_solve(double t1, double t2) {
     return 1.0 + (t1 < t2 ? t1 : t2);
 }
 
-__device__ __forceinline__ uint64_t lanes_below(int lane) { return (1ull << lane) - 1ull; }
+// ---- L1 distance transform -------------------------------------------------------------------
 
-// A block's slice of the next frontier list, gathered in LDS and appended with one global atomic
-// per flush: a wave-per-atomic append serialises on the one counter when a frontier is tens of
-// thousands of pixels (the first layers of a map with scattered holes).
-template <int CAP>
-struct BlockQueue {
-    int buf[CAP];
-    int n, base;
-};
-
-// Adds the lanes with `want` set (one LDS atomic per wave).  Called by the whole wave.
-template <int CAP>
-__device__ __forceinline__ void bq_push(BlockQueue<CAP> &bq, bool want, int value) {
-    const int lane = threadIdx.x & 63;
-    const uint64_t m = __ballot(want);
-    if (!m) return;
-    int at = 0;
-    if (lane == 0) at = atomicAdd(&bq.n, __popcll(m));
-    at = __shfl(at, 0);
-    if (want) bq.buf[at + __popcll(m & lanes_below(lane))] = value;
-}
-
-// Moves the gathered entries to list (slots from *cnt).  Called by the whole block; leaves n = 0.
-template <int CAP>
-__device__ __forceinline__ void bq_flush(BlockQueue<CAP> &bq, int *list, int *cnt) {
+// Block-wide inclusive scan over 256 values (Hillis-Steele in LDS); MAXOP: max, else min.
+template <bool MAXOP>
+__device__ __forceinline__ int block_scan(int v, int *buf) {
+    const int t = threadIdx.x;
+    buf[t] = v;
     __syncthreads();
-    const int n = bq.n;
-    if (n) {
-        if (threadIdx.x == 0) bq.base = atomicAdd(cnt, n);
-        __syncthreads();
-        const int base = bq.base;
-        for (int j = threadIdx.x; j < n; j += blockDim.x) list[base + j] = bq.buf[j];
-        __syncthreads();
-        if (threadIdx.x == 0) bq.n = 0;
-    }
-    __syncthreads();
-}
-
-// Copies the map, sets layer 0 / unfilled / T, and lists layer 1: the holes with a known 4-neighbour.
-// Each block covers kInitChunk consecutive pixels and appends its layer-1 pixels with one atomic.
-constexpr int kInitChunk = 4096;
-
-__global__ __launch_bounds__(256) void inpaint_init(const float *in, int64_t pitch, int H, int W, float *out, int *layer,
-                                                    double *T, int *list1, int *cnt1) {
-    __shared__ BlockQueue<kInitChunk> bq;
-    if (threadIdx.x == 0) bq.n = 0;
-    __syncthreads();
-    const int n = H * W;  // < 2^31 (host check)
-    const int c0 = blockIdx.x * kInitChunk;
-    for (int p = c0 + (int)threadIdx.x; p < c0 + kInitChunk; p += 256) {  // block-uniform trip count
-        bool first = false;
-        if (p < n) {
-            const int y = p / W, x = p - y * W;
-            const float *row = in + (int64_t)y * pitch;
-            const float v = row[x];
-            const bool hole = v <= 0.0f;  // fill_holes' mask = disparity <= 0 (postprocess.py:96-97)
-            if (hole)
-                first = (x > 0 && row[x - 1] > 0.0f) || (x < W - 1 && row[x + 1] > 0.0f) ||
-                        (y > 0 && row[x - pitch] > 0.0f) || (y < H - 1 && row[x + pitch] > 0.0f);
-            out[p] = v;
-            layer[p] = hole ? (first ? kQueued : kUnfilled) : 0;
-            T[p] = hole ? 1e6 : 0.0;
+    for (int o = 1; o < 256; o <<= 1) {
+        int u = v;
+        if (MAXOP ? t >= o : t + o < 256) {
+            const int w = buf[MAXOP ? t - o : t + o];
+            u = MAXOP ? (w > v ? w : v) : (w < v ? w : v);
         }
-        bq_push(bq, first, p);
+        __syncthreads();
+        buf[t] = v = u;
+        __syncthreads();
     }
-    bq_flush(bq, list1, cnt1);
+    return v;
 }
+
+// One block per row: out = in, T = 1e6 on holes (else 0), g = distance to the nearest known pixel
+// of the row (kFar if none).  Block 0..: also zeroes the per-layer counters and the control words.
+__global__ __launch_bounds__(256) void inp_rows(const float *in, int64_t pitch, int H, int W, float *out, double *T,
+                                                int *g, int *cnt, int ncnt, int *ctl) {
+    __shared__ int buf[256];
+    const int y = blockIdx.x, t = threadIdx.x;
+    for (int i = y * 256 + t; i < ncnt; i += H * 256) cnt[i] = 0;
+    if (y == 0 && t < kCtlWords) ctl[t] = 0;
+    const float *row = in + (int64_t)y * pitch;
+    const int chunk = (W + 255) / 256;
+    const int x0 = min(W, t * chunk), x1 = min(W, x0 + chunk);
+    int last = -kFar, first = kFar;
+    for (int x = x0; x < x1; ++x) {
+        const float v = row[x];
+        const bool hole = v <= 0.0f;  // fill_holes' mask = disparity <= 0 (postprocess.py:96-97)
+        out[(int64_t)y * W + x] = v;
+        T[(int64_t)y * W + x] = hole ? 1e6 : 0.0;
+        if (!hole) {
+            first = first == kFar ? x : first;
+            last = x;
+        }
+    }
+    // last known left of this chunk, first known right of it
+    const int incl_last = block_scan<true>(last, buf);
+    const int prev_last = t > 0 ? buf[t - 1] : -kFar;
+    (void)incl_last;
+    __syncthreads();
+    block_scan<false>(first, buf);
+    const int next_first = t < 255 ? buf[t + 1] : kFar;
+    int p = prev_last;
+    for (int x = x0; x < x1; ++x) {
+        if (row[x] > 0.0f) p = x;
+        g[(int64_t)y * W + x] = p == -kFar ? kFar : x - p;
+    }
+    int q = next_first;
+    for (int x = x1 - 1; x >= x0; --x) {
+        if (row[x] > 0.0f) q = x;
+        if (q != kFar) {
+            const int64_t o = (int64_t)y * W + x;
+            g[o] = min(g[o], q - x);
+        }
+    }
+}
+
+// Column pass: layer = min over y' of g(x, y') + |y - y'| (exact L1 distance), 0 on known pixels,
+// kUnreached where no known pixel exists.  Block = 64 columns x 16 row segments; each thread
+// summarises its segment for both directions, takes the other segments' summaries from LDS, then
+// scans its segment forwards (into `layer`) and backwards (combining).
+__global__ __launch_bounds__(1024) void inp_cols(const int *g, int H, int W, int *layer) {
+    __shared__ int sf[16][64], sb[16][64];
+    const int cx = threadIdx.x & 63, sj = threadIdx.x >> 6;
+    const int x = blockIdx.x * 64 + cx;
+    const int SL = (H + 15) / 16;
+    const int y0 = min(H, sj * SL), y1 = min(H, y0 + SL);
+    const bool live = x < W;
+    int cf = kFar, cb = kFar;  // min_y g(y) + (y1 - 1 - y) and min_y g(y) + (y - y0)
+    if (live)
+        for (int y = y0; y < y1; ++y) {
+            const int v = g[(int64_t)y * W + x];
+            cf = min(cf, v + (y1 - 1 - y));
+            cb = min(cb, v + (y - y0));
+        }
+    sf[sj][cx] = cf;
+    sb[sj][cx] = cb;
+    __syncthreads();
+    if (!live || y0 >= y1) return;
+    int hf = kFar, hb = kFar;  // distance from rows above y0 (at row y0 - 1) / below y1 - 1 (at row y1)
+    for (int j = 0; j < sj; ++j) {
+        const int ye = min(H, (j + 1) * SL);  // segment j ends at row ye - 1
+        hf = min(hf, sf[j][cx] + (y0 - 1 - (ye - 1)));
+    }
+    for (int j = sj + 1; j < 16; ++j) {
+        const int ys = min(H, j * SL);
+        if (ys < H) hb = min(hb, sb[j][cx] + (ys - y1));
+    }
+    for (int y = y0; y < y1; ++y) {
+        hf = min(g[(int64_t)y * W + x], hf + 1);
+        layer[(int64_t)y * W + x] = hf;
+    }
+    for (int y = y1 - 1; y >= y0; --y) {
+        const int64_t o = (int64_t)y * W + x;
+        hb = min(g[o], hb + 1);
+        const int d = min(layer[o], hb);
+        layer[o] = d >= kFar ? kUnreached : d;  // known pixels: g = 0
+    }
+}
+
+// Per-layer hole counts (cnt[k], k >= 1) and the deepest reached layer ctl[kCtlK].
+__global__ __launch_bounds__(256) void inp_hist(const int *layer, int n, int *cnt, int *ctl) {
+    __shared__ int h[kHistBins];
+    __shared__ int kmax;
+    for (int i = threadIdx.x; i < kHistBins; i += 256) h[i] = 0;
+    if (threadIdx.x == 0) kmax = 0;
+    __syncthreads();
+    const int p0 = blockIdx.x * kChunk;
+    int km = 0;
+    for (int p = p0 + (int)threadIdx.x; p < min(n, p0 + kChunk); p += 256) {
+        const int k = layer[p];
+        if (k > 0 && k != kUnreached) {
+            km = k > km ? k : km;
+            if (k < kHistBins) atomicAdd(&h[k], 1);
+            else atomicAdd(&cnt[k], 1);
+        }
+    }
+    atomicMax(&kmax, km);
+    __syncthreads();
+    for (int i = threadIdx.x; i < kHistBins; i += 256)
+        if (h[i]) atomicAdd(&cnt[i], h[i]);
+    if (threadIdx.x == 0 && kmax) atomicMax(&ctl[kCtlK], kmax);
+}
+
+// off[k] = first list slot of layer k (k = 1..K+1); cur[k] = off[k] (scatter cursors, in place of
+// the counts).  One block.
+__global__ __launch_bounds__(1024) void inp_scan(int *cnt_cur, int *off, const int *ctl, int *host_k) {
+    __shared__ int part[1024];
+    const int K = ctl[kCtlK];
+    const int t = threadIdx.x;
+    const int chunk = (K + 1024) / 1024;  // layers 1..K
+    const int k0 = 1 + t * chunk, k1 = min(K + 1, k0 + chunk);
+    int s = 0;
+    for (int k = k0; k < k1; ++k) s += cnt_cur[k];
+    part[t] = s;
+    __syncthreads();
+    for (int o = 1; o < 1024; o <<= 1) {
+        const int v = t >= o ? part[t - o] : 0;
+        __syncthreads();
+        part[t] += v;
+        __syncthreads();
+    }
+    int base = t > 0 ? part[t - 1] : 0;
+    for (int k = k0; k < k1; ++k) {
+        const int c = cnt_cur[k];
+        off[k] = base;
+        cnt_cur[k] = base;
+        base += c;
+    }
+    if (t == 1023) off[K + 1] = part[1023];
+    if (t == 0 && host_k) __hip_atomic_store(host_k, K, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// Hole pixels into their layer's list (order inside a layer is free: its pixels are independent).
+__global__ __launch_bounds__(256) void inp_scatter(const int *layer, int n, int *cur, int *list) {
+    __shared__ int h[kHistBins], base[kHistBins];
+    constexpr int PER = kChunk / 256;
+    for (int i = threadIdx.x; i < kHistBins; i += 256) h[i] = 0;
+    __syncthreads();
+    const int p0 = blockIdx.x * kChunk;
+    int rank[PER];
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+        const int p = p0 + j * 256 + (int)threadIdx.x;
+        rank[j] = -1;
+        if (p < n) {
+            const int k = layer[p];
+            if (k > 0 && k != kUnreached) {
+                if (k < kHistBins) rank[j] = atomicAdd(&h[k], 1);
+                else list[atomicAdd(&cur[k], 1)] = p;
+            }
+        }
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < kHistBins; i += 256)
+        if (h[i]) base[i] = atomicAdd(&cur[i], h[i]);
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+        const int p = p0 + j * 256 + (int)threadIdx.x;
+        if (rank[j] >= 0) list[base[layer[p]] + rank[j]] = p;
+    }
+}
+
+// ---- the march ------------------------------------------------------------------------------
 
 struct Front {
     double tp, gx, gy;
-    int lay[4];  // the 4-neighbours' layers (up, down, left, right; kQueued when outside the map)
 };
 
-// T and grad T of a frontier pixel p (layer k) from its earlier-layer 4-neighbours (T 1e6 when
-// absent).  The neighbours' layers and T load together (one memory round trip).
+// T and grad T of a pixel p of layer k from its earlier-layer 4-neighbours (T 1e6 when absent).
 __device__ __forceinline__ Front front_of(const int *layer, const double *T, int p, int y, int x, int H, int W, int k) {
     Front f;
     const bool iu = y > 0, id = y < H - 1, il = x > 0, ir = x < W - 1;
-    f.lay[0] = iu ? layer[p - W] : kQueued;
-    f.lay[1] = id ? layer[p + W] : kQueued;
-    f.lay[2] = il ? layer[p - 1] : kQueued;
-    f.lay[3] = ir ? layer[p + 1] : kQueued;
+    const int lu = iu ? layer[p - W] : kUnreached, ld = id ? layer[p + W] : kUnreached;
+    const int ll = il ? layer[p - 1] : kUnreached, lr = ir ? layer[p + 1] : kUnreached;
     const double Tu = iu ? T[p - W] : 1e6, Td = id ? T[p + W] : 1e6;
     const double Tl = il ? T[p - 1] : 1e6, Tr = ir ? T[p + 1] : 1e6;
-    const bool ou = f.lay[0] < k, od = f.lay[1] < k, ol = f.lay[2] < k, orr = f.lay[3] < k;
+    const bool ou = lu < k, od = ld < k, ol = ll < k, orr = lr < k;
     const double tu = ou ? Tu : 1e6, td = od ? Td : 1e6, tl = ol ? Tl : 1e6, tr = orr ? Tr : 1e6;
     const double a0 = telea_solve(tu, tl), a1 = telea_solve(td, tl);
     const double a2 = telea_solve(tu, tr), a3 = telea_solve(td, tr);
@@ -160,164 +296,231 @@ __device__ __forceinline__ bool cell_term(const float *out, const int *layer, co
     return true;
 }
 
-// Claims 4-neighbour `dir` (0..3 = up, down, left, right) of a pixel just filled for layer k+1:
-// only a neighbour that was still unfilled when the pixel's step read it can be, and the CAS makes
-// one claimant win.
-__device__ __forceinline__ bool claim_neighbour(int *layer, const Front &f, int p, int W, int dir, int &q) {
-    q = dir == 0 ? p - W : dir == 1 ? p + W : dir == 2 ? p - 1 : p + 1;
-    return f.lay[dir] == kUnfilled && atomicCAS(&layer[q], kUnfilled, kQueued) == kUnfilled;
-}
-
-constexpr int kQueueCap = 2048;  // per-block next-frontier entries between flushes
-
-// One frontier pixel per half-wave (radius <= 7): its 32 lanes evaluate the window cells (row-major
-// cell c on lane c mod 32 in pass c / 32: the divisions, square roots and neighbour loads run in
-// parallel), then every lane accumulates the terms in cell order through shuffles - the operation
-// sequence of the host restatement's loop, so the result keeps its bits.  (One pixel per thread left
-// a layer of a few thousand frontier pixels to a few dozen waves walking 28 dependent
-// double-precision terms each: ~30 us per layer at C4.)  Lanes 0-3 then claim the 4 neighbours.
+// Layer k's pixels list[beg..end), work item i = (global half-wave); radius <= 7: one pixel per
+// half-wave, its 32 lanes evaluate the window cells (row-major cell c on lane c mod 32 in pass c / 32)
+// and then every lane accumulates the terms in cell order through shuffles - the operation sequence
+// of the host restatement's loop, so the result keeps its bits.
 template <int NPASS>
-__global__ __launch_bounds__(256) void inpaint_layer_hw(float *out, int *layer, double *T, int H, int W, int radius,
-                                                        int k, const int *list, const int *cnt, int *nlist, int *ncnt) {
-    const int count = *cnt;
-    if ((int)blockIdx.x * 8 >= count) return;  // block-uniform
-    __shared__ BlockQueue<kQueueCap> bq;
-    if (threadIdx.x == 0) bq.n = 0;
-    __syncthreads();
-    const int hl = threadIdx.x & 31;  // lane within the half-wave
+__device__ __forceinline__ void march_layer_hw(float *out, const int *layer, double *T, int H, int W, int radius, int k,
+                                               const int *list, int beg, int end, int hw0, int hwstride) {
+    const int hl = threadIdx.x & 31;
     const int r2 = radius * radius, side = 2 * radius + 1, ncell = side * side;
-    for (int b0 = blockIdx.x * 8; b0 < count; b0 += gridDim.x * 8) {  // block-uniform trip count
-        const int i = b0 + ((int)threadIdx.x >> 5);
-        const bool valid = i < count;
-        const int p = valid ? list[i] : 0;
+    for (int i = beg + hw0; i < end; i += hwstride) {  // half-wave-uniform
+        const int p = list[i];
         const int y = p / W, x = p - y * W;
-        bool want = false;
-        int q = 0;
-        if (valid) {
-            const Front f = front_of(layer, T, p, y, x, H, W, k);
-            double wt[NPASS], wv[NPASS];
+        const Front f = front_of(layer, T, p, y, x, H, W, k);
+        double wt[NPASS], wv[NPASS];
 #pragma unroll
-            for (int ps = 0; ps < NPASS; ++ps) {
-                const int c = ps * 32 + hl;
-                wt[ps] = 0.0;  // w >= 1e-6 on every used cell: 0 marks the unused ones
-                wv[ps] = 0.0;
-                if (c < ncell)
-                    cell_term(out, layer, T, y, x, c / side - radius, c % side - radius, H, W, r2, k, f, wt[ps], wv[ps]);
-            }
-            double num = 0.0, den = 0.0;
+        for (int ps = 0; ps < NPASS; ++ps) {
+            const int c = ps * 32 + hl;
+            wt[ps] = 0.0;  // w >= 1e-6 on every used cell: 0 marks the unused ones
+            wv[ps] = 0.0;
+            if (c < ncell) cell_term(out, layer, T, y, x, c / side - radius, c % side - radius, H, W, r2, k, f, wt[ps], wv[ps]);
+        }
+        double num = 0.0, den = 0.0;
 #pragma unroll
-            for (int ps = 0; ps < NPASS; ++ps) {
-                const int nc = ncell - ps * 32 < 32 ? ncell - ps * 32 : 32;
-                for (int s = 0; s < nc; ++s) {
-                    const double w = __shfl(wt[ps], s, 32), v = __shfl(wv[ps], s, 32);
-                    if (w != 0.0) {
-                        num = num + v;
-                        den = den + w;
-                    }
+        for (int ps = 0; ps < NPASS; ++ps) {
+            const int nc = ncell - ps * 32 < 32 ? ncell - ps * 32 : 32;
+            for (int s = 0; s < nc; ++s) {
+                const double w = __shfl(wt[ps], s, 32), v = __shfl(wv[ps], s, 32);
+                if (w != 0.0) {
+                    num = num + v;
+                    den = den + w;
                 }
             }
-            if (hl == 0) {
-                if (den > 0) out[p] = (float)(num / den);
-                T[p] = f.tp;
-                layer[p] = k;
-            }
-            if (hl < 4) want = claim_neighbour(layer, f, p, W, hl, q);
         }
-        bq_push(bq, want, q);
-        __syncthreads();
-        const int held = bq.n;
-        __syncthreads();  // every thread has read it before the next pushes
-        if (held > kQueueCap - 32) bq_flush(bq, nlist, ncnt);
+        if (hl == 0) {
+            if (den > 0) out[p] = (float)(num / den);
+            T[p] = f.tp;
+        }
     }
-    bq_flush(bq, nlist, ncnt);
 }
 
 // Larger windows: one pixel per thread, cells walked in order.
-__global__ __launch_bounds__(256) void inpaint_layer_px(float *out, int *layer, double *T, int H, int W, int radius,
-                                                        int k, const int *list, const int *cnt, int *nlist, int *ncnt) {
-    const int count = *cnt;
-    if ((int)blockIdx.x * 256 >= count) return;
-    __shared__ BlockQueue<kQueueCap> bq;
-    if (threadIdx.x == 0) bq.n = 0;
-    __syncthreads();
+__device__ __forceinline__ void march_layer_px(float *out, const int *layer, double *T, int H, int W, int radius, int k,
+                                               const int *list, int beg, int end, int t0, int tstride) {
     const int r2 = radius * radius;
-    for (int b0 = blockIdx.x * 256; b0 < count; b0 += gridDim.x * 256) {
-        const int i = b0 + (int)threadIdx.x;
-        const bool valid = i < count;
-        const int p = valid ? list[i] : 0;
+    for (int i = beg + t0; i < end; i += tstride) {
+        const int p = list[i];
         const int y = p / W, x = p - y * W;
-        Front f;
-        if (valid) {
-            f = front_of(layer, T, p, y, x, H, W, k);
-            double num = 0.0, den = 0.0;
-            for (int oy = -radius; oy <= radius; ++oy)
-                for (int ox = -radius; ox <= radius; ++ox) {
-                    double w, wv;
-                    if (cell_term(out, layer, T, y, x, oy, ox, H, W, r2, k, f, w, wv)) {
-                        num = num + wv;
-                        den = den + w;
-                    }
+        const Front f = front_of(layer, T, p, y, x, H, W, k);
+        double num = 0.0, den = 0.0;
+        for (int oy = -radius; oy <= radius; ++oy)
+            for (int ox = -radius; ox <= radius; ++ox) {
+                double w, wv;
+                if (cell_term(out, layer, T, y, x, oy, ox, H, W, r2, k, f, w, wv)) {
+                    num = num + wv;
+                    den = den + w;
                 }
-            if (den > 0) out[p] = (float)(num / den);
-            T[p] = f.tp;
-            layer[p] = k;
-        }
-        for (int dir = 0; dir < 4; ++dir) {
-            int q = 0;
-            const bool want = valid && claim_neighbour(layer, f, p, W, dir, q);
-            bq_push(bq, want, q);
-        }
-        __syncthreads();
-        const int held = bq.n;
-        __syncthreads();
-        if (held > kQueueCap - 1024) bq_flush(bq, nlist, ncnt);
+            }
+        if (den > 0) out[p] = (float)(num / den);
+        T[p] = f.tp;
     }
-    bq_flush(bq, nlist, ncnt);
+}
+
+template <int NPASS>
+__device__ __forceinline__ void march_layer(float *out, const int *layer, double *T, int H, int W, int radius, int k,
+                                            const int *list, int beg, int end, int blk, int nblk) {
+    if constexpr (NPASS > 0)
+        march_layer_hw<NPASS>(out, layer, T, H, W, radius, k, list, beg, end, blk * 8 + (int)(threadIdx.x >> 5),
+                              nblk * 8);
+    else
+        march_layer_px(out, layer, T, H, W, radius, k, list, beg, end, blk * 256 + (int)threadIdx.x, nblk * 256);
+}
+
+// Step k of the march (a launch past the deepest layer does nothing).
+template <int NPASS>
+__global__ __launch_bounds__(256) void inp_layer(float *out, const int *layer, double *T, int H, int W, int radius,
+                                                 int k, const int *list, const int *off, const int *ctl) {
+    if (k > ctl[kCtlK]) return;
+    const int beg = off[k], end = off[k + 1];
+    march_layer<NPASS>(out, layer, T, H, W, radius, k, list, beg, end, blockIdx.x, gridDim.x);
+}
+
+// Grid barrier (one monotonic counter): every wave drains its stores, lane 0 of the block releases
+// them to the device (agent scope), arrives, polls the counter relaxed with s_sleep, then acquires
+// (invalidates this CU's L1) before any wave reads pixels other blocks wrote.  Spins are bounded: on
+// a timeout the block sets the timeout word and every block leaves the march.
+__device__ __forceinline__ bool grid_barrier(unsigned *ctr, unsigned target, int *tmo) {
+    __shared__ int ok;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        int good = 1;
+        for (unsigned spins = 0; __hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target; ++spins) {
+            __builtin_amdgcn_s_sleep(2);
+            if ((spins & 255u) == 255u &&
+                (spins > (1u << 22) || __hip_atomic_load(tmo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))) {
+                __hip_atomic_store(tmo, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                good = 0;
+                break;
+            }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        ok = good;
+    }
+    __syncthreads();
+    return ok;
+}
+
+// Layers k0..K in one persistent launch (grid = one block per CU, all resident), a grid barrier
+// between layers.  Exits at once when the per-layer launches already reached K.
+template <int NPASS>
+__global__ __launch_bounds__(256) void inp_rest(float *out, const int *layer, double *T, int H, int W, int radius,
+                                                int k0, const int *list, const int *off, int *ctl) {
+    const int K = ctl[kCtlK];
+    if (k0 > K) return;  // grid-uniform
+    unsigned epoch = 0;
+    for (int k = k0; k <= K; ++k) {
+        march_layer<NPASS>(out, layer, T, H, W, radius, k, list, off[k], off[k + 1], blockIdx.x, gridDim.x);
+        if (k == K) break;
+        ++epoch;
+        if (!grid_barrier(reinterpret_cast<unsigned *>(ctl + kCtlBar), epoch * gridDim.x, ctl + kCtlTmo)) return;
+    }
 }
 
 size_t align256(size_t b) { return (b + 255) & ~(size_t)255; }
+
+struct Views {
+    int *layer, *g, *list, *cnt, *off, *ctl;
+    double *T;
+    int ncnt;
+};
+
+Views views(void *ws, int H, int W) {
+    const size_t n = (size_t)H * W;
+    const int ncnt = H + W + 3;  // layers 0..H+W (+1 end slot)
+    uint8_t *w = static_cast<uint8_t *>(ws);
+    Views v;
+    v.ncnt = ncnt;
+    v.layer = reinterpret_cast<int *>(w);
+    w += align256(n * 4);
+    v.T = reinterpret_cast<double *>(w);
+    w += align256(n * 8);
+    v.g = reinterpret_cast<int *>(w);
+    w += align256(n * 4);
+    v.list = reinterpret_cast<int *>(w);
+    w += align256(n * 4);
+    v.cnt = reinterpret_cast<int *>(w);
+    w += align256((size_t)ncnt * 4);
+    v.off = reinterpret_cast<int *>(w);
+    w += align256((size_t)ncnt * 4);
+    v.ctl = reinterpret_cast<int *>(w);
+    return v;
+}
+
+// The deepest layer of the previous call (any device / stream): the device writes it into mapped
+// host memory; it only sizes the next call's run of per-layer launches.
+int *lastk_host() {
+    static int *p = [] {
+        int *h = nullptr;
+        if (hipHostMalloc(&h, 64, hipHostMallocMapped | hipHostMallocPortable) != hipSuccess) return (int *)nullptr;
+        *h = -1;
+        return h;
+    }();
+    return p;
+}
 
 }  // namespace
 
 size_t inpaint_workspace(int H, int W) {
     const size_t n = (size_t)H * W;
-    // layer | T | 2 frontier lists (ping-pong) | per-layer frontier sizes
-    return align256(n * 4) + align256(n * 8) + 2 * align256(n * 4) + align256((size_t)(H + W + 3) * 4);
+    const size_t ncnt = (size_t)H + W + 3;
+    return align256(n * 4) + align256(n * 8) + 2 * align256(n * 4) + 2 * align256(ncnt * 4) + align256(kCtlWords * 4);
 }
 
 hipError_t launch_inpaint(const float *in, int64_t pitch, int H, int W, int radius, float *out, void *ws, hipStream_t st) {
-    const size_t n = (size_t)H * W;
-    uint8_t *w = static_cast<uint8_t *>(ws);
-    int *layer = reinterpret_cast<int *>(w);
-    double *T = reinterpret_cast<double *>(w + align256(n * 4));
-    int *lists[2] = {reinterpret_cast<int *>(w + align256(n * 4) + align256(n * 8)),
-                     reinterpret_cast<int *>(w + align256(n * 4) + align256(n * 8) + align256(n * 4))};
-    int *cnt = reinterpret_cast<int *>(w + align256(n * 4) + align256(n * 8) + 2 * align256(n * 4));
-    const int maxk = H + W + 1;  // no 4-connected distance exceeds H + W
-    const int grid = (int)((n + kInitChunk - 1) / kInitChunk);
-    hipError_t e = hipMemsetAsync(cnt, 0, (size_t)(maxk + 2) * 4, st);  // cnt[k] = size of layer k
-    if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(inpaint_init, dim3(grid), dim3(256), 0, st, in, pitch, H, W, out, layer, T, lists[1], cnt + 1);
+    const int n = H * W;  // < 2^31 (host check)
+    const Views v = views(ws, H, W);
+    hipError_t e;
+    hipLaunchKernelGGL(inp_rows, dim3(H), dim3(256), 0, st, in, pitch, H, W, out, v.T, v.g, v.cnt, v.ncnt, v.ctl);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     if (radius < 1) return hipSuccess;  // no neighbourhood: nothing changes (cv2 uses radius >= 1)
-    // a fixed grid strides over each frontier's device-side size (8 half-waves or 256 threads a
-    // block; the blocks past it return at once); batches of 8 layers between read-backs of the next frontier's size
-    constexpr int kBatch = 8;
+    hipLaunchKernelGGL(inp_cols, dim3((W + 63) / 64), dim3(1024), 0, st, v.g, H, W, v.layer);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    const int nch = (n + kChunk - 1) / kChunk;
+    hipLaunchKernelGGL(inp_hist, dim3(nch), dim3(256), 0, st, v.layer, n, v.cnt, v.ctl);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    int *hk = lastk_host();
+    int *hk_dev = nullptr;
+    if (hk && hipHostGetDevicePointer(reinterpret_cast<void **>(&hk_dev), hk, 0) != hipSuccess) hk_dev = nullptr;
+    hipLaunchKernelGGL(inp_scan, dim3(1), dim3(1024), 0, st, v.cnt, v.off, v.ctl, hk_dev);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    hipLaunchKernelGGL(inp_scatter, dim3(nch), dim3(256), 0, st, v.layer, n, v.cnt, v.list);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+
+    // per-layer launches, enqueued without waiting: as many as the previous call needed (+4), at
+    // least 8; the persistent kernel takes whatever is left
+    const int maxk = H + W;
+    const int prev = hk ? __atomic_load_n(hk, __ATOMIC_RELAXED) : -1;
+    int L0 = std::min(maxk, prev < 0 ? 64 : std::max(8, prev + 4));
+    if (const char *fl = getenv("DSX_INPAINT_L0")) L0 = std::min(maxk, std::max(0, atoi(fl)));  // tests: force the split
     const bool hw = radius <= 7;
-    const int lgrid = (int)std::min<size_t>(hw ? (n + 7) / 8 : (n + 255) / 256, 2048);
-    auto lay = radius <= 3 ? inpaint_layer_hw<2> : radius <= 5 ? inpaint_layer_hw<4> : hw ? inpaint_layer_hw<8>
-                                                                                          : inpaint_layer_px;
-    for (int k0 = 1; k0 <= maxk; k0 += kBatch) {
-        const int k1 = std::min(maxk, k0 + kBatch - 1);
-        for (int k = k0; k <= k1; ++k) {
-            hipLaunchKernelGGL(lay, dim3(lgrid), dim3(256), 0, st, out, layer, T, H, W, radius, k, lists[k & 1], cnt + k,
-                               lists[(k + 1) & 1], cnt + k + 1);
-            if ((e = hipGetLastError()) != hipSuccess) return e;
+    const int np = radius <= 3 ? 2 : radius <= 5 ? 4 : hw ? 8 : 0;
+    const int lgrid = (int)std::min<size_t>(hw ? ((size_t)n + 7) / 8 : ((size_t)n + 255) / 256, 1024);
+    auto lay = np == 2 ? inp_layer<2> : np == 4 ? inp_layer<4> : np == 8 ? inp_layer<8> : inp_layer<0>;
+    for (int k = 1; k <= L0; ++k) {
+        hipLaunchKernelGGL(lay, dim3(lgrid), dim3(256), 0, st, out, v.layer, v.T, H, W, radius, k, v.list, v.off, v.ctl);
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+    }
+    if (L0 < maxk) {
+        static int ncu[64] = {};
+        int dev = 0;
+        if ((e = hipGetDevice(&dev)) != hipSuccess) return e;
+        if (dev < 0 || dev >= 64) return hipErrorInvalidDevice;
+        if (!ncu[dev]) {
+            int c = 0;
+            if ((e = hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev)) != hipSuccess) return e;
+            ncu[dev] = c > 0 ? c : 1;
         }
-        int next = 0;
-        if ((e = hipMemcpyAsync(&next, cnt + k1 + 1, 4, hipMemcpyDeviceToHost, st)) != hipSuccess) return e;
-        if ((e = hipStreamSynchronize(st)) != hipSuccess) return e;
-        if (next == 0) break;
+        auto rest = np == 2 ? inp_rest<2> : np == 4 ? inp_rest<4> : np == 8 ? inp_rest<8> : inp_rest<0>;
+        hipLaunchKernelGGL(rest, dim3(ncu[dev]), dim3(256), 0, st, out, v.layer, v.T, H, W, radius, L0 + 1, v.list, v.off,
+                           v.ctl);
+        if ((e = hipGetLastError()) != hipSuccess) return e;
     }
     return hipSuccess;
 }

@@ -162,7 +162,7 @@ hipError_t launch_sgbm_post(const int16_t *in, int H, int W, int newv, int max_s
 hipError_t launch_post_full(PostFullArgs a, void *ws, hipStream_t st);
 
 // Hole filling (dsx_inpaint.hip): fill_holes(method='inpaint') on d <= 0, layered Telea marching.
-// Synchronises the stream once per 8 layers (frontier read-back).
+// Asynchronous: nothing is read back to the host.
 size_t inpaint_workspace(int H, int W);
 hipError_t launch_inpaint(const float *in, int64_t pitch, int H, int W, int radius, float *out, void *ws, hipStream_t st);
 

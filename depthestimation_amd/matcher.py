@@ -314,8 +314,8 @@ def postprocess_full_device(disp, crop, max_speckle_size=50, max_diff=1.0, apply
                             eps=1e-6, max_depth=None, stream=None, apply_hole_filling=False, fill_kernel=3):
     """postprocess_disparity (postprocess.py:120-171) + depth on the device
     (dsx_postprocess_full_ex_device): speckles -> outliers -> hole filling
-    (Telea 'inpaint' with radius ``fill_kernel`` when ``apply_hole_filling``; synchronises the
-    stream then) -> 3x3 median -> depth.  ``disp``: float32 H x W HIP tensor.
+    (Telea 'inpaint' with radius ``fill_kernel`` when ``apply_hole_filling``) -> 3x3 median -> depth,
+    all enqueued on ``stream`` without host synchronisation.  ``disp``: float32 H x W HIP tensor.
     Returns (disp_cropped, depth or None) as HIP tensors."""
     import torch
 
@@ -348,7 +348,7 @@ def fill_holes_device(disp, radius=5, out=None, stream=None):
     """fill_holes(disparity, method='inpaint', kernel_size=radius) on the device
     (postprocess.py:72-118; dsx_fill_holes_device): Telea inpainting of the pixels <= 0, equal to
     the host restatement (postprocess._telea_inpaint).  ``disp``: float32 H x W HIP tensor (unit
-    column stride).  Synchronises ``stream``; returns the filled float32 H x W tensor."""
+    column stride).  Asynchronous on ``stream``; returns the filled float32 H x W tensor."""
     import torch
 
     if disp.dtype != torch.float32 or disp.dim() != 2 or disp.stride(1) != 1 or not disp.is_cuda:

@@ -177,8 +177,7 @@ int dsx_postprocess_full_device(const void *d_disp, int32_t H, int32_t W, int64_
 
 /* As dsx_postprocess_full_device, with hole filling (StereoCore hole_filling=True: fill_holes
  * method 'inpaint', postprocess.py:160-166, stereo_core.py:175-184) between the outlier removal and
- * the median when fill_radius > 0 (the reference passes fill_kernel 3, postprocess.py:165).
- * Synchronous when fill_radius > 0 (see dsx_fill_holes_device). */
+ * the median when fill_radius > 0 (the reference passes fill_kernel 3, postprocess.py:165). Async. */
 int dsx_postprocess_full_ex_device(const void *d_disp, int32_t H, int32_t W, int64_t in_pitch, int32_t crop,
                                    int32_t max_speckle_size, double max_diff, int32_t apply_outlier_removal,
                                    double outlier_threshold, int32_t outlier_kernel, int32_t fill_radius,
@@ -190,8 +189,9 @@ int dsx_postprocess_full_ex_device(const void *d_disp, int32_t H, int32_t W, int
  * cv2.inpaint INPAINT_TELEA on d <= 0): Telea fast-marching inpainting marched in 4-connected
  * distance layers, equal bit for bit to the host restatement (postprocess.py _telea_inpaint).
  * d_disp: float32 H x W, row pitch `in_pitch` elements; d_out: contiguous float32 H x W.
- * d_workspace: >= dsx_fill_holes_workspace_bytes(H, W).  Enqueued on hip_stream and synchronised
- * with it once per 8 layers (frontier read-back); returns when the result is complete. */
+ * d_workspace: >= dsx_fill_holes_workspace_bytes(H, W).  Asynchronous on hip_stream: the layers come
+ * from an L1 distance transform on the device, the march runs as per-layer launches plus one
+ * persistent launch for any layers beyond them; nothing is read back to the host. */
 size_t dsx_fill_holes_workspace_bytes(int32_t H, int32_t W);
 int dsx_fill_holes_device(const void *d_disp, int32_t H, int32_t W, int64_t in_pitch, int32_t radius, void *d_out,
                           void *d_workspace, size_t workspace_bytes, void *hip_stream);

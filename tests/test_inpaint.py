@@ -159,3 +159,43 @@ def test_process_pair_device_with_hole_filling_matches_host():
     torch.cuda.synchronize()
     np.testing.assert_array_equal(dd.cpu().numpy(), hd)
     np.testing.assert_array_equal(dz.cpu().numpy(), hz)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("l0", ["0", "3", "5000"])
+def test_fill_holes_device_layer_split(l0, monkeypatch):
+    """The march's two forms: per-layer launches for layers 1..L0 and the persistent kernel (grid
+    barrier per layer) for the rest - all of them in the persistent kernel (L0 = 0), a split
+    (L0 = 3) and none (L0 = 5000) - on maps whose deepest layer is 1 to ~400."""
+    import torch
+    from depthestimation_amd.matcher import fill_holes_device
+    monkeypatch.setenv("DSX_INPAINT_L0", l0)
+    d1 = np.zeros((160, 240), np.float32)
+    d1[7, 200] = 5.0                                   # one known pixel: ~390 layers
+    d1[150, 3] = 9.0
+    d2 = _holey(90, 130, 11, frac=0.3)                 # scattered holes: few layers
+    d3 = np.zeros((64, 64), np.float32)                # nothing known: nothing reached
+    for d, r in ((d1, 3), (d2, 5), (d3, 3), (_holey(50, 70, 12), 9)):
+        ref = pp.fill_holes(d, method="inpaint", kernel_size=r)
+        got = fill_holes_device(torch.from_numpy(d).cuda(), radius=r)
+        np.testing.assert_array_equal(got.cpu().numpy(), ref)
+
+
+@pytest.mark.gpu
+def test_fill_holes_device_does_not_block():
+    """dsx_fill_holes_device only enqueues: behind a long-running kernel on the same stream the call
+    returns while the stream is still busy, and the result is right once it drains."""
+    import torch
+    from depthestimation_amd.matcher import fill_holes_device
+    d = _holey(200, 300, 13, frac=0.25)
+    ref = pp.fill_holes(d, method="inpaint", kernel_size=3)
+    x = torch.from_numpy(d).cuda()
+    st = torch.cuda.Stream()
+    torch.cuda.synchronize()
+    with torch.cuda.stream(st):
+        torch.cuda._sleep(200_000_000)  # ~0.1 s of GPU time ahead of the fill
+        got = fill_holes_device(x, radius=3, stream=st)
+        busy = not st.query()
+    st.synchronize()
+    assert busy
+    np.testing.assert_array_equal(got.cpu().numpy(), ref)
