@@ -41,6 +41,9 @@
 #ifndef DSX_WPE
 #define DSX_WPE 3
 #endif
+#ifndef DSX_EXP  // experiment bits (tools/exp_build.sh; timing only, results wrong): 1 no LR exit
+#define DSX_EXP 0  // stores, 2 no LR atomics, 4 no diagonal minima, 8 no dstar store, 16 scan argmin on LR
+#endif
 #ifndef DSX_WPE_SSD
 #define DSX_WPE_SSD 4
 #endif
@@ -671,7 +674,10 @@ __device__ __forceinline__ void bm2_segment(const Bm2Args &a, uint8_t *smem, int
                             // (C << 16) | d by byte permute
                             const uint32_t kE = __builtin_amdgcn_perm(as1(acc), (uint32_t)d0, selE);
                             const uint32_t kO = __builtin_amdgcn_perm(as1(acc), (uint32_t)(d0 + 1), selO);
-                            if constexpr (FULL) {
+                            if constexpr (DSX_EXP & 4) {
+                                Ae = kE;
+                                Ao = kO;
+                            } else if constexpr (FULL) {
                                 if (k > 0) {
                                     const uint32_t nE = min_shr1(Ao, kE);
                                     Ao = umin2(Ae, kO);
@@ -691,7 +697,7 @@ __device__ __forceinline__ void bm2_segment(const Bm2Args &a, uint8_t *smem, int
                                     Ao = umin2(Ao, kO);
                                 }
                             }
-                            if (k < TX - 1 && top) *reinterpret_cast<uint32_t *>(xq + k * PITCH) = Ao;  // exit
+                            if (!(DSX_EXP & 1) && k < TX - 1 && top) *reinterpret_cast<uint32_t *>(xq + k * PITCH) = Ao;  // exit
                         }
                     }
                 };
@@ -702,7 +708,8 @@ __device__ __forceinline__ void bm2_segment(const Bm2Args &a, uint8_t *smem, int
                 else diag_loop(std::false_type{});
                 uint32_t *krow = a.lr_keys + fout + (long)y * W;
                 const int dtop = (wv + 1) * G::LDW - 1;  // disparity of the wave's top slot
-                if constexpr (SSD) {
+                if constexpr (DSX_EXP & 2) {
+                } else if constexpr (SSD) {
                     const int xe = x0 + (TX - 2 - ln) - m - dtop;  // E lane j: exit of pixel TX-2-j
                     if (ln < TX - 1 && E != 0xFFFFFFFFu && xe >= 0 && xe < W) atomicMin(krow + xe, E);
                 } else if (ln < TX - 1) {
@@ -711,8 +718,8 @@ __device__ __forceinline__ void bm2_segment(const Bm2Args &a, uint8_t *smem, int
                     if (E != 0xFFFFFFFFu && xe >= 0 && xe < W) atomicMin(krow + xe, E);
                 }
                 const int xa = x0 + TX - 1 - m - d0;
-                if (Ae != 0xFFFFFFFFu && xa >= 0 && xa < W) atomicMin(krow + xa, Ae);
-                if constexpr (!SSD) {
+                if (!(DSX_EXP & 2) && Ae != 0xFFFFFFFFu && xa >= 0 && xa < W) atomicMin(krow + xa, Ae);
+                if constexpr (!SSD && !(DSX_EXP & 2)) {
                     if (Ao != 0xFFFFFFFFu && xa - 1 >= 0 && xa - 1 < W) atomicMin(krow + xa - 1, Ao);
                 }
             } else if (lane_writes) {
@@ -779,7 +786,7 @@ __device__ __forceinline__ void bm2_segment(const Bm2Args &a, uint8_t *smem, int
             // Two argmin forms, chosen per instantiation from measurements (r01e): the key tree
             // wins on the LR pass (C3, C4) and 15x15 windows (C5); the compare/select scan keeps
             // the SIDE 0 pass at <= 11x11 at 151 VGPRs (the key tree costs C2 +7 %).
-            constexpr bool KEYS = (SIDE == 3 && DSX_LR_KEYS) || R >= 6;
+            constexpr bool KEYS = (SIDE == 3 && DSX_LR_KEYS && !(DSX_EXP & 16)) || R >= 6;
             uint32_t cb, dl;
             if constexpr (KEYS) {
                 // lowest-d argmin without compare/select scans: keys (cost << GB | global block) give
@@ -904,7 +911,7 @@ __device__ __forceinline__ void bm2_segment(const Bm2Args &a, uint8_t *smem, int
                     if (a.float_mode == 1) pf = (float)(m + b) + (float)(cm - cp) / (float)(2 * den);
                 }
                 if (h == 0 && x < W) {
-                    if (lr_on) a.dstar[o] = valid ? (int16_t)b : (int16_t)-1;  // LR check: lr_fixup
+                    if (lr_on && !(DSX_EXP & 8)) a.dstar[o] = valid ? (int16_t)b : (int16_t)-1;  // LR check: lr_fixup
                     const int16_t fx = valid ? (int16_t)(m * 16 + f) : (int16_t)((m - 1) * 16);
                     if (a.out_fixed) a.out_fixed[o] = fx;
                     if (a.out_float) a.out_float[o] = a.float_mode == 0 ? (float)fx * 0.0625f : (valid ? pf : (float)(m - 1));

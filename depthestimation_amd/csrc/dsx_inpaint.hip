@@ -123,14 +123,15 @@ __global__ __launch_bounds__(256) void inp_rows(const float *in, int64_t pitch, 
 }
 
 // Column pass: layer = min over y' of g(x, y') + |y - y'| (exact L1 distance), 0 on known pixels,
-// kUnreached where no known pixel exists.  Block = 64 columns x 16 row segments; each thread
+// kUnreached where no known pixel exists.  Block = 16 columns x 64 row segments; each thread
 // summarises its segment for both directions, takes the other segments' summaries from LDS, then
 // scans its segment forwards (into `layer`) and backwards (combining).
+constexpr int kColW = 16, kColS = 64;
 __global__ __launch_bounds__(1024) void inp_cols(const int *g, int H, int W, int *layer) {
-    __shared__ int sf[16][64], sb[16][64];
-    const int cx = threadIdx.x & 63, sj = threadIdx.x >> 6;
-    const int x = blockIdx.x * 64 + cx;
-    const int SL = (H + 15) / 16;
+    __shared__ int sf[kColS][kColW], sb[kColS][kColW];
+    const int cx = threadIdx.x % kColW, sj = threadIdx.x / kColW;
+    const int x = blockIdx.x * kColW + cx;
+    const int SL = (H + kColS - 1) / kColS;
     const int y0 = min(H, sj * SL), y1 = min(H, y0 + SL);
     const bool live = x < W;
     int cf = kFar, cb = kFar;  // min_y g(y) + (y1 - 1 - y) and min_y g(y) + (y - y0)
@@ -147,9 +148,9 @@ __global__ __launch_bounds__(1024) void inp_cols(const int *g, int H, int W, int
     int hf = kFar, hb = kFar;  // distance from rows above y0 (at row y0 - 1) / below y1 - 1 (at row y1)
     for (int j = 0; j < sj; ++j) {
         const int ye = min(H, (j + 1) * SL);  // segment j ends at row ye - 1
-        hf = min(hf, sf[j][cx] + (y0 - 1 - (ye - 1)));
+        hf = min(hf, sf[j][cx] + (y0 - ye));
     }
-    for (int j = sj + 1; j < 16; ++j) {
+    for (int j = sj + 1; j < kColS; ++j) {
         const int ys = min(H, j * SL);
         if (ys < H) hb = min(hb, sb[j][cx] + (ys - y1));
     }
@@ -296,40 +297,46 @@ __device__ __forceinline__ bool cell_term(const float *out, const int *layer, co
     return true;
 }
 
-// Layer k's pixels list[beg..end), work item i = (global half-wave); radius <= 7: one pixel per
-// half-wave, its 32 lanes evaluate the window cells (row-major cell c on lane c mod 32 in pass c / 32)
-// and then every lane accumulates the terms in cell order through shuffles - the operation sequence
-// of the host restatement's loop, so the result keeps its bits.
+__device__ __forceinline__ double readlane_f64(double v, int s) {
+    const uint64_t b = __builtin_bit_cast(uint64_t, v);
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)b, s);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(b >> 32), s);
+    return __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
+}
+
+// Layer k's pixels list[beg..end), one pixel per wave (radius <= 7): lane c evaluates window cell
+// c + 64 pass (row-major; the divisions, square roots and neighbour loads in parallel), then the
+// terms are summed in cell order through v_readlane - the operation sequence of the host
+// restatement's loop, so the result keeps its bits.  Unused cells hold exact zeros, and adding +0.0
+// to the (positive) partial sums changes nothing, so the sum runs over all 64 lanes unrolled.
 template <int NPASS>
-__device__ __forceinline__ void march_layer_hw(float *out, const int *layer, double *T, int H, int W, int radius, int k,
-                                               const int *list, int beg, int end, int hw0, int hwstride) {
-    const int hl = threadIdx.x & 31;
+__device__ __forceinline__ void march_layer_wave(float *out, const int *layer, double *T, int H, int W, int radius,
+                                                 int k, const int *list, int beg, int end, int w0, int wstride) {
+    const int ln = threadIdx.x & 63;
     const int r2 = radius * radius, side = 2 * radius + 1, ncell = side * side;
-    for (int i = beg + hw0; i < end; i += hwstride) {  // half-wave-uniform
+    for (int i = beg + w0; i < end; i += wstride) {  // wave-uniform
         const int p = list[i];
         const int y = p / W, x = p - y * W;
         const Front f = front_of(layer, T, p, y, x, H, W, k);
         double wt[NPASS], wv[NPASS];
 #pragma unroll
         for (int ps = 0; ps < NPASS; ++ps) {
-            const int c = ps * 32 + hl;
-            wt[ps] = 0.0;  // w >= 1e-6 on every used cell: 0 marks the unused ones
+            const int c = ps * 64 + ln;
+            wt[ps] = 0.0;
             wv[ps] = 0.0;
             if (c < ncell) cell_term(out, layer, T, y, x, c / side - radius, c % side - radius, H, W, r2, k, f, wt[ps], wv[ps]);
         }
         double num = 0.0, den = 0.0;
 #pragma unroll
         for (int ps = 0; ps < NPASS; ++ps) {
-            const int nc = ncell - ps * 32 < 32 ? ncell - ps * 32 : 32;
-            for (int s = 0; s < nc; ++s) {
-                const double w = __shfl(wt[ps], s, 32), v = __shfl(wv[ps], s, 32);
-                if (w != 0.0) {
-                    num = num + v;
-                    den = den + w;
-                }
+#pragma unroll 8
+            for (int s = 0; s < 64; ++s) {  // 8 cells per trip: unrolled fully, the readlanes were
+                                             // all hoisted into 256 SGPRs and spilled
+                num = num + readlane_f64(wv[ps], s);
+                den = den + readlane_f64(wt[ps], s);
             }
         }
-        if (hl == 0) {
+        if (ln == 0) {
             if (den > 0) out[p] = (float)(num / den);
             T[p] = f.tp;
         }
@@ -362,8 +369,8 @@ template <int NPASS>
 __device__ __forceinline__ void march_layer(float *out, const int *layer, double *T, int H, int W, int radius, int k,
                                             const int *list, int beg, int end, int blk, int nblk) {
     if constexpr (NPASS > 0)
-        march_layer_hw<NPASS>(out, layer, T, H, W, radius, k, list, beg, end, blk * 8 + (int)(threadIdx.x >> 5),
-                              nblk * 8);
+        march_layer_wave<NPASS>(out, layer, T, H, W, radius, k, list, beg, end, blk * 4 + (int)(threadIdx.x >> 6),
+                                nblk * 4);
     else
         march_layer_px(out, layer, T, H, W, radius, k, list, beg, end, blk * 256 + (int)threadIdx.x, nblk * 256);
 }
@@ -480,7 +487,7 @@ hipError_t launch_inpaint(const float *in, int64_t pitch, int H, int W, int radi
     hipLaunchKernelGGL(inp_rows, dim3(H), dim3(256), 0, st, in, pitch, H, W, out, v.T, v.g, v.cnt, v.ncnt, v.ctl);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     if (radius < 1) return hipSuccess;  // no neighbourhood: nothing changes (cv2 uses radius >= 1)
-    hipLaunchKernelGGL(inp_cols, dim3((W + 63) / 64), dim3(1024), 0, st, v.g, H, W, v.layer);
+    hipLaunchKernelGGL(inp_cols, dim3((W + kColW - 1) / kColW), dim3(1024), 0, st, v.g, H, W, v.layer);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     const int nch = (n + kChunk - 1) / kChunk;
     hipLaunchKernelGGL(inp_hist, dim3(nch), dim3(256), 0, st, v.layer, n, v.cnt, v.ctl);
@@ -499,10 +506,10 @@ hipError_t launch_inpaint(const float *in, int64_t pitch, int H, int W, int radi
     const int prev = hk ? __atomic_load_n(hk, __ATOMIC_RELAXED) : -1;
     int L0 = std::min(maxk, prev < 0 ? 64 : std::max(8, prev + 4));
     if (const char *fl = getenv("DSX_INPAINT_L0")) L0 = std::min(maxk, std::max(0, atoi(fl)));  // tests: force the split
-    const bool hw = radius <= 7;
-    const int np = radius <= 3 ? 2 : radius <= 5 ? 4 : hw ? 8 : 0;
-    const int lgrid = (int)std::min<size_t>(hw ? ((size_t)n + 7) / 8 : ((size_t)n + 255) / 256, 1024);
-    auto lay = np == 2 ? inp_layer<2> : np == 4 ? inp_layer<4> : np == 8 ? inp_layer<8> : inp_layer<0>;
+    const bool wv = radius <= 7;  // one pixel per wave; larger windows one per thread
+    const int np = radius <= 3 ? 1 : radius <= 5 ? 2 : wv ? 4 : 0;
+    const int lgrid = (int)std::min<size_t>(wv ? ((size_t)n + 3) / 4 : ((size_t)n + 255) / 256, 2048);
+    auto lay = np == 1 ? inp_layer<1> : np == 2 ? inp_layer<2> : np == 4 ? inp_layer<4> : inp_layer<0>;
     for (int k = 1; k <= L0; ++k) {
         hipLaunchKernelGGL(lay, dim3(lgrid), dim3(256), 0, st, out, v.layer, v.T, H, W, radius, k, v.list, v.off, v.ctl);
         if ((e = hipGetLastError()) != hipSuccess) return e;
@@ -517,7 +524,7 @@ hipError_t launch_inpaint(const float *in, int64_t pitch, int H, int W, int radi
             if ((e = hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev)) != hipSuccess) return e;
             ncu[dev] = c > 0 ? c : 1;
         }
-        auto rest = np == 2 ? inp_rest<2> : np == 4 ? inp_rest<4> : np == 8 ? inp_rest<8> : inp_rest<0>;
+        auto rest = np == 1 ? inp_rest<1> : np == 2 ? inp_rest<2> : np == 4 ? inp_rest<4> : inp_rest<0>;
         hipLaunchKernelGGL(rest, dim3(ncu[dev]), dim3(256), 0, st, out, v.layer, v.T, H, W, radius, L0 + 1, v.list, v.off,
                            v.ctl);
         if ((e = hipGetLastError()) != hipSuccess) return e;
