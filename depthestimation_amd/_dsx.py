@@ -38,6 +38,9 @@ EXPORTS = (
 )
 
 
+LR_FORM = {"bm": 0, "sgbm": 1}  # DSX_LR_FORM_* (include/dsx.h)
+
+
 class DsxParams(ctypes.Structure):
     _fields_ = [
         ("min_disp", ctypes.c_int32),
@@ -58,7 +61,8 @@ class DsxParams(ctypes.Structure):
         ("sgbm_post", ctypes.c_int32),
         ("speckle_window_size", ctypes.c_int32),
         ("speckle_range", ctypes.c_int32),
-        ("reserved", ctypes.c_int32 * 4),
+        ("lr_form", ctypes.c_int32),
+        ("reserved", ctypes.c_int32 * 3),
     ]
 
 
@@ -157,7 +161,7 @@ def default_params() -> DsxParams:
 def make_params(min_disp=0, num_disp=128, block_size=5, cost="sad", uniqueness_ratio=10,
                 disp12_max_diff=1, subpixel=True, float_mode="fixed", path="fused",
                 timing=False, grid_blocks=0, aggregation=None, p1=0, p2=0, prefilter_cap=31,
-                sgbm_post=False, speckle_window_size=50, speckle_range=2) -> DsxParams:
+                sgbm_post=False, speckle_window_size=50, speckle_range=2, lr_form="bm") -> DsxParams:
     p = default_params()
     p.min_disp = int(min_disp)
     p.num_disp = int(num_disp)
@@ -185,6 +189,9 @@ def make_params(min_disp=0, num_disp=128, block_size=5, cost="sad", uniqueness_r
     p.sgbm_post = int(bool(sgbm_post))
     p.speckle_window_size = int(speckle_window_size)
     p.speckle_range = int(speckle_range)
+    if lr_form not in LR_FORM:
+        raise ValueError(f"lr_form must be one of {list(LR_FORM)}")
+    p.lr_form = LR_FORM[lr_form]
     return p
 
 

@@ -46,7 +46,7 @@ bool pick_geometry(const dsx_params &p, dsx::Geometry &g) {
         return e && *e == '1';
     }();
     const bool sad1 = !no_sad1 && cost == DSX_COST_SAD && D <= 64 && p.path == DSX_PATH_FUSED &&
-                      p.aggregation == DSX_AGG_NONE;
+                      p.aggregation == DSX_AGG_NONE && p.lr_form == DSX_LR_FORM_BM;
     const bool lane1 = cost == DSX_COST_SSD || sad1;  // one disparity per lane
     g.kind = cost == DSX_COST_SSD ? dsx::BM_SSD : (sad1 ? dsx::BM_SAD1 : dsx::BM_SAD);
     const int unit = lane1 ? 64 : 128;
@@ -103,6 +103,8 @@ int check(const dsx_params *p) {
     if (p->float_mode != DSX_FLOAT_FIXED && p->float_mode != DSX_FLOAT_PARABOLA)
         return fail(DSX_EINVAL, "float_mode must be 0 or 1");
     if (p->path != DSX_PATH_FUSED && p->path != DSX_PATH_VOLUME) return fail(DSX_EINVAL, "path must be 0 or 1");
+    if (p->lr_form != DSX_LR_FORM_BM && p->lr_form != DSX_LR_FORM_SGBM)
+        return fail(DSX_EINVAL, "lr_form must be 0 (bm) or 1 (sgbm)");
     if (p->grid_blocks < 0) return fail(DSX_EINVAL, "grid_blocks must be >= 0");
     if (p->min_disp < -2047 || p->min_disp + p->num_disp > 2047)
         return fail(DSX_EINVAL, "min_disp/num_disp out of the int16 x16 fixed-point range");
@@ -226,7 +228,9 @@ int ensure_buffers(dsx_handle *h, int H, int W, bool host_staging, int nframes =
         DSX_HIP(hipMalloc(&h->dFixed, n * 2));
         DSX_HIP(hipMalloc(&h->dFloat, n * 4));
     }
-    if (h->p.disp12_max_diff >= 0 && h->p.path == DSX_PATH_FUSED && h->lrFrames < nframes) {
+    const bool fused = h->p.path == DSX_PATH_FUSED && !h->p.aggregation && h->p.cost != DSX_COST_BT &&
+                       h->p.lr_form == DSX_LR_FORM_BM;
+    if (h->p.disp12_max_diff >= 0 && fused && h->lrFrames < nframes) {
         (void)hipFree(h->lrKeys);
         (void)hipFree(h->dStar);
         h->lrKeys = nullptr;
@@ -244,7 +248,7 @@ int ensure_buffers(dsx_handle *h, int H, int W, bool host_staging, int nframes =
     }
 
     const bool bt = h->p.cost == DSX_COST_BT;
-    if ((h->p.path == DSX_PATH_VOLUME || h->p.aggregation || bt) && !h->vol) {
+    if (!fused && !h->vol) {
         h->vol_bytes = n * h->g.Dp * cbytes;
         DSX_HIP(hipMalloc(&h->vol, h->vol_bytes));
     }
@@ -395,14 +399,14 @@ int run(dsx_handle *h, const void *dL, const void *dR, int H, int W, int64_t str
     const bool bt = h->p.cost == DSX_COST_BT;  // BT costs exist only as a volume
     // sgbm_post: the matcher writes int16 maps into postIn, the tail then writes the outputs
     void *const finalFixed = outFixed, *const finalFloat = outFloat;
-    const bool scratch = h->p.disp12_max_diff >= 0 || h->p.path != DSX_PATH_FUSED || h->p.aggregation || bt ||
-                         h->p.sgbm_post;
+    const bool fused = h->p.path == DSX_PATH_FUSED && !h->p.aggregation && !bt && h->p.lr_form == DSX_LR_FORM_BM;
+    const bool scratch = h->p.disp12_max_diff >= 0 || !fused || h->p.sgbm_post;
     if (scratch && h->scratchPending && h->scratchStream != st) DSX_HIP(hipStreamWaitEvent(st, h->scratchDone, 0));
     if (h->p.sgbm_post) {
         outFixed = h->postIn;
         outFloat = nullptr;
     }
-    if (h->p.path == DSX_PATH_FUSED && !h->p.aggregation && !bt) {
+    if (fused) {
         const bool lr = h->p.disp12_max_diff >= 0;
         dsx::Bm2Args a = base_args(h, H, W, stride);
         a.side = dsx::SIDE_LEFT;
@@ -550,6 +554,7 @@ int run(dsx_handle *h, const void *dL, const void *dR, int H, int W, int64_t str
             v.TPP = h->g.TPP;
             v.uniq = h->p.uniqueness_ratio;
             v.lr = h->p.disp12_max_diff;
+            v.lr_form = h->p.lr_form;
             v.subpix = h->p.subpixel;
             v.float_mode = h->p.float_mode;
             v.out_fixed = outFixed ? static_cast<int16_t *>(outFixed) + fo : nullptr;

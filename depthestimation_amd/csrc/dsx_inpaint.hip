@@ -7,7 +7,8 @@
 // arithmetic; this file follows it operation for operation, float64 throughout, no contraction):
 //   layer k = hole pixels not yet filled with a 4-neighbour in layer k-1 (known pixels: layer 0);
 //   T(p)   = min over the 4 quadrants of Telea's upwind solve from earlier-layer neighbours' T;
-//   value  = sum w v / sum w over earlier-layer pixels q with 0 < |p-q|^2 <= r^2 (offset order),
+//   value  = sum w v / sum w over earlier-layer pixels q with 0 < |p-q|^2 <= r^2 (window rows
+//            summed left to right, then the row sums top to bottom),
 //            w = max(|(p-q).gradT| / |p-q| / |p-q|^2 / (1 + |T(q) - T(p)|), 1e-6).
 //
 // The layers are known before the march: a hole pixel's layer is its 4-connected (BFS) distance
@@ -297,53 +298,44 @@ __device__ __forceinline__ bool cell_term(const float *out, const int *layer, co
     return true;
 }
 
-__device__ __forceinline__ double readlane_f64(double v, int s) {
-    const uint64_t b = __builtin_bit_cast(uint64_t, v);
-    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)b, s);
-    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(b >> 32), s);
-    return __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
-}
-
-// Layer k's pixels list[beg..end), one pixel per wave (radius <= 7): lane c evaluates window cell
-// c + 64 pass (row-major; the divisions, square roots and neighbour loads in parallel), then the
-// terms are summed in cell order through v_readlane - the operation sequence of the host
-// restatement's loop, so the result keeps its bits.  Unused cells hold exact zeros, and adding +0.0
-// to the (positive) partial sums changes nothing, so the sum runs over all 64 lanes unrolled.
-template <int NPASS>
-__device__ __forceinline__ void march_layer_wave(float *out, const int *layer, double *T, int H, int W, int radius,
-                                                 int k, const int *list, int beg, int end, int w0, int wstride) {
-    const int ln = threadIdx.x & 63;
-    const int r2 = radius * radius, side = 2 * radius + 1, ncell = side * side;
-    for (int i = beg + w0; i < end; i += wstride) {  // wave-uniform
+// Layer k's pixels list[beg..end), one pixel per group of G lanes (G = 8 for radius <= 3, 16 for
+// radius <= 7): lane j of the group sums window row j - radius, cell by cell from 0.0 (the divisions,
+// square roots and neighbour loads of the rows in parallel), then the row sums are added top to
+// bottom through shuffles - the order of the host restatement, so the result keeps its bits.
+template <int G>
+__device__ __forceinline__ void march_layer_grp(float *out, const int *layer, double *T, int H, int W, int radius,
+                                                int k, const int *list, int beg, int end, int g0, int gstride) {
+    const int j = threadIdx.x & (G - 1);
+    const int r2 = radius * radius;
+    for (int i = beg + g0; i < end; i += gstride) {  // group-uniform
         const int p = list[i];
         const int y = p / W, x = p - y * W;
         const Front f = front_of(layer, T, p, y, x, H, W, k);
-        double wt[NPASS], wv[NPASS];
-#pragma unroll
-        for (int ps = 0; ps < NPASS; ++ps) {
-            const int c = ps * 64 + ln;
-            wt[ps] = 0.0;
-            wv[ps] = 0.0;
-            if (c < ncell) cell_term(out, layer, T, y, x, c / side - radius, c % side - radius, H, W, r2, k, f, wt[ps], wv[ps]);
+        double rn = 0.0, rd = 0.0;
+        if (j <= 2 * radius) {
+            const int oy = j - radius;
+            for (int ox = -radius; ox <= radius; ++ox) {
+                double w, wv;
+                if (cell_term(out, layer, T, y, x, oy, ox, H, W, r2, k, f, w, wv)) {
+                    rn = rn + wv;
+                    rd = rd + w;
+                }
+            }
         }
         double num = 0.0, den = 0.0;
 #pragma unroll
-        for (int ps = 0; ps < NPASS; ++ps) {
-#pragma unroll 8
-            for (int s = 0; s < 64; ++s) {  // 8 cells per trip: unrolled fully, the readlanes were
-                                             // all hoisted into 256 SGPRs and spilled
-                num = num + readlane_f64(wv[ps], s);
-                den = den + readlane_f64(wt[ps], s);
-            }
+        for (int q = 0; q < G; ++q) {  // rows past 2 radius add +0.0: exact
+            num = num + __shfl(rn, q, G);
+            den = den + __shfl(rd, q, G);
         }
-        if (ln == 0) {
+        if (j == 0) {
             if (den > 0) out[p] = (float)(num / den);
             T[p] = f.tp;
         }
     }
 }
 
-// Larger windows: one pixel per thread, cells walked in order.
+// Larger windows: one pixel per thread, the same row-by-row order.
 __device__ __forceinline__ void march_layer_px(float *out, const int *layer, double *T, int H, int W, int radius, int k,
                                                const int *list, int beg, int end, int t0, int tstride) {
     const int r2 = radius * radius;
@@ -352,36 +344,41 @@ __device__ __forceinline__ void march_layer_px(float *out, const int *layer, dou
         const int y = p / W, x = p - y * W;
         const Front f = front_of(layer, T, p, y, x, H, W, k);
         double num = 0.0, den = 0.0;
-        for (int oy = -radius; oy <= radius; ++oy)
+        for (int oy = -radius; oy <= radius; ++oy) {
+            double rn = 0.0, rd = 0.0;
             for (int ox = -radius; ox <= radius; ++ox) {
                 double w, wv;
                 if (cell_term(out, layer, T, y, x, oy, ox, H, W, r2, k, f, w, wv)) {
-                    num = num + wv;
-                    den = den + w;
+                    rn = rn + wv;
+                    rd = rd + w;
                 }
             }
+            num = num + rn;
+            den = den + rd;
+        }
         if (den > 0) out[p] = (float)(num / den);
         T[p] = f.tp;
     }
 }
 
-template <int NPASS>
+// G > 0: groups of G lanes per pixel; G = 0: one pixel per thread.
+template <int G>
 __device__ __forceinline__ void march_layer(float *out, const int *layer, double *T, int H, int W, int radius, int k,
                                             const int *list, int beg, int end, int blk, int nblk) {
-    if constexpr (NPASS > 0)
-        march_layer_wave<NPASS>(out, layer, T, H, W, radius, k, list, beg, end, blk * 4 + (int)(threadIdx.x >> 6),
-                                nblk * 4);
+    if constexpr (G > 0)
+        march_layer_grp<G>(out, layer, T, H, W, radius, k, list, beg, end, blk * (256 / G) + (int)(threadIdx.x / G),
+                           nblk * (256 / G));
     else
         march_layer_px(out, layer, T, H, W, radius, k, list, beg, end, blk * 256 + (int)threadIdx.x, nblk * 256);
 }
 
 // Step k of the march (a launch past the deepest layer does nothing).
-template <int NPASS>
+template <int G>
 __global__ __launch_bounds__(256) void inp_layer(float *out, const int *layer, double *T, int H, int W, int radius,
                                                  int k, const int *list, const int *off, const int *ctl) {
     if (k > ctl[kCtlK]) return;
     const int beg = off[k], end = off[k + 1];
-    march_layer<NPASS>(out, layer, T, H, W, radius, k, list, beg, end, blockIdx.x, gridDim.x);
+    march_layer<G>(out, layer, T, H, W, radius, k, list, beg, end, blockIdx.x, gridDim.x);
 }
 
 // Grid barrier (one monotonic counter): every wave drains its stores, lane 0 of the block releases
@@ -416,14 +413,14 @@ __device__ __forceinline__ bool grid_barrier(unsigned *ctr, unsigned target, int
 
 // Layers k0..K in one persistent launch (grid = one block per CU, all resident), a grid barrier
 // between layers.  Exits at once when the per-layer launches already reached K.
-template <int NPASS>
+template <int G>
 __global__ __launch_bounds__(256) void inp_rest(float *out, const int *layer, double *T, int H, int W, int radius,
                                                 int k0, const int *list, const int *off, int *ctl) {
     const int K = ctl[kCtlK];
     if (k0 > K) return;  // grid-uniform
     unsigned epoch = 0;
     for (int k = k0; k <= K; ++k) {
-        march_layer<NPASS>(out, layer, T, H, W, radius, k, list, off[k], off[k + 1], blockIdx.x, gridDim.x);
+        march_layer<G>(out, layer, T, H, W, radius, k, list, off[k], off[k + 1], blockIdx.x, gridDim.x);
         if (k == K) break;
         ++epoch;
         if (!grid_barrier(reinterpret_cast<unsigned *>(ctl + kCtlBar), epoch * gridDim.x, ctl + kCtlTmo)) return;
@@ -506,10 +503,11 @@ hipError_t launch_inpaint(const float *in, int64_t pitch, int H, int W, int radi
     const int prev = hk ? __atomic_load_n(hk, __ATOMIC_RELAXED) : -1;
     int L0 = std::min(maxk, prev < 0 ? 64 : std::max(8, prev + 4));
     if (const char *fl = getenv("DSX_INPAINT_L0")) L0 = std::min(maxk, std::max(0, atoi(fl)));  // tests: force the split
-    const bool wv = radius <= 7;  // one pixel per wave; larger windows one per thread
-    const int np = radius <= 3 ? 1 : radius <= 5 ? 2 : wv ? 4 : 0;
-    const int lgrid = (int)std::min<size_t>(wv ? ((size_t)n + 3) / 4 : ((size_t)n + 255) / 256, 2048);
-    auto lay = np == 1 ? inp_layer<1> : np == 2 ? inp_layer<2> : np == 4 ? inp_layer<4> : inp_layer<0>;
+    // lanes per pixel: one per window row (8 up to radius 3, 16 up to 7); larger windows one pixel
+    // per thread.  512 blocks: an empty launch (a layer past K) costs ~1.5 us where 2048 cost ~4.6 us
+    const int np = radius <= 3 ? 8 : radius <= 7 ? 16 : 0;
+    const int lgrid = (int)std::min<size_t>(((size_t)n * (np ? np : 1) + 255) / 256, 512);
+    auto lay = np == 8 ? inp_layer<8> : np == 16 ? inp_layer<16> : inp_layer<0>;
     for (int k = 1; k <= L0; ++k) {
         hipLaunchKernelGGL(lay, dim3(lgrid), dim3(256), 0, st, out, v.layer, v.T, H, W, radius, k, v.list, v.off, v.ctl);
         if ((e = hipGetLastError()) != hipSuccess) return e;
@@ -524,7 +522,7 @@ hipError_t launch_inpaint(const float *in, int64_t pitch, int H, int W, int radi
             if ((e = hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev)) != hipSuccess) return e;
             ncu[dev] = c > 0 ? c : 1;
         }
-        auto rest = np == 1 ? inp_rest<1> : np == 2 ? inp_rest<2> : np == 4 ? inp_rest<4> : inp_rest<0>;
+        auto rest = np == 8 ? inp_rest<8> : np == 16 ? inp_rest<16> : inp_rest<0>;
         hipLaunchKernelGGL(rest, dim3(ncu[dev]), dim3(256), 0, st, out, v.layer, v.T, H, W, radius, L0 + 1, v.list, v.off,
                            v.ctl);
         if ((e = hipGetLastError()) != hipSuccess) return e;

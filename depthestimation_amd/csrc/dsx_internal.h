@@ -56,6 +56,7 @@ struct VolArgs {
     size_t sstride;
     int H, W, m, D, Dp, DB, TPP;
     int uniq, lr, subpix, float_mode;
+    int lr_form;      // DSX_LR_FORM_BM: right-view argmin over every cost; DSX_LR_FORM_SGBM: OpenCV's form
     int16_t *out_fixed;
     float *out_float;
 };

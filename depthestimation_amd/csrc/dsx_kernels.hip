@@ -70,7 +70,9 @@ __device__ __forceinline__ uint32_t slice_cost(const uint4 (&v)[NV], int j) {
     }
 }
 
-template <bool SSD, bool UNIQ, bool LR, int RING, int NSUM = 0>
+// LRM: 0 no left-right check, 1 the A5' form (right-view argmin over every cost), 2 OpenCV
+// StereoSGBM's form (disp2 from the unique left winners, floor / ceiling test; DSX_LR_FORM_SGBM)
+template <bool SSD, bool UNIQ, int LRM, int RING, int NSUM = 0>
 __global__ __launch_bounds__(kVolThreads) void vol_wta(VolArgs a) {
     // NSUM > 0 (SGM, SSD = true): the u32 costs are the sums of NSUM u16 volumes (one L_r per
     // path direction), loaded as 2 x 16 B per volume and summed when the chunk is processed
@@ -84,7 +86,7 @@ __global__ __launch_bounds__(kVolThreads) void vol_wta(VolArgs a) {
     const int TPP = a.Dp / TX, Dp = a.Dp, W = a.W, m = a.m, D = a.D, DB = a.DB;
     const int XC = kVolThreads / TPP;  // pixels per chunk
     const int y = blockIdx.x;
-    constexpr bool lr = LR;
+    constexpr bool lr = LRM != 0;
     // row segment [xa, xb) of this block (gridDim.y segments per row; 1 with the LR check, whose
     // right-view winners need the whole row)
     const int XSg = ((W + gridDim.y - 1) / gridDim.y + XC - 1) / XC * XC;
@@ -182,7 +184,8 @@ __global__ __launch_bounds__(kVolThreads) void vol_wta(VolArgs a) {
         best = group_min(best, TPP);
         const int b = (int)(best & dmask);
         const uint32_t cb = best >> DB;
-        bool valid = inb && x >= m + D - 1 && x <= W - 1 + m;
+        // valid band: A5' [m + D - 1, W - 1 + m]; OpenCV SGBM [max(m + D, 0), W + min(m, 0))
+        bool valid = LRM == 2 ? (inb && x >= max(m + D, 0) && x < W + min(m, 0)) : (inb && x >= m + D - 1 && x <= W - 1 + m);
         if (UNIQ) {
             uint32_t nm = 0xFFFFFFFFu;
 #pragma unroll
@@ -193,7 +196,7 @@ __global__ __launch_bounds__(kVolThreads) void vol_wta(VolArgs a) {
             nm = group_min(nm, TPP);
             if ((uint64_t)nm * (uint64_t)(100 - a.uniq) < (uint64_t)cb * 100u) valid = false;
         }
-        if (lr && inb) {
+        if (LRM == 1 && inb) {
             // right-view winners: C(x, d) competes for xr = x - m - d
 #pragma unroll
             for (int j = 0; j < TX; ++j) {
@@ -225,7 +228,11 @@ __global__ __launch_bounds__(kVolThreads) void vol_wta(VolArgs a) {
             // results go to LDS row buffers: no global stores inside the streaming loop, so the
             // compiler's vmcnt counting stays exact and the ring keeps two chunks in flight
             rowFixed[x - xa] = valid ? fx : (int16_t)((m - 1) * 16);
-            if (lr) rowB[x] = valid ? (int16_t)b : (int16_t)-1;
+            if (LRM == 1) rowB[x] = valid ? (int16_t)b : (int16_t)-1;
+            // OpenCV form: each unique left winner offers (cost, d) to its right pixel; minimum
+            // cost, equal costs -> the largest x (OpenCV's descending x loop, strict '>'), i.e.
+            // the largest d: key (cost << DB) | (dmask - d)
+            if (LRM == 2 && valid) atomicMin(&bestR[ridx(x - m - b)], (cb << DB) | (dmask - (uint32_t)b));
             if (a.float_mode == 1) rowF[x - xa] = valid ? pf : (float)(m - 1);
         }
         if (a.subpix) __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront", "local");  // reads before next writes
@@ -248,7 +255,7 @@ __global__ __launch_bounds__(kVolThreads) void vol_wta(VolArgs a) {
     for (int x = xa + tid; x < xb; x += kVolThreads) {
         int16_t fx = (int16_t)rowFixed[x - xa];
         bool valid = true;
-        if (lr) {
+        if (LRM == 1) {
             const int b = rowB[x];
             valid = b >= 0;
             if (valid) {
@@ -257,6 +264,24 @@ __global__ __launch_bounds__(kVolThreads) void vol_wta(VolArgs a) {
                 if (df > a.lr || df < -a.lr) valid = false;
             }
             if (!valid) fx = (int16_t)((m - 1) * 16);
+        } else if (LRM == 2) {
+            // both the floor and the ceiling of the sub-pixel disparity must fail, each against a
+            // right pixel inside the image that holds a winner (disp2 >= minD)
+            const int inv = (m - 1) * 16;
+            valid = fx != inv;
+            if (valid) {
+                const int d12 = a.lr > 0 ? a.lr : 1;
+                auto fails = [&](int dq) __attribute__((always_inline)) {
+                    const int xq = x - dq;
+                    if (xq < 0 || xq >= W) return false;
+                    const uint32_t key = bestR[ridx(xq)];
+                    if (key == 0xFFFFFFFFu) return false;
+                    const int d2 = m + (int)(dmask - (key & dmask));
+                    return d2 - dq > d12 || dq - d2 > d12;
+                };
+                if (fails((int)fx >> 4) && fails(((int)fx + 15) >> 4)) valid = false;
+            }
+            if (!valid) fx = (int16_t)inv;
         }
         const long o = (long)y * W + x;
         if (a.out_fixed) a.out_fixed[o] = fx;
@@ -332,13 +357,14 @@ size_t volume_smem_bytes(int TX, bool ssd, int Dp, int TPP, int W) {
     return vol_smem(ssd, W, W, true, true);  // the largest form (one segment per row, LR, float_mode 1)
 }
 
-template <bool SSD, bool UNIQ, bool LR, int RING, int NSUM = 0>
+template <bool SSD, bool UNIQ, int LRM, int RING, int NSUM = 0>
 static hipError_t launch_vol_ring(const VolArgs &a, hipStream_t st) {
+    constexpr bool LR = LRM != 0;
     static bool attr_done[64] = {};
     int dev = 0;
     (void)hipGetDevice(&dev);
     if (dev < 0 || dev >= 64 || !attr_done[dev]) {
-        hipError_t e = hipFuncSetAttribute((const void *)vol_wta<SSD, UNIQ, LR, RING, NSUM>,
+        hipError_t e = hipFuncSetAttribute((const void *)vol_wta<SSD, UNIQ, LRM, RING, NSUM>,
                                            hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         if (e != hipSuccess) return e;
         if (dev >= 0 && dev < 64) attr_done[dev] = true;
@@ -353,20 +379,25 @@ static hipError_t launch_vol_ring(const VolArgs &a, hipStream_t st) {
     const int XC = kVolThreads / (a.Dp / 16);
     const int XSg = ((a.W + nseg - 1) / nseg + XC - 1) / XC * XC;  // as the kernel computes it
     const size_t smem = vol_smem(SSD, std::min(XSg, a.W), a.W, LR, a.float_mode == 1);
-    hipLaunchKernelGGL((vol_wta<SSD, UNIQ, LR, RING, NSUM>), dim3(a.H, nseg), dim3(kVolThreads), smem, st, a);
+    hipLaunchKernelGGL((vol_wta<SSD, UNIQ, LRM, RING, NSUM>), dim3(a.H, nseg), dim3(kVolThreads), smem, st, a);
     return hipGetLastError();
 }
 
-template <bool SSD, bool UNIQ, bool LR>
-static hipError_t launch_vol_one(const VolArgs &a, hipStream_t st) {
-    return launch_vol_ring<SSD, UNIQ, LR, 3>(a, st);
+// LR form: 0 off, 1 A5' (disp12_max_diff >= 0), 2 OpenCV SGBM (always on, disp12MaxDiff >= 1)
+static int lr_mode(const VolArgs &a) { return a.lr_form == 1 ? 2 : (a.lr >= 0 ? 1 : 0); }
+
+template <bool SSD, bool UNIQ, int RING, int NSUM = 0>
+static hipError_t launch_vol_lr(const VolArgs &a, hipStream_t st) {
+    switch (lr_mode(a)) {
+        case 0: return launch_vol_ring<SSD, UNIQ, 0, RING, NSUM>(a, st);
+        case 1: return launch_vol_ring<SSD, UNIQ, 1, RING, NSUM>(a, st);
+        default: return launch_vol_ring<SSD, UNIQ, 2, RING, NSUM>(a, st);
+    }
 }
 
 template <bool SSD>
 static hipError_t launch_vol_cost(const VolArgs &a, hipStream_t st) {
-    const bool u = a.uniq > 0, l = a.lr >= 0;
-    if (u) return l ? launch_vol_one<SSD, true, true>(a, st) : launch_vol_one<SSD, true, false>(a, st);
-    return l ? launch_vol_one<SSD, false, true>(a, st) : launch_vol_one<SSD, false, false>(a, st);
+    return a.uniq > 0 ? launch_vol_lr<SSD, true, 3>(a, st) : launch_vol_lr<SSD, false, 3>(a, st);
 }
 
 // summed SGM volumes: ring depth 3 up to 4 directions, 2 beyond (register budget of 2 x 16 B per
@@ -374,9 +405,7 @@ static hipError_t launch_vol_cost(const VolArgs &a, hipStream_t st) {
 template <int N>
 static hipError_t launch_vol_sum(const VolArgs &a, hipStream_t st) {
     constexpr int RING = N <= 4 ? 3 : 2;
-    const bool u = a.uniq > 0, l = a.lr >= 0;
-    if (u) return l ? launch_vol_ring<true, true, true, RING, N>(a, st) : launch_vol_ring<true, true, false, RING, N>(a, st);
-    return l ? launch_vol_ring<true, false, true, RING, N>(a, st) : launch_vol_ring<true, false, false, RING, N>(a, st);
+    return a.uniq > 0 ? launch_vol_lr<true, true, RING, N>(a, st) : launch_vol_lr<true, false, RING, N>(a, st);
 }
 
 hipError_t launch_volume_wta(int TX, bool ssd, const VolArgs &a, hipStream_t st) {

@@ -112,8 +112,9 @@ def _telea_inpaint(img: np.ndarray, hole: np.ndarray, radius: int) -> np.ndarray
       * grad T at p from central / one-sided differences of earlier-layer neighbours' T;
       * value(p) = sum w(q) v(q) / sum w(q) over earlier-layer q with 0 < |p - q|^2 <= radius^2,
         w = max(|(p - q) . grad T| / |p - q| * 1 / |p - q|^2 * 1 / (1 + |T(q) - T(p)|), 1e-6)
-        (direction, distance and level-set factors), summed in float64 in offset order, rounded
-        to float32 once.
+        (direction, distance and level-set factors), summed in float64 row by row (each window
+        row's cells left to right from 0.0, then the row sums top to bottom - the order the GPU
+        sums in, one lane per window row), rounded to float32 once.
     Hole pixels no layer reaches (no known pixel in their region) keep their value.  Parity with
     OpenCV's heap order is unpinned (cv2 absent); the device kernel equals this bit for bit."""
     H, W = img.shape
@@ -151,19 +152,26 @@ def _telea_inpaint(img: np.ndarray, hole: np.ndarray, radius: int) -> np.ndarray
         gy = np.where(od & ou, (td - tu) * 0.5, np.where(od, td - tp, np.where(ou, tp - tu, 0.0)))
         num = np.zeros(ys.size)
         den = np.zeros(ys.size)
-        for oy, ox in offs:
-            yy, xx = ys + oy, xs + ox
-            inb = (yy >= 0) & (yy < H) & (xx >= 0) & (xx < W)
-            yc, xc = np.clip(yy, 0, H - 1), np.clip(xx, 0, W - 1)
-            ok = inb & (layer[yc, xc] < k)
-            ry, rx = -oy, -ox
-            d2 = ry * ry + rx * rx
-            w_dir = np.abs(ry * gy + rx * gx) / np.sqrt(float(d2))
-            w_dst = 1.0 / d2
-            w_lev = 1.0 / (1.0 + np.abs(T[yc, xc] - tp))
-            w = np.maximum(w_dir * w_dst * w_lev, 1e-6)
-            num = np.where(ok, num + w * out[yc, xc].astype(np.float64), num)
-            den = np.where(ok, den + w, den)
+        for oyr in range(-radius, radius + 1):
+            rn = np.zeros(ys.size)
+            rd = np.zeros(ys.size)
+            for oy, ox in offs:
+                if oy != oyr:
+                    continue
+                yy, xx = ys + oy, xs + ox
+                inb = (yy >= 0) & (yy < H) & (xx >= 0) & (xx < W)
+                yc, xc = np.clip(yy, 0, H - 1), np.clip(xx, 0, W - 1)
+                ok = inb & (layer[yc, xc] < k)
+                ry, rx = -oy, -ox
+                d2 = ry * ry + rx * rx
+                w_dir = np.abs(ry * gy + rx * gx) / np.sqrt(float(d2))
+                w_dst = 1.0 / d2
+                w_lev = 1.0 / (1.0 + np.abs(T[yc, xc] - tp))
+                w = np.maximum(w_dir * w_dst * w_lev, 1e-6)
+                rn = np.where(ok, rn + w * out[yc, xc].astype(np.float64), rn)
+                rd = np.where(ok, rd + w, rd)
+            num = num + rn  # +0.0 for a row without terms: exact
+            den = den + rd
         fill = den > 0
         vals = out[ys, xs]
         vals[fill] = (num[fill] / den[fill]).astype(np.float32)

@@ -16,6 +16,11 @@ Keys added to ``sgbm_params`` (accepted by ``configure_sgbm`` like the reference
                                        (min_disp - 1) * 16)
   'subpixel' : bool                   (1/16-px parabola refinement, on by default)
   'device'   : int                    (HIP device of the matcher)
+  'lr_form'  : 'bm' | 'sgbm'          ('bm', the default: the A5' right-view argmin over every cost;
+                                       'sgbm': cv2.StereoSGBM's own check - disp2 from the unique left
+                                       winners, floor / ceiling test, disp12MaxDiff >= 1, its valid
+                                       band [max(min_disp + num_disp, 0), W + min(min_disp, 0));
+                                       runs on the volume path)
   'aggregation': 'none' | 'sgm'       ('none', the default, is the north-star block matching;
                                        'sgm' adds semi-global aggregation over the SAD costs with
                                        the path set of 'sgbm_mode' and P1 = 8 bs^2, P2 = 32 bs^2 as
@@ -23,8 +28,8 @@ Keys added to ``sgbm_params`` (accepted by ``configure_sgbm`` like the reference
 Keys of the reference that have no block-matching meaning are kept, validated and reported
 but do not change the result: 'prefilter_cap' unless 'cost' is 'bt', 'speckle_window_size' /
 'speckle_range' unless 'sgbm_post' is set, and 'sgbm_mode' / P1 / P2 while 'aggregation' is 'none'
-(SURVEY.md 8a A5').  cost='bt' + aggregation='sgm' + sgbm_post=True is this build's closest form
-of the reference's cv2.StereoSGBM (its LR check stays the A5' one).
+(SURVEY.md 8a A5').  cost='bt' + aggregation='sgm' + lr_form='sgbm' + sgbm_post=True is this build's
+closest form of the reference's cv2.StereoSGBM.
 
 There is no CPU fallback: without libdsx.so or a HIP device ``compute_disparity`` raises.
 """
@@ -113,6 +118,7 @@ class StereoCore:
             'device': 0,
             'aggregation': 'none',
             'sgbm_post': False,
+            'lr_form': 'bm',
         }
         self._build_sgbm()
         self.disparity_map = None
@@ -145,6 +151,7 @@ class StereoCore:
             sgbm_post=bool(p.get('sgbm_post', False)),
             speckle_window_size=p['speckle_window_size'],
             speckle_range=p['speckle_range'],
+            lr_form=p.get('lr_form', 'bm'),
         )
         if old is not None:
             old.close()

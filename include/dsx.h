@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define DSX_VERSION 101 /* 1.0.1: DSX_COST_BT, dsx_params.prefilter_cap */
+#define DSX_VERSION 102 /* 1.0.2: dsx_params.lr_form (OpenCV StereoSGBM left-right check form) */
 
 #define DSX_OK 0
 #define DSX_EINVAL (-1) /* bad argument (mirrors ValueError / cv2.error on bad input) */
@@ -49,6 +49,19 @@ extern "C" {
 
 #define DSX_FLOAT_FIXED 0    /* out_float = out_fixed / 16 (stereo_core.py:232 contract) */
 #define DSX_FLOAT_PARABOLA 1 /* out_float = continuous parabola vertex (north-star 1e-3 path) */
+
+/* Left-right check form (dsx_params.lr_form):
+ *   DSX_LR_FORM_BM   : the right-view winner of every right pixel is the argmin over ALL costs
+ *                      C(xr + m + d, d) (lowest d); valid band x in [m + D - 1, W - 1 + m]; the
+ *                      check runs when disp12_max_diff >= 0 (SURVEY.md 8a row A5').
+ *   DSX_LR_FORM_SGBM : cv2.StereoSGBM's own form (stereo_core.py:63-75): disp2 is built from the
+ *                      unique LEFT winners only (minimum cost; equal costs: the largest x), each
+ *                      sub-pixel disparity's floor and ceiling are tested and the pixel is dropped
+ *                      only if both have a disp2 entry and both differ by more than disp12MaxDiff
+ *                      (which is max(disp12_max_diff, 1): always on); valid band
+ *                      x in [max(m + D, 0), W + min(m, 0)).  Runs on the volume path (K1 + K2). */
+#define DSX_LR_FORM_BM 0
+#define DSX_LR_FORM_SGBM 1
 
 #define DSX_PATH_FUSED 0  /* cost computed in LDS, never written to HBM (default) */
 #define DSX_PATH_VOLUME 1 /* K1 writes the [H][W][D] cost volume to HBM, K2 reduces it */
@@ -86,7 +99,8 @@ typedef struct dsx_params {
                               /* speckle_window_size > 0; needs float_mode DSX_FLOAT_FIXED         */
     int32_t speckle_window_size; /* 'speckle_window_size' (stereo_core.py:23), >= 0              */
     int32_t speckle_range;    /* 'speckle_range'     (stereo_core.py:24), maxDiff = 16 * range   */
-    int32_t reserved[4];
+    int32_t lr_form;          /* DSX_LR_FORM_BM (default) | DSX_LR_FORM_SGBM                     */
+    int32_t reserved[3];
 } dsx_params;
 
 typedef struct dsx_handle dsx_handle;

@@ -69,3 +69,118 @@ def sgbm_post(fixed, min_disp: int, speckle_window_size: int, speckle_range: int
     if speckle_window_size > 0:
         out = filter_speckles_flood(out, (min_disp - 1) * 16, speckle_window_size, 16 * speckle_range)
     return out
+
+
+# ------------------------------------------------------------------------------------------------
+# cv2.StereoSGBM's own decision step (VERDICT r2 missing item 4): the left-right check builds disp2
+# from the LEFT winners and tests the floor and the ceiling of each sub-pixel disparity; the valid
+# band is [max(minD + numDisparities, 0), width + min(minD, 0)).  Restated from OpenCV 4.x's
+# computeDisparitySGBM (third-party source, opencv-python==4.12.0.88, requirements.txt:7, absent
+# here - **parity against OpenCV unpinned**):
+#   disp12MaxDiff = params.disp12MaxDiff > 0 ? params.disp12MaxDiff : 1   (the check is always on)
+#   uniquenessRatio = params.uniquenessRatio >= 0 ? params.uniquenessRatio : 10
+#   for x = width1 - 1 .. 0 (descending):                     X = x + minX1
+#       minS, bestDisp = lowest-d minimum of S[X, :]
+#       skip X unless unique (no d with |d - bestDisp| > 1 and S[d] (100 - u) < minS 100)
+#       X2 = X - bestDisp - minD;  if disp2cost[X2] > minS: disp2cost[X2] = minS, disp2[X2] = bestDisp + minD
+#       disp1[X] = 16 (bestDisp + minD) + parabola correction (C integer division)
+#   for X in [minX1, maxX1): d1 = disp1[X]; skip invalid; _d = d1 >> 4, d_ = (d1 + 15) >> 4;
+#       invalid if BOTH X - _d and X - d_ are in [0, width) with disp2 >= minD there and
+#       |disp2[X - _d] - _d| > disp12MaxDiff and |disp2[X - d_] - d_| > disp12MaxDiff
+# ------------------------------------------------------------------------------------------------
+def wta_sgbm(C, min_disp: int, uniqueness_ratio: int = 10, disp12_max_diff: int = 1, subpixel: bool = True):
+    """Vectorised form on an int64 volume C[y, x, d]; returns dict(fixed=int16, disp2=int32)."""
+    C = np.asarray(C, np.int64)
+    H, W, D = C.shape
+    m = min_disp
+    inv = (m - 1) * 16
+    u = uniqueness_ratio if uniqueness_ratio >= 0 else 10
+    d12 = disp12_max_diff if disp12_max_diff > 0 else 1
+    x = np.arange(W)[None, :].repeat(H, 0)
+    band = (x >= max(m + D, 0)) & (x < W + min(m, 0))
+    b = np.argmin(C, axis=2)
+    cb = np.take_along_axis(C, b[..., None], 2)[..., 0]
+    dd = np.arange(D)[None, None, :]
+    unique = ~((np.abs(dd - b[..., None]) > 1) & (C * (100 - u) < (cb * 100)[..., None])).any(axis=2)
+    ok = band & unique
+    fixed = b * 16
+    if subpixel:
+        inner = (b > 0) & (b < D - 1)
+        Cm = np.take_along_axis(C, np.clip(b - 1, 0, D - 1)[..., None], 2)[..., 0]
+        Cp = np.take_along_axis(C, np.clip(b + 1, 0, D - 1)[..., None], 2)[..., 0]
+        den = np.maximum(Cm + Cp - 2 * cb, 1)
+        num = (Cm - Cp) * 16 + den
+        q = np.abs(num) // (2 * den)
+        fixed = np.where(inner, fixed + np.where(num < 0, -q, q), fixed)
+    disp1 = np.where(ok, m * 16 + fixed, inv)
+    # disp2: per right pixel the minimum cost over the unique left winners mapping to it; equal costs
+    # keep the first one of the descending x loop (the largest x, i.e. the largest d)
+    disp2 = np.full((H, W), m - 1, np.int64)
+    key = cb * (2 * D) + (2 * D - 1 - b)  # min key: min cost, then max d
+    for y in range(H):
+        xs = np.nonzero(ok[y])[0]
+        if xs.size == 0:
+            continue
+        xr = xs - m - b[y, xs]
+        best = np.full(W, np.iinfo(np.int64).max, np.int64)
+        np.minimum.at(best, xr, key[y, xs])
+        hit = best != np.iinfo(np.int64).max
+        disp2[y, hit] = m + (2 * D - 1 - best[hit] % (2 * D))
+    lo = disp1 >> 4
+    hi = (disp1 + 15) >> 4
+    xl, xh = x - lo, x - hi
+    rows = np.arange(H)[:, None].repeat(W, 1)
+
+    def bad(xq, dq):
+        inside = (xq >= 0) & (xq < W)
+        d2 = disp2[rows, np.clip(xq, 0, W - 1)]
+        return inside & (d2 >= m) & (np.abs(d2 - dq) > d12)
+
+    fails = (disp1 != inv) & band & bad(xl, lo) & bad(xh, hi)
+    out = np.where(fails, inv, disp1).astype(np.int16)
+    return {"fixed": out, "disp2": disp2.astype(np.int32)}
+
+
+def wta_sgbm_loop(C, min_disp: int, uniqueness_ratio: int = 10, disp12_max_diff: int = 1, subpixel: bool = True):
+    """The same decision step as plain loops in OpenCV's order (tiny volumes; pins ``wta_sgbm``)."""
+    C = np.asarray(C, np.int64)
+    H, W, D = C.shape
+    minD = min_disp
+    maxD = minD + D
+    INV = (minD - 1) * 16
+    u = uniqueness_ratio if uniqueness_ratio >= 0 else 10
+    d12 = disp12_max_diff if disp12_max_diff > 0 else 1
+    minX1, maxX1 = max(maxD, 0), W + min(minD, 0)
+    out = np.full((H, W), INV, np.int64)
+    for y in range(H):
+        disp2cost = [1 << 62] * W
+        disp2 = [minD - 1] * W
+        for X in range(maxX1 - 1, minX1 - 1, -1):
+            S = [int(v) for v in C[y, X]]
+            minS, best = 1 << 62, -1
+            for d in range(D):
+                if S[d] < minS:
+                    minS, best = S[d], d
+            if any(S[d] * (100 - u) < minS * 100 and abs(best - d) > 1 for d in range(D)):
+                continue
+            x2 = X - best - minD
+            if disp2cost[x2] > minS:
+                disp2cost[x2] = minS
+                disp2[x2] = best + minD
+            d = best * 16
+            if subpixel and 0 < best < D - 1:
+                den = max(S[best - 1] + S[best + 1] - 2 * S[best], 1)
+                num = (S[best - 1] - S[best + 1]) * 16 + den
+                q = abs(num) // (2 * den)
+                d += -q if num < 0 else q
+            out[y, X] = d + minD * 16
+        for X in range(minX1, maxX1):
+            d1 = int(out[y, X])
+            if d1 == INV:
+                continue
+            lo, hi = d1 >> 4, (d1 + 15) >> 4
+            xl, xh = X - lo, X - hi
+            if 0 <= xl < W and disp2[xl] >= minD and abs(disp2[xl] - lo) > d12 and \
+                    0 <= xh < W and disp2[xh] >= minD and abs(disp2[xh] - hi) > d12:
+                out[y, X] = INV
+    return out.astype(np.int16)

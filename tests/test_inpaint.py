@@ -48,15 +48,19 @@ def _loop_inpaint(img, hole, radius):
             gx = (tr - tl) * 0.5 if (orr and ol) else (tr - tp if orr else (tp - tl if ol else 0.0))
             gy = (td - tu) * 0.5 if (od and ou) else (td - tp if od else (tp - tu if ou else 0.0))
             num = den = 0.0
-            for oy, ox in offs:
-                qy, qx = y + oy, x + ox
-                if not (0 <= qy < H and 0 <= qx < W) or layer[qy][qx] >= k:
-                    continue
-                ry, rx = -oy, -ox
-                d2 = ry * ry + rx * rx
-                w = max(abs(ry * gy + rx * gx) / math.sqrt(d2) * (1.0 / d2) * (1.0 / (1.0 + abs(T[qy][qx] - tp))), 1e-6)
-                num += w * out[qy][qx]
-                den += w
+            for oyr in range(-radius, radius + 1):  # window rows, each summed from 0.0
+                rn = rd = 0.0
+                for oy, ox in offs:
+                    qy, qx = y + oy, x + ox
+                    if oy != oyr or not (0 <= qy < H and 0 <= qx < W) or layer[qy][qx] >= k:
+                        continue
+                    ry, rx = -oy, -ox
+                    d2 = ry * ry + rx * rx
+                    w = max(abs(ry * gy + rx * gx) / math.sqrt(d2) * (1.0 / d2) * (1.0 / (1.0 + abs(T[qy][qx] - tp))), 1e-6)
+                    rn += w * out[qy][qx]
+                    rd += w
+                num += rn
+                den += rd
             new.append((y, x, tp, float(np.float32(num / den)) if den > 0 else out[y][x]))
         for y, x, tp, v in new:
             T[y][x], out[y][x], layer[y][x] = tp, v, k

@@ -15,7 +15,7 @@ import pytest
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 FIELDS = ("min_disp", "num_disp", "block_size", "cost", "uniqueness_ratio", "disp12_max_diff", "subpixel",
           "float_mode", "path", "timing", "grid_blocks", "aggregation", "p1", "p2", "prefilter_cap", "sgbm_post",
-          "speckle_window_size", "speckle_range", "reserved")
+          "speckle_window_size", "speckle_range", "lr_form", "reserved")
 
 
 @pytest.fixture(scope="module")

@@ -1,0 +1,130 @@
+"""cv2.StereoSGBM's own left-right check and valid band ('lr_form': 'sgbm', DSX_LR_FORM_SGBM; VERDICT
+r2 missing item 4; the reference's matcher, depthlib/stereo_core.py:63-75, disp12MaxDiff at :69).
+
+OpenCV builds disp2 from the unique LEFT winners, tests the floor and the ceiling of each
+sub-pixel disparity, forces disp12MaxDiff >= 1 and keeps [max(minD + numDisparities, 0),
+width + min(minD, 0)) as the valid band.  OpenCV is absent, so parity against it is unpinned: the
+vectorised restatement (oracle/sgbm_post.wta_sgbm) is pinned by a loop restatement in OpenCV's own
+order (wta_sgbm_loop), and the GPU (vol_wta's LRM = 2 form) is checked bit for bit against it on
+every cost the volume path runs: SAD, SSD, BT, SGM path sums, and with the sgbm_post tail."""
+from __future__ import annotations
+
+import numpy as np
+import pytest
+
+from depthestimation_amd import _dsx
+from depthestimation_amd.synthetic import stereo_pair
+from oracle.bt_cost import cost_volume_bt
+from oracle.sgbm_post import sgbm_post, wta_sgbm, wta_sgbm_loop
+from oracle.sgm import aggregate
+from oracle.stereo_bm import cost_volume
+
+
+@pytest.mark.parametrize("seed", range(12))
+def test_vectorised_matches_loop_restatement(seed):
+    rng = np.random.default_rng(seed)
+    H, W, D = int(rng.integers(1, 5)), int(rng.integers(1, 40)), int(rng.integers(2, 12))
+    m = int(rng.integers(-4, 5))
+    C = rng.integers(0, 50, (H, W, D))
+    if seed % 3 == 0:
+        C //= 9  # many equal costs: the tie rules of disp2 and of the WTA
+    for u in (0, 10):
+        for d12 in (-1, 0, 1, 3):
+            for sp in (True, False):
+                np.testing.assert_array_equal(wta_sgbm(C, m, u, d12, sp)["fixed"], wta_sgbm_loop(C, m, u, d12, sp))
+
+
+def test_known_answers():
+    # one row, D = 4: x = 4 is the first valid column (band starts at m + D, not m + D - 1)
+    C = np.full((1, 8, 4), 50, np.int64)
+    C[0, :, 2] = 0
+    out = wta_sgbm(C, 0, 0, 1, False)["fixed"][0]
+    assert (out[:4] == -16).all() and (out[4:] == 32).all()
+    # disp2 ties: right pixel 2 receives (cost 0, d 2) from x = 4 and (cost 0, d 3) from x = 5 ->
+    # the larger x (d 3) is kept, as OpenCV's descending loop with a strict '>' keeps the first one
+    C = np.full((1, 8, 4), 50, np.int64)
+    C[0, 4, 2] = 0
+    C[0, 5, 3] = 0
+    r = wta_sgbm(C, 0, 0, 1, False)
+    assert r["disp2"][0, 2] == 3
+    # disp12MaxDiff <= 0 means 1 (the check is always on)
+    assert (wta_sgbm(C, 0, 0, -1, False)["fixed"] == wta_sgbm(C, 0, 0, 1, False)["fixed"]).all()
+
+
+def test_params():
+    p = _dsx.make_params(lr_form="sgbm")
+    _dsx.check_params(p)
+    assert p.lr_form == 1 and _dsx.default_params().lr_form == 0
+    with pytest.raises(ValueError):
+        _dsx.make_params(lr_form="opencv")
+    bad = _dsx.make_params()
+    bad.lr_form = 7
+    with pytest.raises(ValueError):
+        _dsx.check_params(bad)
+    from depthestimation_amd.stereo_core import StereoCore
+    core = StereoCore()
+    assert core.get_sgbm_params()["lr_form"] == "bm"
+    core.configure_sgbm(lr_form="sgbm")
+    assert core.sgbm.params["lr_form"] == "sgbm"
+    with pytest.raises(ValueError):
+        core.configure_sgbm(lr_form="x")
+
+
+# ---------------------------------------------------------------- GPU -------------------
+def _gpu():
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+
+
+CASES = [  # cost, aggregation, H, W, m, D, bs, uniqueness, disp12MaxDiff
+    ("sad", None, 40, 150, 0, 64, 5, 10, 1),
+    ("sad", None, 23, 97, 3, 48, 3, 0, 2),
+    ("ssd", None, 30, 120, -2, 32, 7, 10, 0),
+    ("sad", None, 17, 300, 0, 160, 9, 5, -1),   # Dp 256
+    ("bt", None, 33, 140, 0, 48, 5, 10, 1),
+    ("bt", "sgbm_3way", 33, 140, 0, 48, 5, 10, 1),
+    ("sad", "hh", 25, 100, 1, 32, 5, 10, 1),
+    ("sad", None, 9, 40, 0, 64, 5, 10, 1),      # D > W: no valid column
+]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", CASES, ids=lambda c: f"{c[0]}_{c[1]}_{c[2]}x{c[3]}_m{c[4]}_D{c[5]}")
+def test_gpu_sgbm_lr_form_matches_oracle(case):
+    _gpu()
+    from depthestimation_amd.matcher import HipBlockMatcher
+    cost, agg, H, W, m, D, bs, u, d12 = case
+    L, R, _ = stereo_pair(H, W, m, D, seed=H * 31 + W)
+    if cost == "bt":
+        C = cost_volume_bt(L, R, m, D, bs, 31)
+    else:
+        C = cost_volume(L, R, m, D, bs, cost)
+    p1, p2 = 8 * bs * bs, 32 * bs * bs
+    if agg:
+        C = aggregate(C, agg, p1, p2)
+    want = wta_sgbm(C, m, u, d12, True)["fixed"]
+    for path in ("fused", "volume"):  # the fused request runs on the volume path in this form
+        mm = HipBlockMatcher(min_disp=m, num_disp=D, block_size=bs, cost=cost, uniqueness_ratio=u,
+                             disp12_max_diff=d12, aggregation=agg, p1=p1, p2=p2, lr_form="sgbm", path=path)
+        flt = np.empty((H, W), np.float32)
+        got = mm.compute(L, R, out_float=flt)
+        mm.close()
+        np.testing.assert_array_equal(got, want)
+        np.testing.assert_array_equal(flt, want.astype(np.float32) / 16)
+
+
+@pytest.mark.gpu
+def test_gpu_sgbm_shaped_matcher_with_tail():
+    """BT + sgbm_3way + OpenCV's LR form + OpenCV's median/speckle tail: this build's closest form of
+    cv2.StereoSGBM as the reference configures it (stereo_core.py:63-75), through StereoCore."""
+    _gpu()
+    from depthestimation_amd.stereo_core import StereoCore
+    L, R, _ = stereo_pair(96, 320, 0, 64, seed=9)
+    core = StereoCore()
+    core.configure_sgbm(num_disp=64, block_size=5, cost="bt", aggregation="sgm", sgbm_mode="sgbm_3way",
+                        lr_form="sgbm", sgbm_post=True)
+    got = core.compute_disparity(L, R)
+    C = aggregate(cost_volume_bt(L, R, 0, 64, 5, 31), "sgbm_3way", 200, 800)
+    want = sgbm_post(wta_sgbm(C, 0, 10, 1, True)["fixed"], 0, 50, 2)
+    np.testing.assert_array_equal(got, want.astype(np.float32) / 16.0)
