@@ -747,6 +747,8 @@ int dsx_postprocess_full_ex_device(const void *d_disp, int32_t H, int32_t W, int
     if (!d_workspace || workspace_bytes < dsx::post_full_workspace(H, W, crop))
         return fail(DSX_EINVAL, "workspace too small (dsx_postprocess_workspace_bytes)");
     if ((int64_t)H * (W - crop) > 0x7FFFFFFF) return fail(DSX_EINVAL, "image too large for int32 labels");
+    if (fill_radius > 0 && W - crop > dsx::kInpaintMaxW)
+        return fail(DSX_EINVAL, "image too wide for hole filling (W > 19200)");
     dsx::PostFullArgs a{};
     a.disp = static_cast<const float *>(d_disp);
     a.in_pitch = in_pitch;
@@ -782,6 +784,7 @@ int dsx_fill_holes_device(const void *d_disp, int32_t H, int32_t W, int64_t in_p
     if (H <= 0 || W <= 0 || in_pitch < W) return fail(DSX_EINVAL, "bad shape / pitch");
     if (radius < 0) return fail(DSX_EINVAL, "radius must be >= 0");
     if ((int64_t)H * W > 0x7FFFFFFF) return fail(DSX_EINVAL, "image too large");
+    if (W > dsx::kInpaintMaxW) return fail(DSX_EINVAL, "image too wide for hole filling (W > 19200)");
     if (!d_workspace || workspace_bytes < dsx::inpaint_workspace(H, W))
         return fail(DSX_EINVAL, "workspace too small (dsx_fill_holes_workspace_bytes)");
     DSX_HIP(dsx::launch_inpaint(static_cast<const float *>(d_disp), in_pitch, H, W, radius, static_cast<float *>(d_out),

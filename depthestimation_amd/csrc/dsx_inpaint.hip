@@ -17,9 +17,9 @@
 // pixels are all holes, else one of them would be nearer).  So the layers come from a separable L1
 // distance transform (row scans, then column scans), the hole pixels are bucketed by layer with a
 // counting sort, and the march visits list k at step k.  Nothing is read back to the host:
-//   inp_rows     copy, T init, distance to the nearest known pixel of the row (block scans)
-//   inp_cols     column pass of the L1 transform (segment summaries + scans) -> layer map
-//   inp_hist     per-layer counts and the deepest layer K (LDS histograms)
+//   inp_rows     copy, distance to the nearest known pixel of the row (block scans)
+//   inp_cols     column pass of the L1 transform (segment summaries + scans) -> layer map, with the
+//                per-layer counts and the deepest layer K (LDS histograms)
 //   inp_scan     per-layer list offsets
 //   inp_scatter  hole pixels into their layer's list
 //   inp_layer    one launch per layer k = 1..L0, enqueued without waiting; a launch past K exits
@@ -43,8 +43,8 @@ constexpr int kFar = 1 << 28;             // "no known pixel" in the distance tr
 constexpr int kUnreached = 0x7FFFFFFF;    // layer of a hole no known pixel reaches
 constexpr int kCtlK = 0, kCtlBar = 1, kCtlTmo = 2;
 constexpr int kCtlWords = 64;
-constexpr int kHistBins = 2048;           // LDS histogram bins of inp_hist / inp_scatter
-constexpr int kChunk = 4096;              // pixels per block of inp_hist / inp_scatter
+constexpr int kHistBins = 2048;           // LDS histogram bins of inp_cols / inp_scatter
+constexpr int kChunk = 4096;              // pixels per block of inp_scatter
 
 __device__ __forceinline__ double telea_solve(double t1, double t2) {
     if (t1 < 1e6 && t2 < 1e6) {
@@ -79,48 +79,56 @@ __device__ __forceinline__ int block_scan(int v, int *buf) {
     return v;
 }
 
-// One block per row: out = in, T = 1e6 on holes (else 0), g = distance to the nearest known pixel
-// of the row (kFar if none).  Block 0..: also zeroes the per-layer counters and the control words.
-__global__ __launch_bounds__(256) void inp_rows(const float *in, int64_t pitch, int H, int W, float *out, double *T,
-                                                int *g, int *cnt, int ncnt, int *ctl) {
+// One block per row: out = in, g = distance to the nearest known pixel of the row (kFar if none).
+// The row is staged in LDS with coalesced loads, each thread scans a contiguous chunk of it, and two
+// block scans carry the last / first known pixel across chunks.  T is not initialised: it is only
+// read at pixels of earlier layers, i.e. known pixels (T = 0, substituted by layer) or pixels the
+// march has filled.  Block 0..: also zeroes the per-layer counters and the control words.
+__global__ __launch_bounds__(256) void inp_rows(const float *in, int64_t pitch, int H, int W, float *out, int *g,
+                                                int *cnt, int ncnt, int *ctl) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t rsm[];
+    float *sv = reinterpret_cast<float *>(rsm);
+    int *sg = reinterpret_cast<int *>(rsm + (size_t)W * 4);
     __shared__ int buf[256];
     const int y = blockIdx.x, t = threadIdx.x;
     for (int i = y * 256 + t; i < ncnt; i += H * 256) cnt[i] = 0;
     if (y == 0 && t < kCtlWords) ctl[t] = 0;
     const float *row = in + (int64_t)y * pitch;
+    float *orow = out + (int64_t)y * W;
+    for (int x = t; x < W; x += 256) {
+        const float v = row[x];
+        sv[x] = v;
+        orow[x] = v;
+    }
+    __syncthreads();
     const int chunk = (W + 255) / 256;
     const int x0 = min(W, t * chunk), x1 = min(W, x0 + chunk);
     int last = -kFar, first = kFar;
     for (int x = x0; x < x1; ++x) {
-        const float v = row[x];
-        const bool hole = v <= 0.0f;  // fill_holes' mask = disparity <= 0 (postprocess.py:96-97)
-        out[(int64_t)y * W + x] = v;
-        T[(int64_t)y * W + x] = hole ? 1e6 : 0.0;
-        if (!hole) {
+        if (sv[x] > 0.0f) {  // fill_holes' mask = disparity <= 0 (postprocess.py:96-97)
             first = first == kFar ? x : first;
             last = x;
         }
     }
     // last known left of this chunk, first known right of it
-    const int incl_last = block_scan<true>(last, buf);
+    block_scan<true>(last, buf);
     const int prev_last = t > 0 ? buf[t - 1] : -kFar;
-    (void)incl_last;
     __syncthreads();
     block_scan<false>(first, buf);
     const int next_first = t < 255 ? buf[t + 1] : kFar;
     int p = prev_last;
     for (int x = x0; x < x1; ++x) {
-        if (row[x] > 0.0f) p = x;
-        g[(int64_t)y * W + x] = p == -kFar ? kFar : x - p;
+        if (sv[x] > 0.0f) p = x;
+        sg[x] = p == -kFar ? kFar : x - p;
     }
     int q = next_first;
     for (int x = x1 - 1; x >= x0; --x) {
-        if (row[x] > 0.0f) q = x;
-        if (q != kFar) {
-            const int64_t o = (int64_t)y * W + x;
-            g[o] = min(g[o], q - x);
-        }
+        if (sv[x] > 0.0f) q = x;
+        if (q != kFar) sg[x] = min(sg[x], q - x);
     }
+    __syncthreads();
+    int *grow = g + (int64_t)y * W;
+    for (int x = t; x < W; x += 256) grow[x] = sg[x];
 }
 
 // Column pass: layer = min over y' of g(x, y') + |y - y'| (exact L1 distance), 0 on known pixels,
@@ -128,8 +136,12 @@ __global__ __launch_bounds__(256) void inp_rows(const float *in, int64_t pitch, 
 // summarises its segment for both directions, takes the other segments' summaries from LDS, then
 // scans its segment forwards (into `layer`) and backwards (combining).
 constexpr int kColW = 16, kColS = 64;
-__global__ __launch_bounds__(1024) void inp_cols(const int *g, int H, int W, int *layer) {
+__global__ __launch_bounds__(1024) void inp_cols(const int *g, int H, int W, int *layer, int *cnt, int *ctl) {
     __shared__ int sf[kColS][kColW], sb[kColS][kColW];
+    __shared__ int hist[kHistBins];
+    __shared__ int kmax;
+    for (int i = threadIdx.x; i < kHistBins; i += 1024) hist[i] = 0;
+    if (threadIdx.x == 0) kmax = 0;
     const int cx = threadIdx.x % kColW, sj = threadIdx.x / kColW;
     const int x = blockIdx.x * kColW + cx;
     const int SL = (H + kColS - 1) / kColS;
@@ -145,7 +157,8 @@ __global__ __launch_bounds__(1024) void inp_cols(const int *g, int H, int W, int
     sf[sj][cx] = cf;
     sb[sj][cx] = cb;
     __syncthreads();
-    if (!live || y0 >= y1) return;
+    int km = 0;
+    if (live && y0 < y1) {
     int hf = kFar, hb = kFar;  // distance from rows above y0 (at row y0 - 1) / below y1 - 1 (at row y1)
     for (int j = 0; j < sj; ++j) {
         const int ye = min(H, (j + 1) * SL);  // segment j ends at row ye - 1
@@ -164,30 +177,18 @@ __global__ __launch_bounds__(1024) void inp_cols(const int *g, int H, int W, int
         hb = min(g[o], hb + 1);
         const int d = min(layer[o], hb);
         layer[o] = d >= kFar ? kUnreached : d;  // known pixels: g = 0
-    }
-}
-
-// Per-layer hole counts (cnt[k], k >= 1) and the deepest reached layer ctl[kCtlK].
-__global__ __launch_bounds__(256) void inp_hist(const int *layer, int n, int *cnt, int *ctl) {
-    __shared__ int h[kHistBins];
-    __shared__ int kmax;
-    for (int i = threadIdx.x; i < kHistBins; i += 256) h[i] = 0;
-    if (threadIdx.x == 0) kmax = 0;
-    __syncthreads();
-    const int p0 = blockIdx.x * kChunk;
-    int km = 0;
-    for (int p = p0 + (int)threadIdx.x; p < min(n, p0 + kChunk); p += 256) {
-        const int k = layer[p];
-        if (k > 0 && k != kUnreached) {
-            km = k > km ? k : km;
-            if (k < kHistBins) atomicAdd(&h[k], 1);
-            else atomicAdd(&cnt[k], 1);
+        // per-layer hole counts (cnt[k], k >= 1) and the deepest reached layer ctl[kCtlK]
+        if (d > 0 && d < kFar) {
+            km = d > km ? d : km;
+            if (d < kHistBins) atomicAdd(&hist[d], 1);
+            else atomicAdd(&cnt[d], 1);
         }
+    }
     }
     atomicMax(&kmax, km);
     __syncthreads();
-    for (int i = threadIdx.x; i < kHistBins; i += 256)
-        if (h[i]) atomicAdd(&cnt[i], h[i]);
+    for (int i = threadIdx.x; i < kHistBins; i += 1024)
+        if (hist[i]) atomicAdd(&cnt[i], hist[i]);
     if (threadIdx.x == 0 && kmax) atomicMax(&ctl[kCtlK], kmax);
 }
 
@@ -266,7 +267,9 @@ __device__ __forceinline__ Front front_of(const int *layer, const double *T, int
     const double Tu = iu ? T[p - W] : 1e6, Td = id ? T[p + W] : 1e6;
     const double Tl = il ? T[p - 1] : 1e6, Tr = ir ? T[p + 1] : 1e6;
     const bool ou = lu < k, od = ld < k, ol = ll < k, orr = lr < k;
-    const double tu = ou ? Tu : 1e6, td = od ? Td : 1e6, tl = ol ? Tl : 1e6, tr = orr ? Tr : 1e6;
+    // T is never initialised: known pixels (layer 0) have T = 0, holes of earlier layers their march value
+    const double tu = ou ? (lu == 0 ? 0.0 : Tu) : 1e6, td = od ? (ld == 0 ? 0.0 : Td) : 1e6;
+    const double tl = ol ? (ll == 0 ? 0.0 : Tl) : 1e6, tr = orr ? (lr == 0 ? 0.0 : Tr) : 1e6;
     const double a0 = telea_solve(tu, tl), a1 = telea_solve(td, tl);
     const double a2 = telea_solve(tu, tr), a3 = telea_solve(td, tr);
     const double m01 = a0 < a1 ? a0 : a1, m23 = a2 < a3 ? a2 : a3;
@@ -285,7 +288,7 @@ __device__ __forceinline__ bool cell_term(const float *out, const int *layer, co
     if (d2 == 0 || d2 > r2 || qy < 0 || qy >= H || qx < 0 || qx >= W) return false;
     const int64_t q = (int64_t)qy * W + qx;
     const int lq = layer[q];
-    const double tq = T[q];
+    const double tq = lq == 0 ? 0.0 : T[q];  // known pixels: T = 0 (not stored)
     const float vq = out[q];
     if (lq >= k) return false;
     const double ry = (double)(-oy), rx = (double)(-ox);
@@ -376,8 +379,8 @@ __device__ __forceinline__ void march_layer(float *out, const int *layer, double
 template <int G>
 __global__ __launch_bounds__(256) void inp_layer(float *out, const int *layer, double *T, int H, int W, int radius,
                                                  int k, const int *list, const int *off, const int *ctl) {
-    if (k > ctl[kCtlK]) return;
-    const int beg = off[k], end = off[k + 1];
+    const int K = ctl[kCtlK], beg = off[k], end = off[k + 1];  // independent loads, one round trip
+    if (k > K) return;
     march_layer<G>(out, layer, T, H, W, radius, k, list, beg, end, blockIdx.x, gridDim.x);
 }
 
@@ -481,14 +484,24 @@ hipError_t launch_inpaint(const float *in, int64_t pitch, int H, int W, int radi
     const int n = H * W;  // < 2^31 (host check)
     const Views v = views(ws, H, W);
     hipError_t e;
-    hipLaunchKernelGGL(inp_rows, dim3(H), dim3(256), 0, st, in, pitch, H, W, out, v.T, v.g, v.cnt, v.ncnt, v.ctl);
+    if (W > kInpaintMaxW) return hipErrorInvalidValue;  // the row kernel stages a row in LDS
+    static bool attr[64] = {};
+    {
+        int dev = 0;
+        if ((e = hipGetDevice(&dev)) != hipSuccess) return e;
+        if (dev >= 0 && dev < 64 && !attr[dev]) {
+            if ((e = hipFuncSetAttribute((const void *)inp_rows, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                         150 * 1024)) != hipSuccess)
+                return e;
+            attr[dev] = true;
+        }
+    }
+    hipLaunchKernelGGL(inp_rows, dim3(H), dim3(256), (size_t)W * 8, st, in, pitch, H, W, out, v.g, v.cnt, v.ncnt, v.ctl);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     if (radius < 1) return hipSuccess;  // no neighbourhood: nothing changes (cv2 uses radius >= 1)
-    hipLaunchKernelGGL(inp_cols, dim3((W + kColW - 1) / kColW), dim3(1024), 0, st, v.g, H, W, v.layer);
+    hipLaunchKernelGGL(inp_cols, dim3((W + kColW - 1) / kColW), dim3(1024), 0, st, v.g, H, W, v.layer, v.cnt, v.ctl);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     const int nch = (n + kChunk - 1) / kChunk;
-    hipLaunchKernelGGL(inp_hist, dim3(nch), dim3(256), 0, st, v.layer, n, v.cnt, v.ctl);
-    if ((e = hipGetLastError()) != hipSuccess) return e;
     int *hk = lastk_host();
     int *hk_dev = nullptr;
     if (hk && hipHostGetDevicePointer(reinterpret_cast<void **>(&hk_dev), hk, 0) != hipSuccess) hk_dev = nullptr;
@@ -497,11 +510,11 @@ hipError_t launch_inpaint(const float *in, int64_t pitch, int H, int W, int radi
     hipLaunchKernelGGL(inp_scatter, dim3(nch), dim3(256), 0, st, v.layer, n, v.cnt, v.list);
     if ((e = hipGetLastError()) != hipSuccess) return e;
 
-    // per-layer launches, enqueued without waiting: as many as the previous call needed (+4), at
+    // per-layer launches, enqueued without waiting: as many as the previous call needed (+1), at
     // least 8; the persistent kernel takes whatever is left
     const int maxk = H + W;
     const int prev = hk ? __atomic_load_n(hk, __ATOMIC_RELAXED) : -1;
-    int L0 = std::min(maxk, prev < 0 ? 64 : std::max(8, prev + 4));
+    int L0 = std::min(maxk, prev < 0 ? 64 : std::max(8, prev + 1));
     if (const char *fl = getenv("DSX_INPAINT_L0")) L0 = std::min(maxk, std::max(0, atoi(fl)));  // tests: force the split
     // lanes per pixel: one per window row (8 up to radius 3, 16 up to 7); larger windows one pixel
     // per thread.  512 blocks: an empty launch (a layer past K) costs ~1.5 us where 2048 cost ~4.6 us

@@ -165,6 +165,7 @@ hipError_t launch_post_full(PostFullArgs a, void *ws, hipStream_t st);
 // Hole filling (dsx_inpaint.hip): fill_holes(method='inpaint') on d <= 0, layered Telea marching.
 // Asynchronous: nothing is read back to the host.
 size_t inpaint_workspace(int H, int W);
+constexpr int kInpaintMaxW = 19200;  // the row pass stages a row (8 B / px) in LDS
 hipError_t launch_inpaint(const float *in, int64_t pitch, int H, int W, int radius, float *out, void *ws, hipStream_t st);
 
 // Birchfield-Tomasi block costs into K1's volume layout (dsx_bt.hip, oracle/bt_cost.py)
