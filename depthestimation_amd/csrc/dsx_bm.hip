@@ -41,6 +41,9 @@
 #ifndef DSX_WPE
 #define DSX_WPE 3
 #endif
+#ifndef DSX_XB4  // SAD LR pass: exits parked 4 at a time (one b128 store) in a per-wave region
+#define DSX_XB4 1
+#endif
 #ifndef DSX_EXP  // experiment bits (tools/exp_build.sh; timing only, results wrong): 1 no LR exit
 #define DSX_EXP 0  // stores, 2 no LR atomics, 4 no diagonal minima, 8 no dstar store, 16 scan argmin on LR
 #endif
@@ -646,7 +649,13 @@ __device__ __forceinline__ void bm2_segment(const Bm2Args &a, uint8_t *smem, int
                 const uint32_t dmE = d0 < D ? (uint32_t)d0 : 0xFFFFFFFFu;
                 const bool lane0 = ln == 0;
                 const bool top = ln == 63;
-                uint8_t *xq = tile + Dp * CB + 4 * wv;  // SAD: this wave's exit slot in each tile row's padding
+                // SAD exits: pixel k's at xq + k * XST - a 128-B region per wave after the block's LDS
+                // (DSX_XB4: the full-strip loop keeps 4 exits in registers and parks them with one
+                // single-lane b128 store; r03: 31 exec-masked b32 stores per row cost ~6 % at C2r),
+                // else this wave's slot in each tile row's padding
+                uint8_t *xq = DSX_XB4 ? smem + G::SMEM + 128 * wv : tile + Dp * CB + 4 * wv;
+                constexpr int XST = DSX_XB4 ? 4 : PITCH;
+                uint32_t X[4] = {0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu};
                 uint32_t Ae = 0xFFFFFFFFu, Ao = 0xFFFFFFFFu, E = 0xFFFFFFFFu;
                 // FULL: the strip lies inside the image and every lane owns real disparities
                 // (D == Dp), so the per-pixel bounds / lane checks drop out of the unrolled loop
@@ -697,7 +706,15 @@ __device__ __forceinline__ void bm2_segment(const Bm2Args &a, uint8_t *smem, int
                                     Ao = umin2(Ao, kO);
                                 }
                             }
-                            if (!(DSX_EXP & 1) && k < TX - 1 && top) *reinterpret_cast<uint32_t *>(xq + k * PITCH) = Ao;  // exit
+                            if (!(DSX_EXP & 1) && k < TX - 1) {  // exit
+                                if constexpr (DSX_XB4 && FULL) {
+                                    X[k & 3] = Ao;
+                                    if (((k & 3) == 3 || k == TX - 2) && top)
+                                        *reinterpret_cast<uint4 *>(xq + (k & ~3) * 4) = make_uint4(X[0], X[1], X[2], X[3]);
+                                } else if (top) {
+                                    *reinterpret_cast<uint32_t *>(xq + k * XST) = Ao;
+                                }
+                            }
                         }
                     }
                 };
@@ -713,7 +730,7 @@ __device__ __forceinline__ void bm2_segment(const Bm2Args &a, uint8_t *smem, int
                     const int xe = x0 + (TX - 2 - ln) - m - dtop;  // E lane j: exit of pixel TX-2-j
                     if (ln < TX - 1 && E != 0xFFFFFFFFu && xe >= 0 && xe < W) atomicMin(krow + xe, E);
                 } else if (ln < TX - 1) {
-                    E = *reinterpret_cast<const uint32_t *>(xq + ln * PITCH);  // exit of pixel ln, parked in LDS
+                    E = *reinterpret_cast<const uint32_t *>(xq + ln * XST);  // exit of pixel ln, parked in LDS
                     const int xe = x0 + ln - m - dtop;
                     if (E != 0xFFFFFFFFu && xe >= 0 && xe < W) atomicMin(krow + xe, E);
                 }
@@ -1079,6 +1096,7 @@ static hipError_t bm2_partition_dev(const PartKey &k, int TX, const int **out) {
 template <int R, bool SSD, int NW, int SIDE, bool ABS = false>
 static hipError_t launch_bm2_side(const Bm2Args &a, hipStream_t st) {
     using G = Geo<R, SSD, NW>;
+    constexpr int SM = G::SMEM + ((SIDE == 3 && !SSD && DSX_XB4) ? 128 * NW : 0);  // + the LR exit region
     const void *fn = (const void *)bm2<R, SSD, NW, SIDE, ABS>;
     static int blocks_per_cu[64] = {};
     static int num_cu[64] = {};
@@ -1090,10 +1108,10 @@ static hipError_t launch_bm2_side(const Bm2Args &a, hipStream_t st) {
     // through the launch itself (see bm2_partition_dev)
     std::lock_guard<std::mutex> lock(launch_mutex());
     if (!blocks_per_cu[dev]) {
-        e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, G::SMEM);
+        e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, SM);
         if (e != hipSuccess) return e;
         int nb = 0;
-        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, fn, G::NT, G::SMEM);
+        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, fn, G::NT, SM);
         if (e != hipSuccess) return e;
         int cus = 0;
         e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
@@ -1124,7 +1142,7 @@ static hipError_t launch_bm2_side(const Bm2Args &a, hipStream_t st) {
     if (grid < 1) grid = 1;
     if (getenv("DSX_VERBOSE"))
         fprintf(stderr, "[dsx] bm2<R=%d,SSD=%d,NW=%d,SIDE=%d> grid %ld (%d/CU) smem %d\n", R, (int)SSD, NW, SIDE, grid,
-                blocks_per_cu[dev], G::SMEM);
+                blocks_per_cu[dev], SM);
     // age levels: with one block per resident slot, block b is the (b / num_cu)-th block its CU
     // received, and co-resident waves of a SIMD differ in age (issue arbitration) by that rank
     Bm2Args la = a;
@@ -1151,7 +1169,7 @@ static hipError_t launch_bm2_side(const Bm2Args &a, hipStream_t st) {
         e = bm2_partition_dev(k, G::TX, &la.part);
         if (e != hipSuccess) return e;
     }
-    hipLaunchKernelGGL((bm2<R, SSD, NW, SIDE, ABS>), dim3((unsigned)grid), dim3(G::NT), G::SMEM, st, la);
+    hipLaunchKernelGGL((bm2<R, SSD, NW, SIDE, ABS>), dim3((unsigned)grid), dim3(G::NT), SM, st, la);
     return hipGetLastError();
 }
 
