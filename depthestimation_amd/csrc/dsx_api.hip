@@ -12,6 +12,10 @@
 #include "../../include/dsx.h"
 #include "dsx_internal.h"
 
+#ifndef DSX_RESET_LEFT  // 1: the LR pass resets the other key half; 0: lr_fixup does
+#define DSX_RESET_LEFT 1
+#endif
+
 namespace {
 
 thread_local std::string g_err;
@@ -421,6 +425,10 @@ int run(dsx_handle *h, const void *dL, const void *dR, int H, int W, int64_t str
             // diagonal starts left of the valid band); lr_fixup applies the check afterwards
             a.side = dsx::SIDE_LEFT_LR;
             a.lr_keys = h->lrKeys + (size_t)h->lrParity * H * W * h->lrFrames;
+            // the other half holds the keys of the previous call (consumed by its lr_fixup, which
+            // precedes this launch): the left pass resets them for the next call
+            a.lr_reset = h->lrKeys + (size_t)(h->lrParity ^ 1) * H * W * h->lrFrames;
+            a.lr_reset_n = DSX_RESET_LEFT ? (int64_t)H * W * h->lrDirty[h->lrParity ^ 1] : 0;
             a.dstar = h->dStar;
             a.kshift = h->g.kind != dsx::BM_SAD ? h->g.DB : 16;  // u32 layouts: (C << DB) | d
         } else {
@@ -443,12 +451,12 @@ int run(dsx_handle *h, const void *dL, const void *dR, int H, int W, int64_t str
         a.timeline = tl;
         DSX_LAUNCH(h, "bm_pass_left", st, dsx::launch_bm2(radius, h->g.kind, h->g.NW, a, st));
         if (lr) {
-            // this call dirties nframes frames of half P; lr_fixup resets every dirty frame of
-            // the other half (consumed by the previous call), however many frames that call had
+            // this call dirties nframes frames of half P; its left pass has reset every dirty frame
+            // of the other half (consumed by the previous call), however many frames that call had
             const int P = h->lrParity;
             DSX_LAUNCH(h, "lr_fixup", st,
-                       dsx::launch_lr_fixup(h->dStar, a.lr_keys, h->lrKeys + (size_t)(P ^ 1) * H * W * h->lrFrames,
-                                            H * nframes, H * h->lrDirty[P ^ 1], W, h->p.min_disp,
+                       dsx::launch_lr_fixup(h->dStar, a.lr_keys, a.lr_reset,
+                                            DSX_RESET_LEFT ? 0 : H * h->lrDirty[P ^ 1], H * nframes, W, h->p.min_disp,
                                             h->p.disp12_max_diff, a.kshift, a.out_fixed, a.out_float, st));
             h->lrDirty[P ^ 1] = 0;
             h->lrDirty[P] = nframes;

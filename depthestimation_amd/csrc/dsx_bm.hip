@@ -978,6 +978,20 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu((SSD &&
         }
     }
 
+    // ---- LR pass: reset the other key half (the previous call's keys, already checked) ----
+    if (side == 3 && a.lr_reset_n > 0) {
+        uint32_t *kr = a.lr_reset;
+        const int64_t n = a.lr_reset_n, stride = (int64_t)gridDim.x * NT;
+        const int64_t t0 = (int64_t)blockIdx.x * NT + tid;
+        if (((uintptr_t)kr & 15u) == 0) {
+            for (int64_t q = t0; q < n / 4; q += stride)
+                reinterpret_cast<uint4 *>(kr)[q] = make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu);
+            for (int64_t q = n / 4 * 4 + t0; q < n; q += stride) kr[q] = 0xFFFFFFFFu;
+        } else {
+            for (int64_t q = t0; q < n; q += stride) kr[q] = 0xFFFFFFFFu;
+        }
+    }
+
     // ---- work partition (host-computed, bm2_partition): block b owns linear (frame, strip, row)
     // units [part[b], part[b+1]); nframes * H * W < 2^31 (host check)
     const int lin0 = a.part[blockIdx.x], lin1 = a.part[blockIdx.x + 1];

@@ -43,6 +43,8 @@ struct Bm2Args {
     uint32_t *lr_keys;     // left pass with LR: per-pixel right-view winner keys (C << kshift | d),
     int kshift;            //   filled by atomicMin (memset to ~0 first)
     int16_t *dstar;        // left pass with LR: winning d (or -1) for lr_fixup
+    uint32_t *lr_reset;    // left pass with LR: the other key half, reset to ~0 here for the next call
+    int64_t lr_reset_n;    //   (keys the previous call's lr_fixup consumed)
     int16_t *out_fixed;    // left pass outputs (either may be null)
     float *out_float;
     int16_t *out_dR;       // right pass output
@@ -85,9 +87,9 @@ enum { BM_SAD = 0, BM_SSD = 1, BM_SAD1 = 2 };
 hipError_t launch_bm2(int radius, int kind, int nw, const Bm2Args &a, hipStream_t st);
 hipError_t launch_volume_wta(int TX, bool ssd, const VolArgs &a, hipStream_t st);
 // LR check after the left pass: invalidate x where |dR(x - m - d*) - d*| > lr over `rows` rows
-// (frames stacked), reading this call's key buffer and resetting the first `reset_rows` rows of
-// the other one (double-buffered keys, see dsx_api.hip).
-hipError_t launch_lr_fixup(const int16_t *dstar, const uint32_t *keys, uint32_t *keys_next, int rows, int reset_rows,
+// (frames stacked), reading this call's key buffer (double-buffered keys, see dsx_api.hip; the left
+// pass resets the other half).
+hipError_t launch_lr_fixup(const int16_t *dstar, const uint32_t *keys, uint32_t *keys_next, int reset_rows, int rows,
                            int W, int m, int lr, int kshift, int16_t *out_fixed, float *out_float, hipStream_t st);
 
 size_t volume_smem_bytes(int TX, bool ssd, int Dp, int TPP, int W);

@@ -35,7 +35,10 @@ __device__ __forceinline__ uint32_t group_min(uint32_t v, int tpp) {
 }
 
 constexpr int kVolScratch = kVolThreads + kVolThreads / 8;  // padded scratch slots per vector
-__host__ __device__ constexpr int kvpad(int W) { return W + (W >> 4) + 1; }  // padded LR key row (ridx)
+// LR key row: every right pixel a cost can name, xr = x - m - d in [-m - Dp + 1, W - 1 - m], at
+// xr + m + Dp - 1 (linear, so a lane's 16 scatters are one base + immediate offsets and need no
+// bounds checks: out-of-image slots are written but never read)
+__host__ __device__ constexpr int kvrow(int W, int Dp) { return W + Dp; }
 
 template <bool SSD>
 using cost_t = typename std::conditional<SSD, uint32_t, uint16_t>::type;
@@ -107,14 +110,15 @@ __global__ __launch_bounds__(kVolThreads) void vol_wta(VolArgs a) {
     const size_t fbytes = a.float_mode == 1 ? (size_t)round16(S * 4) : 0;  // rowF only for float_mode 1
     int32_t *rowFixed = reinterpret_cast<int32_t *>(rowbase);
     float *rowF = reinterpret_cast<float *>(rowbase + (size_t)round16(S * 4));
-    // LR: right-view keys of the whole row (S = W) at ridx(xr) = xr + xr / 16.  The lanes of one
-    // ds_min_u32 scatter hit xr = x0 + k - 16 s - j (pixel k, slice s), i.e. only 8 banks for 64
-    // lanes unpadded; one pad word per 16 keys spreads the slices over the banks (17 s mod 32).
+    // LR: right-view keys of the whole row (S = W) at ridx(xr) = xr + m + Dp - 1 (kvrow).  (Round 2
+    // padded the row (xr + xr / 16) against the 4-way bank conflicts of one scatter's lanes,
+    // xr = x0 + k - 16 s - j: 7.4 -> 1.0 conflict cycles per instruction at an unchanged time; the
+    // linear row instead drops the per-entry address and bounds arithmetic.)
     uint32_t *bestR = reinterpret_cast<uint32_t *>(rowbase + (size_t)round16(S * 4) + fbytes);
-    auto ridx = [](int xr) __attribute__((always_inline)) { return xr + (xr >> 4); };
-    int16_t *rowB = reinterpret_cast<int16_t *>(rowbase + (size_t)round16(S * 4) + fbytes + (size_t)round16(kvpad(W) * 4));
+    auto ridx = [&](int xr) __attribute__((always_inline)) { return xr + m + Dp - 1; };
+    int16_t *rowB = reinterpret_cast<int16_t *>(rowbase + (size_t)round16(S * 4) + fbytes + (size_t)round16(kvrow(W, Dp) * 4));
     if (lr) {
-        for (int i = tid; i < W + (W >> 4) + 1; i += kVolThreads) bestR[i] = 0xFFFFFFFFu;
+        for (int i = tid; i < kvrow(W, Dp); i += kVolThreads) bestR[i] = 0xFFFFFFFFu;
         __syncthreads();
     }
 
@@ -197,13 +201,12 @@ __global__ __launch_bounds__(kVolThreads) void vol_wta(VolArgs a) {
             if ((uint64_t)nm * (uint64_t)(100 - a.uniq) < (uint64_t)cb * 100u) valid = false;
         }
         if (LRM == 1 && inb) {
-            // right-view winners: C(x, d) competes for xr = x - m - d
+            // right-view winners: C(x, d) competes for xr = x - m - d.  No masks: padding
+            // disparities (d >= D) carry the pad cost, so their keys lose to the real key every read
+            // slot holds (the left winner's own), and slots outside the image are never read
+            uint32_t *bl = bestR + ridx(x - m - dbase - (TX - 1));
 #pragma unroll
-            for (int j = 0; j < TX; ++j) {
-                const int dj = dbase + j;
-                const int xr = x - m - dj;
-                if (dj < D && xr >= 0 && xr < W) atomicMin(&bestR[ridx(xr)], (slice_cost<SSD>(cur, j) << DB) | (uint32_t)dj);
-            }
+            for (int j = 0; j < TX; ++j) atomicMin(&bl[TX - 1 - j], (slice_cost<SSD>(cur, j) << DB) | (uint32_t)(dbase + j));
         }
         if (s == 0 && inb) {
             int32_t f = b * 16;
@@ -294,51 +297,59 @@ __global__ __launch_bounds__(kVolThreads) void vol_wta(VolArgs a) {
 // left pass has built the right-view winners by atomicMin over its cost diagonals.
 // ---------------------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void lr_fixup(const int16_t *__restrict__ dstar, const uint32_t *__restrict__ keys,
-                                              uint32_t *__restrict__ keys_next, int64_t n, int64_t nreset, int m, int lr,
+                                              uint32_t *__restrict__ keys_next, int64_t nreset, int64_t n, int m, int lr,
                                               int kshift, int16_t *out_fixed, float *out_float) {
-    // elementwise over the frames' flat pixel index i (4 pixels per thread, 8-B dstar / 16-B
-    // key-reset accesses): the keys read here (this call's buffer) are never written, and the
-    // other buffer's dirty pixels (nreset, consumed by the previous call) are reset to ~0 - so
-    // no row-wide barrier is needed.  Pixel i's right-view partner is key i - m - d*, inside its
-    // own row for every pixel with a winner (x >= m + D - 1 >= m + d*).
+    // elementwise over the frames' flat pixel index i, 8 pixels per thread (one 16-B dstar load,
+    // then the 8 key gathers in flight together): the keys read here (this call's buffer) are never
+    // written, so no row-wide barrier is needed; the other buffer is reset by the next left pass.
+    // Pixel i's right-view partner is key i - m - d*, inside its own row for every pixel with a
+    // winner (x >= m + D - 1 >= m + d*).
     const uint32_t mask = (1u << kshift) - 1u;
-    const int64_t i0 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 4;
-    if (i0 < nreset) {
-        if (i0 + 4 <= nreset && ((uintptr_t)(keys_next + i0) & 15u) == 0) {
-            *reinterpret_cast<uint4 *>(keys_next + i0) = make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu);
+    const int64_t i0 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 8;
+    if (i0 < nreset) {  // DSX_RESET_LEFT 0: the other key half is reset here
+        if (i0 + 8 <= nreset && ((uintptr_t)(keys_next + i0) & 15u) == 0) {
+            const uint4 f = make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu);
+            reinterpret_cast<uint4 *>(keys_next + i0)[0] = f;
+            reinterpret_cast<uint4 *>(keys_next + i0)[1] = f;
         } else {
-            for (int64_t i = i0; i < nreset && i < i0 + 4; ++i) keys_next[i] = 0xFFFFFFFFu;
+            for (int64_t i = i0; i < nreset && i < i0 + 8; ++i) keys_next[i] = 0xFFFFFFFFu;
         }
     }
     if (i0 >= n) return;
-    int16_t b4[4];
-    if (i0 + 4 <= n) {
-        const uint2 v = *reinterpret_cast<const uint2 *>(dstar + i0);
-        b4[0] = (int16_t)(v.x & 0xFFFFu), b4[1] = (int16_t)(v.x >> 16), b4[2] = (int16_t)(v.y & 0xFFFFu), b4[3] = (int16_t)(v.y >> 16);
-    } else {
-        for (int j = 0; j < 4; ++j) b4[j] = i0 + j < n ? dstar[i0 + j] : (int16_t)-1;
-    }
+    int16_t b8[8];
+    if (i0 + 8 <= n) {
+        const uint4 v = *reinterpret_cast<const uint4 *>(dstar + i0);  // dstar is hipMalloc'd: 16-B aligned
+        const uint32_t w[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        const int b = b4[j];
+        for (int j = 0; j < 4; ++j) {
+            b8[2 * j] = (int16_t)(w[j] & 0xFFFFu);
+            b8[2 * j + 1] = (int16_t)(w[j] >> 16);
+        }
+    } else {
+        for (int j = 0; j < 8; ++j) b8[j] = i0 + j < n ? dstar[i0 + j] : (int16_t)-1;
+    }
+    uint32_t kk[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) kk[j] = b8[j] >= 0 ? keys[i0 + j - m - b8[j]] : 0u;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        const int b = b8[j];
         if (b < 0) continue;
-        const int64_t i = i0 + j;
-        const int df = (int)(keys[i - m - b] & mask) - b;
+        const int df = (int)(kk[j] & mask) - b;
         if (df > lr || df < -lr) {
+            const int64_t i = i0 + j;
             if (out_fixed) out_fixed[i] = (int16_t)((m - 1) * 16);
             if (out_float) out_float[i] = (float)(m - 1);
         }
     }
 }
 
-hipError_t launch_lr_fixup(const int16_t *dstar, const uint32_t *keys, uint32_t *keys_next, int rows, int reset_rows,
+hipError_t launch_lr_fixup(const int16_t *dstar, const uint32_t *keys, uint32_t *keys_next, int reset_rows, int rows,
                            int W, int m, int lr, int kshift, int16_t *out_fixed, float *out_float, hipStream_t st) {
-    // dstar is hipMalloc'd, so the flat 4-pixel groups are 8-B aligned; the second key half
-    // starts at an odd multiple of H*W*frames elements, so its resets check 16-B alignment
     const int64_t n = (int64_t)rows * W, nreset = (int64_t)reset_rows * W;
-    const int64_t work = (n > nreset ? n : nreset + 3) / 4 + 1;
-    hipLaunchKernelGGL(lr_fixup, dim3((unsigned)((work + 255) / 256)), dim3(256), 0, st, dstar, keys, keys_next, n, nreset,
-                       m, lr, kshift, out_fixed, out_float);
+    const int64_t work = ((n > nreset ? n : nreset) + 7) / 8;
+    hipLaunchKernelGGL(lr_fixup, dim3((unsigned)((work + 255) / 256)), dim3(256), 0, st, dstar, keys, keys_next, nreset, n, m,
+                       lr, kshift, out_fixed, out_float);
     return hipGetLastError();
 }
 
@@ -347,14 +358,14 @@ hipError_t launch_lr_fixup(const int16_t *dstar, const uint32_t *keys, uint32_t 
 // ---------------------------------------------------------------------------------------
 // scratch (padded slots) + segment results (int32, and f32 for float_mode 1, per pixel of an
 // S-pixel segment) + LR row state (bestR u32 + rowB int16 per pixel of the row)
-static size_t vol_smem(bool ssd, int S, int W, bool lr, bool fm1) {
+static size_t vol_smem(bool ssd, int S, int W, int Dp, bool lr, bool fm1) {
     return (size_t)kVolScratch * (ssd ? 64 : 32) + (size_t)round16(S * 4) * (fm1 ? 2 : 1) +
-           (lr ? (size_t)round16(kvpad(W) * 4) + (size_t)round16(W * 2) : 0);
+           (lr ? (size_t)round16(kvrow(W, Dp) * 4) + (size_t)round16(W * 2) : 0);
 }
 
 size_t volume_smem_bytes(int TX, bool ssd, int Dp, int TPP, int W) {
-    (void)TX, (void)Dp, (void)TPP;
-    return vol_smem(ssd, W, W, true, true);  // the largest form (one segment per row, LR, float_mode 1)
+    (void)TX, (void)TPP;
+    return vol_smem(ssd, W, W, Dp, true, true);  // the largest form (one segment per row, LR, float_mode 1)
 }
 
 template <bool SSD, bool UNIQ, int LRM, int RING, int NSUM = 0>
@@ -378,7 +389,7 @@ static hipError_t launch_vol_ring(const VolArgs &a, hipStream_t st) {
     const int nseg = LR ? 1 : (seg > 1 ? seg : 1);
     const int XC = kVolThreads / (a.Dp / 16);
     const int XSg = ((a.W + nseg - 1) / nseg + XC - 1) / XC * XC;  // as the kernel computes it
-    const size_t smem = vol_smem(SSD, std::min(XSg, a.W), a.W, LR, a.float_mode == 1);
+    const size_t smem = vol_smem(SSD, std::min(XSg, a.W), a.W, a.Dp, LR, a.float_mode == 1);
     hipLaunchKernelGGL((vol_wta<SSD, UNIQ, LRM, RING, NSUM>), dim3(a.H, nseg), dim3(kVolThreads), smem, st, a);
     return hipGetLastError();
 }
