@@ -44,6 +44,9 @@
 #ifndef DSX_XB4  // SAD LR pass: exits parked 4 at a time (one b128 store) in a per-wave region
 #define DSX_XB4 1
 #endif
+#ifndef DSX_SSD_XB  // SSD / SAD1 LR pass: the SAD form of the diagonal move (DPP min + parked exits)
+#define DSX_SSD_XB 0  // measured slower at C3 (326 -> 349 us with 14 % fewer VALU per row step, r03m)
+#endif
 #ifndef DSX_EXP  // experiment bits (tools/exp_build.sh; timing only, results wrong): 1 no LR exit
 #define DSX_EXP 0  // stores, 2 no LR atomics, 4 no diagonal minima, 8 no dstar store, 16 scan argmin on LR
 #endif
@@ -653,8 +656,9 @@ __device__ __forceinline__ void bm2_segment(const Bm2Args &a, uint8_t *smem, int
                 // (DSX_XB4: the full-strip loop keeps 4 exits in registers and parks them with one
                 // single-lane b128 store; r03: 31 exec-masked b32 stores per row cost ~6 % at C2r),
                 // else this wave's slot in each tile row's padding
-                uint8_t *xq = DSX_XB4 ? smem + G::SMEM + 128 * wv : tile + Dp * CB + 4 * wv;
-                constexpr int XST = DSX_XB4 ? 4 : PITCH;
+                constexpr bool XREG = SSD ? DSX_SSD_XB : DSX_XB4;  // exits in the per-wave region
+                uint8_t *xq = XREG ? smem + G::SMEM + 128 * wv : tile + Dp * CB + 4 * wv;
+                constexpr int XST = XREG ? 4 : PITCH;
                 uint32_t X[4] = {0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu};
                 uint32_t Ae = 0xFFFFFFFFu, Ao = 0xFFFFFFFFu, E = 0xFFFFFFFFu;
                 // FULL: the strip lies inside the image and every lane owns real disparities
@@ -672,7 +676,21 @@ __device__ __forceinline__ void bm2_segment(const Bm2Args &a, uint8_t *smem, int
                             if constexpr (SSD) *reinterpret_cast<uint32_t *>(tb + k * PITCH) = abits(acc);
                             else *reinterpret_cast<uint32_t *>(tb + k * PITCH) = as1(acc);
                         }
-                        if constexpr (SSD) {
+                        if constexpr (SSD && DSX_SSD_XB) {
+                            // one slot per lane: the SAD move (min_shr1) with this lane's new key, and
+                            // the top lane's diagonal parked in LDS (4 at a time on full strips)
+                            const uint32_t key = (FULL || x0 + k < W) ? ((abits(acc) << ks) | dmE) : 0xFFFFFFFFu;
+                            Ae = k > 0 ? min_shr1(Ae, key) : key;
+                            if (k < TX - 1) {
+                                if constexpr (FULL) {
+                                    X[k & 3] = Ae;
+                                    if (((k & 3) == 3 || k == TX - 2) && top)
+                                        *reinterpret_cast<uint4 *>(xq + (k & ~3) * 4) = make_uint4(X[0], X[1], X[2], X[3]);
+                                } else if (top) {
+                                    *reinterpret_cast<uint32_t *>(xq + k * XST) = Ae;
+                                }
+                            }
+                        } else if constexpr (SSD) {
                             if (FULL || x0 + k < W) Ae = umin2(Ae, (abits(acc) << ks) | dmE);
                             if (k < TX - 1) {
                                 const uint32_t F = (uint32_t)__builtin_amdgcn_mov_dpp((int)Ae, 0x13C, 0xF, 0xF, false);  // wave_ror:1
@@ -726,7 +744,7 @@ __device__ __forceinline__ void bm2_segment(const Bm2Args &a, uint8_t *smem, int
                 uint32_t *krow = a.lr_keys + fout + (long)y * W;
                 const int dtop = (wv + 1) * G::LDW - 1;  // disparity of the wave's top slot
                 if constexpr (DSX_EXP & 2) {
-                } else if constexpr (SSD) {
+                } else if constexpr (SSD && !DSX_SSD_XB) {
                     const int xe = x0 + (TX - 2 - ln) - m - dtop;  // E lane j: exit of pixel TX-2-j
                     if (ln < TX - 1 && E != 0xFFFFFFFFu && xe >= 0 && xe < W) atomicMin(krow + xe, E);
                 } else if (ln < TX - 1) {
@@ -1110,7 +1128,7 @@ static hipError_t bm2_partition_dev(const PartKey &k, int TX, const int **out) {
 template <int R, bool SSD, int NW, int SIDE, bool ABS = false>
 static hipError_t launch_bm2_side(const Bm2Args &a, hipStream_t st) {
     using G = Geo<R, SSD, NW>;
-    constexpr int SM = G::SMEM + ((SIDE == 3 && !SSD && DSX_XB4) ? 128 * NW : 0);  // + the LR exit region
+    constexpr int SM = G::SMEM + ((SIDE == 3 && (SSD ? DSX_SSD_XB : DSX_XB4)) ? 128 * NW : 0);  // + the LR exit region
     const void *fn = (const void *)bm2<R, SSD, NW, SIDE, ABS>;
     static int blocks_per_cu[64] = {};
     static int num_cu[64] = {};
