@@ -203,3 +203,28 @@ def test_fill_holes_device_does_not_block():
     st.synchronize()
     assert busy
     np.testing.assert_array_equal(got.cpu().numpy(), ref)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("config", ["c4", "c2"])
+def test_fill_holes_device_on_matcher_output(config):
+    """The bench's hole-filling input: the matcher's own map at the config's size after the default
+    post-processing (speckles + outliers), radius 3 as _process_pair passes it - against the host
+    restatement, bit for bit (C4: ~180k holes over ~40 layers)."""
+    import torch
+    from depthestimation_amd.configs import CONFIGS, matcher_kwargs
+    from depthestimation_amd.matcher import HipBlockMatcher, fill_holes_device, postprocess_full_device
+    from depthestimation_amd.synthetic import stereo_pair
+    cfg = CONFIGS[config]
+    H, W, D = cfg["H"], cfg["W"], cfg["num_disp"]
+    L, R, _ = stereo_pair(H, W, 0, D, seed=1234)
+    bm = HipBlockMatcher(device=0, **matcher_kwargs(cfg))
+    dsp = torch.empty((H, W), dtype=torch.float32, device="cuda")
+    bm.compute_device(torch.from_numpy(L).cuda(), torch.from_numpy(R).cuda(), out_float=dsp)
+    clean, _ = postprocess_full_device(dsp, D, max_speckle_size=100, max_diff=1.0, outlier_threshold=2.5)
+    got = fill_holes_device(clean, radius=3)
+    torch.cuda.synchronize()
+    bm.close()
+    c = clean.cpu().numpy()
+    assert (c <= 0).sum() > 1000
+    np.testing.assert_array_equal(got.cpu().numpy(), pp.fill_holes(c, method="inpaint", kernel_size=3))
