@@ -19,8 +19,8 @@
 // counting sort, and the march visits list k at step k.  Nothing is read back to the host:
 //   inp_rows     copy, distance to the nearest known pixel of the row (block scans)
 //   inp_cols     column pass of the L1 transform (segment summaries + scans) -> layer map, with the
-//                per-layer counts and the deepest layer K (LDS histograms)
-//   inp_scan     per-layer list offsets
+//                per-layer counts and the deepest layer K (LDS histograms); its last block to finish
+//                turns the counts into per-layer list offsets
 //   inp_scatter  hole pixels into their layer's list
 //   inp_layer    one launch per layer k = 1..L0, enqueued without waiting; a launch past K exits
 //   inp_rest     layers L0+1..K, if any, in ONE persistent launch with a grid barrier per layer
@@ -41,7 +41,7 @@ namespace {
 
 constexpr int kFar = 1 << 28;             // "no known pixel" in the distance transform
 constexpr int kUnreached = 0x7FFFFFFF;    // layer of a hole no known pixel reaches
-constexpr int kCtlK = 0, kCtlBar = 1, kCtlTmo = 2;
+constexpr int kCtlK = 0, kCtlBar = 1, kCtlTmo = 2, kCtlDone = 3;
 constexpr int kCtlWords = 64;
 constexpr int kHistBins = 2048;           // LDS histogram bins of inp_cols / inp_scatter
 constexpr int kChunk = 4096;              // pixels per block of inp_scatter
@@ -60,23 +60,31 @@ __device__ __forceinline__ double telea_solve(double t1, double t2) {
 
 // ---- L1 distance transform -------------------------------------------------------------------
 
-// Block-wide inclusive scan over 256 values (Hillis-Steele in LDS); MAXOP: max, else min.
+// Block-wide inclusive scan over 256 values into buf[0..255]: MAXOP: prefix max (t' <= t), else
+// suffix min (t' >= t).  Shuffles inside each wave, then the 4 wave totals through LDS.
 template <bool MAXOP>
-__device__ __forceinline__ int block_scan(int v, int *buf) {
-    const int t = threadIdx.x;
+__device__ __forceinline__ void block_scan(int v, int *buf) {
+    __shared__ int wtot[4];
+    const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        if constexpr (MAXOP) {
+            const int u = __shfl_up(v, o);
+            v = lane >= o && u > v ? u : v;
+        } else {
+            const int u = __shfl_down(v, o);
+            v = lane + o < 64 && u < v ? u : v;
+        }
+    }
+    if (lane == (MAXOP ? 63 : 0)) wtot[wv] = v;
+    __syncthreads();
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+        const int u = wtot[w];
+        if (MAXOP ? w < wv : w > wv) v = MAXOP ? (u > v ? u : v) : (u < v ? u : v);
+    }
     buf[t] = v;
     __syncthreads();
-    for (int o = 1; o < 256; o <<= 1) {
-        int u = v;
-        if (MAXOP ? t >= o : t + o < 256) {
-            const int w = buf[MAXOP ? t - o : t + o];
-            u = MAXOP ? (w > v ? w : v) : (w < v ? w : v);
-        }
-        __syncthreads();
-        buf[t] = v = u;
-        __syncthreads();
-    }
-    return v;
 }
 
 // One block per row: out = in, g = distance to the nearest known pixel of the row (kFar if none).
@@ -132,77 +140,123 @@ __global__ __launch_bounds__(256) void inp_rows(const float *in, int64_t pitch, 
 }
 
 // Column pass: layer = min over y' of g(x, y') + |y - y'| (exact L1 distance), 0 on known pixels,
-// kUnreached where no known pixel exists.  Block = 16 columns x 64 row segments; each thread
-// summarises its segment for both directions, takes the other segments' summaries from LDS, then
-// scans its segment forwards (into `layer`) and backwards (combining).
+// kUnreached where no known pixel exists.  Block = 16 columns x 64 row segments; each thread loads
+// its segment of g into registers at once (SLM rows at most; SLM = 0: a row loop for very tall maps),
+// summarises it for both directions, takes the other segments' summaries from LDS, then scans its
+// segment forwards and backwards.  The per-layer counts go through an LDS histogram; the block that
+// finishes last (a done counter, no waiting) turns the counts into list offsets: off[k] = first list
+// slot of layer k (k = 1..K+1), cur[k] = off[k] (the scatter cursors, in place of the counts), and
+// writes the deepest layer K to the host word.
 constexpr int kColW = 16, kColS = 64;
-__global__ __launch_bounds__(1024) void inp_cols(const int *g, int H, int W, int *layer, int *cnt, int *ctl) {
+template <int SLM>
+__global__ __launch_bounds__(1024) void inp_cols(const int *g, int H, int W, int *layer, int *cnt_cur, int *off,
+                                                 int *ctl, int *host_k) {
     __shared__ int sf[kColS][kColW], sb[kColS][kColW];
     __shared__ int hist[kHistBins];
-    __shared__ int kmax;
+    __shared__ int kmax, last;
     for (int i = threadIdx.x; i < kHistBins; i += 1024) hist[i] = 0;
     if (threadIdx.x == 0) kmax = 0;
     const int cx = threadIdx.x % kColW, sj = threadIdx.x / kColW;
     const int x = blockIdx.x * kColW + cx;
-    const int SL = (H + kColS - 1) / kColS;
+    const int SL = (H + kColS - 1) / kColS;  // <= SLM (host) unless SLM == 0
     const int y0 = min(H, sj * SL), y1 = min(H, y0 + SL);
     const bool live = x < W;
+    constexpr int NR = SLM > 0 ? SLM : 1;
+    int gv[NR];
     int cf = kFar, cb = kFar;  // min_y g(y) + (y1 - 1 - y) and min_y g(y) + (y - y0)
-    if (live)
+    if constexpr (SLM > 0) {
+#pragma unroll
+        for (int i = 0; i < SLM; ++i) gv[i] = (live && y0 + i < y1) ? g[(int64_t)(y0 + i) * W + x] : kFar;
+#pragma unroll
+        for (int i = 0; i < SLM; ++i) {
+            // rows past the segment must not count: kFar - offset would read as a (huge) layer
+            if (y0 + i < y1) {
+                cf = min(cf, gv[i] + (y1 - 1 - (y0 + i)));
+                cb = min(cb, gv[i] + i);
+            }
+        }
+    } else if (live) {
         for (int y = y0; y < y1; ++y) {
             const int v = g[(int64_t)y * W + x];
             cf = min(cf, v + (y1 - 1 - y));
             cb = min(cb, v + (y - y0));
         }
+    }
     sf[sj][cx] = cf;
     sb[sj][cx] = cb;
     __syncthreads();
+    // distance from the segments above (at row y0 - 1) / below (at row y1)
+    int hf = kFar, hb = kFar;
+#pragma unroll 16
+    for (int j = 0; j < kColS; ++j) {
+        const int ys = min(H, j * SL), ye = min(H, (j + 1) * SL);  // segment j: rows ys..ye-1
+        const int vf = sf[j][cx] + (y0 - ye), vb = sb[j][cx] + (ys - y1);
+        hf = j < sj ? min(hf, vf) : hf;
+        hb = (j > sj && ys < H) ? min(hb, vb) : hb;
+    }
     int km = 0;
-    if (live && y0 < y1) {
-    int hf = kFar, hb = kFar;  // distance from rows above y0 (at row y0 - 1) / below y1 - 1 (at row y1)
-    for (int j = 0; j < sj; ++j) {
-        const int ye = min(H, (j + 1) * SL);  // segment j ends at row ye - 1
-        hf = min(hf, sf[j][cx] + (y0 - ye));
-    }
-    for (int j = sj + 1; j < kColS; ++j) {
-        const int ys = min(H, j * SL);
-        if (ys < H) hb = min(hb, sb[j][cx] + (ys - y1));
-    }
-    for (int y = y0; y < y1; ++y) {
-        hf = min(g[(int64_t)y * W + x], hf + 1);
-        layer[(int64_t)y * W + x] = hf;
-    }
-    for (int y = y1 - 1; y >= y0; --y) {
-        const int64_t o = (int64_t)y * W + x;
-        hb = min(g[o], hb + 1);
-        const int d = min(layer[o], hb);
-        layer[o] = d >= kFar ? kUnreached : d;  // known pixels: g = 0
-        // per-layer hole counts (cnt[k], k >= 1) and the deepest reached layer ctl[kCtlK]
-        if (d > 0 && d < kFar) {
+    auto emit = [&](int y, int d) {
+        // a reached hole lies at most H + W - 2 from a known pixel; anything past H + W is a
+        // kFar-derived "no known pixel" (and never indexes the per-layer counts)
+        const bool reached = d <= H + W;
+        layer[(int64_t)y * W + x] = reached ? d : kUnreached;  // known pixels: g = 0
+        if (d > 0 && reached) {
             km = d > km ? d : km;
             if (d < kHistBins) atomicAdd(&hist[d], 1);
-            else atomicAdd(&cnt[d], 1);
+            else atomicAdd(&cnt_cur[d], 1);
         }
-    }
+    };
+    if constexpr (SLM > 0) {
+        int fw[SLM];
+#pragma unroll
+        for (int i = 0; i < SLM; ++i) {
+            hf = min(gv[i], hf + 1);
+            fw[i] = hf;
+        }
+#pragma unroll
+        for (int i = SLM - 1; i >= 0; --i) {
+            if (live && y0 + i < y1) {
+                hb = min(gv[i], hb + 1);
+                emit(y0 + i, min(fw[i], hb));
+            }
+        }
+    } else if (live) {
+        for (int y = y0; y < y1; ++y) {
+            hf = min(g[(int64_t)y * W + x], hf + 1);
+            layer[(int64_t)y * W + x] = hf;
+        }
+        for (int y = y1 - 1; y >= y0; --y) {
+            const int64_t o = (int64_t)y * W + x;
+            hb = min(g[o], hb + 1);
+            emit(y, min(layer[o], hb));
+        }
     }
     atomicMax(&kmax, km);
     __syncthreads();
-    for (int i = threadIdx.x; i < kHistBins; i += 1024)
-        if (hist[i]) atomicAdd(&cnt[i], hist[i]);
+    const int kb = min(kmax + 1, kHistBins);
+    for (int i = threadIdx.x; i < kb; i += 1024)
+        if (hist[i]) atomicAdd(&cnt_cur[i], hist[i]);
     if (threadIdx.x == 0 && kmax) atomicMax(&ctl[kCtlK], kmax);
-}
 
-// off[k] = first list slot of layer k (k = 1..K+1); cur[k] = off[k] (scatter cursors, in place of
-// the counts).  One block.
-__global__ __launch_bounds__(1024) void inp_scan(int *cnt_cur, int *off, const int *ctl, int *host_k) {
-    __shared__ int part[1024];
-    const int K = ctl[kCtlK];
+    // ---- the last block to finish: per-layer list offsets ----
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        const unsigned done = __hip_atomic_fetch_add(reinterpret_cast<unsigned *>(ctl + kCtlDone), 1u,
+                                                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        last = done == gridDim.x - 1;
+        if (last) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    }
+    __syncthreads();
+    if (!last) return;  // block-uniform
+    int *part = &sf[0][0];  // 1024 ints of LDS, free now
+    const int K = __hip_atomic_load(&ctl[kCtlK], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const int t = threadIdx.x;
     const int chunk = (K + 1024) / 1024;  // layers 1..K
     const int k0 = 1 + t * chunk, k1 = min(K + 1, k0 + chunk);
-    int s = 0;
-    for (int k = k0; k < k1; ++k) s += cnt_cur[k];
-    part[t] = s;
+    int sum = 0;
+    for (int k = k0; k < k1; ++k) sum += __hip_atomic_load(&cnt_cur[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    part[t] = sum;
     __syncthreads();
     for (int o = 1; o < 1024; o <<= 1) {
         const int v = t >= o ? part[t - o] : 0;
@@ -212,7 +266,7 @@ __global__ __launch_bounds__(1024) void inp_scan(int *cnt_cur, int *off, const i
     }
     int base = t > 0 ? part[t - 1] : 0;
     for (int k = k0; k < k1; ++k) {
-        const int c = cnt_cur[k];
+        const int c = __hip_atomic_load(&cnt_cur[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         off[k] = base;
         cnt_cur[k] = base;
         base += c;
@@ -222,10 +276,11 @@ __global__ __launch_bounds__(1024) void inp_scan(int *cnt_cur, int *off, const i
 }
 
 // Hole pixels into their layer's list (order inside a layer is free: its pixels are independent).
-__global__ __launch_bounds__(256) void inp_scatter(const int *layer, int n, int *cur, int *list) {
+__global__ __launch_bounds__(256) void inp_scatter(const int *layer, int n, int *cur, int *list, const int *ctl) {
     __shared__ int h[kHistBins], base[kHistBins];
     constexpr int PER = kChunk / 256;
-    for (int i = threadIdx.x; i < kHistBins; i += 256) h[i] = 0;
+    const int nb = min(ctl[kCtlK] + 1, kHistBins);  // bins 0..K
+    for (int i = threadIdx.x; i < nb; i += 256) h[i] = 0;
     __syncthreads();
     const int p0 = blockIdx.x * kChunk;
     int rank[PER];
@@ -242,7 +297,7 @@ __global__ __launch_bounds__(256) void inp_scatter(const int *layer, int n, int 
         }
     }
     __syncthreads();
-    for (int i = threadIdx.x; i < kHistBins; i += 256)
+    for (int i = threadIdx.x; i < nb; i += 256)
         if (h[i]) base[i] = atomicAdd(&cur[i], h[i]);
     __syncthreads();
 #pragma unroll
@@ -259,13 +314,15 @@ struct Front {
 };
 
 // T and grad T of a pixel p of layer k from its earlier-layer 4-neighbours (T 1e6 when absent).
+// The 8 loads are unconditional (clamped to p at the border, then discarded) so they issue together.
 __device__ __forceinline__ Front front_of(const int *layer, const double *T, int p, int y, int x, int H, int W, int k) {
     Front f;
     const bool iu = y > 0, id = y < H - 1, il = x > 0, ir = x < W - 1;
-    const int lu = iu ? layer[p - W] : kUnreached, ld = id ? layer[p + W] : kUnreached;
-    const int ll = il ? layer[p - 1] : kUnreached, lr = ir ? layer[p + 1] : kUnreached;
-    const double Tu = iu ? T[p - W] : 1e6, Td = id ? T[p + W] : 1e6;
-    const double Tl = il ? T[p - 1] : 1e6, Tr = ir ? T[p + 1] : 1e6;
+    const int pu = iu ? p - W : p, pd = id ? p + W : p, pl = il ? p - 1 : p, pr = ir ? p + 1 : p;
+    const int lu0 = layer[pu], ld0 = layer[pd], ll0 = layer[pl], lr0 = layer[pr];
+    const double Tu = T[pu], Td = T[pd], Tl = T[pl], Tr = T[pr];
+    const int lu = iu ? lu0 : kUnreached, ld = id ? ld0 : kUnreached;
+    const int ll = il ? ll0 : kUnreached, lr = ir ? lr0 : kUnreached;
     const bool ou = lu < k, od = ld < k, ol = ll < k, orr = lr < k;
     // T is never initialised: known pixels (layer 0) have T = 0, holes of earlier layers their march value
     const double tu = ou ? (lu == 0 ? 0.0 : Tu) : 1e6, td = od ? (ld == 0 ? 0.0 : Td) : 1e6;
@@ -279,18 +336,12 @@ __device__ __forceinline__ Front front_of(const int *layer, const double *T, int
     return f;
 }
 
-// Weight of the window cell (oy, ox) for the pixel (y, x); false when the cell is outside the disc,
-// the image or the earlier layers.  The cell's layer, T and value load together.
-__device__ __forceinline__ bool cell_term(const float *out, const int *layer, const double *T, int y, int x, int oy,
-                                          int ox, int H, int W, int r2, int k, const Front &f, double &w, double &wv) {
+// Telea's weight of the window cell (oy, ox) with layer lq, stored T Tq and value vq (known pixels,
+// layer 0, have T = 0, not stored).
+__device__ __forceinline__ void cell_weight(int oy, int ox, int lq, double Tq, float vq, const Front &f, double &w,
+                                            double &wv) {
     const int d2 = oy * oy + ox * ox;
-    const int qy = y + oy, qx = x + ox;
-    if (d2 == 0 || d2 > r2 || qy < 0 || qy >= H || qx < 0 || qx >= W) return false;
-    const int64_t q = (int64_t)qy * W + qx;
-    const int lq = layer[q];
-    const double tq = lq == 0 ? 0.0 : T[q];  // known pixels: T = 0 (not stored)
-    const float vq = out[q];
-    if (lq >= k) return false;
+    const double tq = lq == 0 ? 0.0 : Tq;
     const double ry = (double)(-oy), rx = (double)(-ox);
     const double w_dir = __builtin_fabs(ry * f.gy + rx * f.gx) / __builtin_sqrt((double)d2);
     const double w_dst = 1.0 / (double)d2;
@@ -298,6 +349,21 @@ __device__ __forceinline__ bool cell_term(const float *out, const int *layer, co
     w = w_dir * w_dst * w_lev;
     w = w > 1e-6 ? w : 1e-6;
     wv = w * (double)vq;
+}
+
+// Weight of the window cell (oy, ox) for the pixel (y, x); false when the cell is outside the disc,
+// the image or the earlier layers.
+__device__ __forceinline__ bool cell_term(const float *out, const int *layer, const double *T, int y, int x, int oy,
+                                          int ox, int H, int W, int r2, int k, const Front &f, double &w, double &wv) {
+    const int d2 = oy * oy + ox * ox;
+    const int qy = y + oy, qx = x + ox;
+    if (d2 == 0 || d2 > r2 || qy < 0 || qy >= H || qx < 0 || qx >= W) return false;
+    const int64_t q = (int64_t)qy * W + qx;
+    const int lq = layer[q];
+    const double Tq = T[q];
+    const float vq = out[q];
+    if (lq >= k) return false;
+    cell_weight(oy, ox, lq, Tq, vq, f, w, wv);
     return true;
 }
 
@@ -308,6 +374,8 @@ __device__ __forceinline__ bool cell_term(const float *out, const int *layer, co
 template <int G>
 __device__ __forceinline__ void march_layer_grp(float *out, const int *layer, double *T, int H, int W, int radius,
                                                 int k, const int *list, int beg, int end, int g0, int gstride) {
+    constexpr int RM = (G - 2) / 2;  // widest radius of the group form: 3 (G 8), 7 (G 16)
+    constexpr int NCELL = 2 * RM + 1;
     const int j = threadIdx.x & (G - 1);
     const int r2 = radius * radius;
     for (int i = beg + g0; i < end; i += gstride) {  // group-uniform
@@ -316,13 +384,33 @@ __device__ __forceinline__ void march_layer_grp(float *out, const int *layer, do
         const Front f = front_of(layer, T, p, y, x, H, W, k);
         double rn = 0.0, rd = 0.0;
         if (j <= 2 * radius) {
+            // the whole window row loads at once (clamped addresses, unused cells discarded), then
+            // the cells are summed left to right, skipping the ones outside the disc / image / layers
             const int oy = j - radius;
-            for (int ox = -radius; ox <= radius; ++ox) {
+            const int qy = y + oy;
+            const bool rowin = qy >= 0 && qy < H;
+            const int64_t rowq = (int64_t)(rowin ? qy : y) * W;
+            int lq[NCELL];
+            double tq[NCELL];
+            float vq[NCELL];
+#pragma unroll
+            for (int c = 0; c < NCELL; ++c) {
+                const int qx = x + c - RM;
+                const int64_t q = rowq + (qx < 0 ? 0 : (qx >= W ? W - 1 : qx));
+                lq[c] = layer[q];
+                tq[c] = T[q];
+                vq[c] = out[q];
+            }
+#pragma unroll
+            for (int c = 0; c < NCELL; ++c) {
+                const int ox = c - RM;
+                const int qx = x + ox;
+                const int d2 = oy * oy + ox * ox;
+                const bool use = rowin && qx >= 0 && qx < W && d2 > 0 && d2 <= r2 && lq[c] < k;
                 double w, wv;
-                if (cell_term(out, layer, T, y, x, oy, ox, H, W, r2, k, f, w, wv)) {
-                    rn = rn + wv;
-                    rd = rd + w;
-                }
+                cell_weight(oy, ox, lq[c], tq[c], vq[c], f, w, wv);
+                rn = use ? rn + wv : rn;
+                rd = use ? rd + w : rd;
             }
         }
         double num = 0.0, den = 0.0;
@@ -432,6 +520,15 @@ __global__ __launch_bounds__(256) void inp_rest(float *out, const int *layer, do
 
 size_t align256(size_t b) { return (b + 255) & ~(size_t)255; }
 
+// DSX_INPAINT_DEBUG=1: synchronise after every launch and name the kernel that failed (stderr).
+hipError_t dbg_sync(const char *what, hipStream_t st) {
+    static const bool on = getenv("DSX_INPAINT_DEBUG") != nullptr;
+    hipError_t e = hipGetLastError();
+    if (e == hipSuccess && on) e = hipStreamSynchronize(st);
+    if (e != hipSuccess && on) fprintf(stderr, "dsx inpaint: %s failed: %s\n", what, hipGetErrorString(e));
+    return e;
+}
+
 struct Views {
     int *layer, *g, *list, *cnt, *off, *ctl;
     double *T;
@@ -497,18 +594,19 @@ hipError_t launch_inpaint(const float *in, int64_t pitch, int H, int W, int radi
         }
     }
     hipLaunchKernelGGL(inp_rows, dim3(H), dim3(256), (size_t)W * 8, st, in, pitch, H, W, out, v.g, v.cnt, v.ncnt, v.ctl);
-    if ((e = hipGetLastError()) != hipSuccess) return e;
+    if ((e = dbg_sync("inp_rows", st)) != hipSuccess) return e;
     if (radius < 1) return hipSuccess;  // no neighbourhood: nothing changes (cv2 uses radius >= 1)
-    hipLaunchKernelGGL(inp_cols, dim3((W + kColW - 1) / kColW), dim3(1024), 0, st, v.g, H, W, v.layer, v.cnt, v.ctl);
-    if ((e = hipGetLastError()) != hipSuccess) return e;
-    const int nch = (n + kChunk - 1) / kChunk;
     int *hk = lastk_host();
     int *hk_dev = nullptr;
     if (hk && hipHostGetDevicePointer(reinterpret_cast<void **>(&hk_dev), hk, 0) != hipSuccess) hk_dev = nullptr;
-    hipLaunchKernelGGL(inp_scan, dim3(1), dim3(1024), 0, st, v.cnt, v.off, v.ctl, hk_dev);
-    if ((e = hipGetLastError()) != hipSuccess) return e;
-    hipLaunchKernelGGL(inp_scatter, dim3(nch), dim3(256), 0, st, v.layer, n, v.cnt, v.list);
-    if ((e = hipGetLastError()) != hipSuccess) return e;
+    const int SL = (H + kColS - 1) / kColS;
+    auto cols = SL <= 16 ? inp_cols<16> : SL <= 32 ? inp_cols<32> : SL <= 48 ? inp_cols<48> : inp_cols<0>;
+    hipLaunchKernelGGL(cols, dim3((W + kColW - 1) / kColW), dim3(1024), 0, st, v.g, H, W, v.layer, v.cnt, v.off, v.ctl,
+                       hk_dev);
+    if ((e = dbg_sync("inp_cols", st)) != hipSuccess) return e;
+    const int nch = (n + kChunk - 1) / kChunk;
+    hipLaunchKernelGGL(inp_scatter, dim3(nch), dim3(256), 0, st, v.layer, n, v.cnt, v.list, v.ctl);
+    if ((e = dbg_sync("inp_scatter", st)) != hipSuccess) return e;
 
     // per-layer launches, enqueued without waiting: as many as the previous call needed (+1), at
     // least 8; the persistent kernel takes whatever is left
@@ -523,7 +621,7 @@ hipError_t launch_inpaint(const float *in, int64_t pitch, int H, int W, int radi
     auto lay = np == 8 ? inp_layer<8> : np == 16 ? inp_layer<16> : inp_layer<0>;
     for (int k = 1; k <= L0; ++k) {
         hipLaunchKernelGGL(lay, dim3(lgrid), dim3(256), 0, st, out, v.layer, v.T, H, W, radius, k, v.list, v.off, v.ctl);
-        if ((e = hipGetLastError()) != hipSuccess) return e;
+        if ((e = dbg_sync("inp_layer", st)) != hipSuccess) return e;
     }
     if (L0 < maxk) {
         static int ncu[64] = {};
@@ -538,7 +636,7 @@ hipError_t launch_inpaint(const float *in, int64_t pitch, int H, int W, int radi
         auto rest = np == 8 ? inp_rest<8> : np == 16 ? inp_rest<16> : inp_rest<0>;
         hipLaunchKernelGGL(rest, dim3(ncu[dev]), dim3(256), 0, st, out, v.layer, v.T, H, W, radius, L0 + 1, v.list, v.off,
                            v.ctl);
-        if ((e = hipGetLastError()) != hipSuccess) return e;
+        if ((e = dbg_sync("inp_rest", st)) != hipSuccess) return e;
     }
     return hipSuccess;
 }

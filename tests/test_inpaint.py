@@ -117,6 +117,24 @@ def test_fill_holes_device_matches_host(shape, radius, seed):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("H", [1, 63, 1030, 2100, 3100])
+def test_fill_holes_device_tall_maps(H):
+    """Every form of the column pass: a thread's row segment (ceil(H / 64) rows) held in registers
+    as 16, 32 or 48 rows, or walked by a row loop past 48 (H > 3072)."""
+    import torch
+    from depthestimation_amd.matcher import fill_holes_device
+    d = _holey(H, 37, 20 + H % 7, frac=0.25)
+    d[H // 3: H // 3 + min(H, 300), 5:20] = 0  # a tall hole: layers across row segments
+    e = d.copy()
+    e[:, 30:] = 0                                # columns with no known pixel in any row ...
+    e[: H // 2, :] = 0                           # ... and rows with none
+    for m in (d, e, np.zeros_like(d)):
+        ref = pp.fill_holes(m, method="inpaint", kernel_size=3)
+        got = fill_holes_device(torch.from_numpy(m).cuda(), radius=3)
+        np.testing.assert_array_equal(got.cpu().numpy(), ref)
+
+
+@pytest.mark.gpu
 def test_fill_holes_device_edge_cases():
     import torch
     from depthestimation_amd.matcher import fill_holes_device
