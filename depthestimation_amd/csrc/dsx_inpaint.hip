@@ -41,7 +41,7 @@ namespace {
 
 constexpr int kFar = 1 << 28;             // "no known pixel" in the distance transform
 constexpr int kUnreached = 0x7FFFFFFF;    // layer of a hole no known pixel reaches
-constexpr int kCtlK = 0, kCtlBar = 1, kCtlTmo = 2, kCtlDone = 3;
+constexpr int kCtlK = 0, kCtlBar = 1, kCtlTmo = 2, kCtlDone = 3, kCtlGen = 32;  // Gen: own cache line
 constexpr int kCtlWords = 64;
 constexpr int kHistBins = 2048;           // LDS histogram bins of inp_cols / inp_scatter
 constexpr int kChunk = 4096;              // pixels per block of inp_scatter
@@ -472,26 +472,33 @@ __global__ __launch_bounds__(256) void inp_layer(float *out, const int *layer, d
     march_layer<G>(out, layer, T, H, W, radius, k, list, beg, end, blockIdx.x, gridDim.x);
 }
 
-// Grid barrier (one monotonic counter): every wave drains its stores, lane 0 of the block releases
-// them to the device (agent scope), arrives, polls the counter relaxed with s_sleep, then acquires
-// (invalidates this CU's L1) before any wave reads pixels other blocks wrote.  Spins are bounded: on
-// a timeout the block sets the timeout word and every block leaves the march.
-__device__ __forceinline__ bool grid_barrier(unsigned *ctr, unsigned target, int *tmo) {
+// Grid barrier: every wave drains its stores, lane 0 of the block releases them to the device
+// (agent scope) and arrives on a monotonic counter; the block that arrives last publishes the epoch
+// in a generation word on its own cache line, which the others poll (relaxed, with s_sleep) - so the
+// pollers never contend with the arrivals.  Then an acquire (invalidates this CU's caches) before any
+// wave reads pixels other blocks wrote.  Spins are bounded: on a timeout the block sets the timeout
+// word and every block leaves the march.
+__device__ __forceinline__ bool grid_barrier(unsigned *ctr, unsigned *gen, unsigned epoch, unsigned nblk, int *tmo) {
     __shared__ int ok;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (threadIdx.x == 0) {
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const unsigned old = __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         int good = 1;
-        for (unsigned spins = 0; __hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target; ++spins) {
-            __builtin_amdgcn_s_sleep(2);
-            if ((spins & 255u) == 255u &&
-                (spins > (1u << 22) || __hip_atomic_load(tmo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))) {
-                __hip_atomic_store(tmo, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                good = 0;
-                break;
+        if (old == epoch * nblk - 1) {  // last arrival of this epoch
+            __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "agent");
+            __hip_atomic_store(gen, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        } else {
+            for (unsigned spins = 0; __hip_atomic_load(gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < epoch; ++spins) {
+                __builtin_amdgcn_s_sleep(1);
+                if ((spins & 255u) == 255u &&
+                    (spins > (1u << 23) || __hip_atomic_load(tmo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))) {
+                    __hip_atomic_store(tmo, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    good = 0;
+                    break;
+                }
             }
         }
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
@@ -514,7 +521,9 @@ __global__ __launch_bounds__(256) void inp_rest(float *out, const int *layer, do
         march_layer<G>(out, layer, T, H, W, radius, k, list, off[k], off[k + 1], blockIdx.x, gridDim.x);
         if (k == K) break;
         ++epoch;
-        if (!grid_barrier(reinterpret_cast<unsigned *>(ctl + kCtlBar), epoch * gridDim.x, ctl + kCtlTmo)) return;
+        if (!grid_barrier(reinterpret_cast<unsigned *>(ctl + kCtlBar), reinterpret_cast<unsigned *>(ctl + kCtlGen), epoch,
+                          gridDim.x, ctl + kCtlTmo))
+            return;
     }
 }
 
@@ -634,7 +643,9 @@ hipError_t launch_inpaint(const float *in, int64_t pitch, int H, int W, int radi
             ncu[dev] = c > 0 ? c : 1;
         }
         auto rest = np == 8 ? inp_rest<8> : np == 16 ? inp_rest<16> : inp_rest<0>;
-        hipLaunchKernelGGL(rest, dim3(ncu[dev]), dim3(256), 0, st, out, v.layer, v.T, H, W, radius, L0 + 1, v.list, v.off,
+        int rb = ncu[dev];
+        if (const char *fb = getenv("DSX_INPAINT_RB")) rb = std::max(1, std::min(ncu[dev], atoi(fb)));  // experiments
+        hipLaunchKernelGGL(rest, dim3(rb), dim3(256), 0, st, out, v.layer, v.T, H, W, radius, L0 + 1, v.list, v.off,
                            v.ctl);
         if ((e = dbg_sync("inp_rest", st)) != hipSuccess) return e;
     }
