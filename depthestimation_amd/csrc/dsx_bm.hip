@@ -172,8 +172,27 @@ typedef const __attribute__((address_space(4))) uint32_t cu32;
 // image (one unaligned dword + one byte load per lane and row); otherwise replicate-clamped
 // byte loads. All per-row state is in plain registers (no structs / arrays with runtime
 // indices, which hipcc would demote to scratch).
+// The LR pass's row loop re-reads the launch arguments from the kernarg segment every row (scalar
+// loads through a pointer the compiler cannot hoist) instead of keeping them live across the loop,
+// where the SGPR budget spilled them to VGPR lanes: one v_readlane (a VALU op) per reuse, ~70 per
+// row step.
+#ifndef DSX_KARG
+#define DSX_KARG 1
+#endif
+template <bool RELOAD>
+__device__ __forceinline__ Bm2Args kargs_row(const Bm2Args &a) {
+    if constexpr (RELOAD) {
+        typedef __attribute__((address_space(4))) const Bm2Args KArgs;
+        KArgs *p = (KArgs *)__builtin_amdgcn_kernarg_segment_ptr();
+        asm volatile("" : "+s"(p));
+        return *(const Bm2Args *)p;  // loads stay scalar: the address space is inferred through the cast
+    } else {
+        return a;
+    }
+}
+
 template <int R, bool SSD, int NW, int SIDE, bool FAST, bool ABS, bool LRFULL>
-__device__ __forceinline__ void bm2_segment(const Bm2Args &a, uint8_t *smem, int x0, int yb, int ye, long fin, long fout,
+__device__ __forceinline__ void bm2_segment(const Bm2Args &a_in, uint8_t *smem, int x0, int yb, int ye, long fin, long fout,
                                             bool lr_on, int done0, const int (&pe)[3], int &qcur
 #ifdef DSX_STAMPS
                                             , uint64_t (&ph)[8], uint64_t &t_prev, uint64_t &nsteps
@@ -184,6 +203,7 @@ __device__ __forceinline__ void bm2_segment(const Bm2Args &a, uint8_t *smem, int
                   PITCH = G::PITCH, NJ = G::NJ, SLOT = G::SLOT, NB = G::NB, NJ4 = (NJ + 3) / 4,
                   NCH = (NC + 7) / 8;
     constexpr int side = SIDE;
+    const Bm2Args &a = a_in;
     // FSS: SSD sums in f32.  Squared differences, column sums and (offset) box sums are integers
     // below 2^24, so v_sub_f32 / v_fma_f32 / v_add_f32 (full rate, ~2 cycles) are exact and
     // replace the quarter-rate v_mad_i32_i24.  Box sums carry a +2^23 offset: for box < 2^23
@@ -528,6 +548,7 @@ __device__ __forceinline__ void bm2_segment(const Bm2Args &a, uint8_t *smem, int
     const bool lane_writes = d0 < D;
 
     for (int y = yb; y < ye; ++y) {
+        const Bm2Args &a = kargs_row<SIDE == 3 && DSX_KARG>(a_in);
 #ifdef DSX_STAMPS
         ++nsteps;
 #endif
