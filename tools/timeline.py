@@ -20,13 +20,14 @@ cfg.pop("desc")
 L, R, _ = stereo_pair(H, W, 0, D, seed=1)
 tL, tR = torch.from_numpy(L).cuda(), torch.from_numpy(R).cuda()
 out = torch.empty((H, W), dtype=torch.int16, device="cuda")
+kw = {"out_float": torch.empty((H, W), dtype=torch.float32, device="cuda")} if os.environ.get("TL_FLOAT") else {}  # bench's outputs
 m = HipBlockMatcher(grid_blocks=grid, **cfg)
-for _ in range(3):
-    m.compute_device(tL, tR, out_fixed=out)
+for _ in range(int(os.environ.get("TL_WARM", "3"))):  # TL_WARM=2000: settled clocks (steady state)
+    m.compute_device(tL, tR, out_fixed=out, **kw)
 torch.cuda.synchronize()
 path = "/tmp/tl.bin"
 os.environ["DSX_TIMELINE"] = path
-m.compute_device(tL, tR, out_fixed=out)
+m.compute_device(tL, tR, out_fixed=out, **kw)
 torch.cuda.synchronize()
 del os.environ["DSX_TIMELINE"]
 raw = np.fromfile(path, dtype=np.uint64)
