@@ -406,8 +406,13 @@ static hipError_t launch_vol_lr(const VolArgs &a, hipStream_t st) {
     }
 }
 
+#ifndef DSX_K2_RING_LR  // ring depth of the A5' LR form (experiment switch)
+#define DSX_K2_RING_LR 3
+#endif
 template <bool SSD>
 static hipError_t launch_vol_cost(const VolArgs &a, hipStream_t st) {
+    if (lr_mode(a) == 1 && DSX_K2_RING_LR != 3)
+        return a.uniq > 0 ? launch_vol_ring<SSD, true, 1, DSX_K2_RING_LR>(a, st) : launch_vol_ring<SSD, false, 1, DSX_K2_RING_LR>(a, st);
     return a.uniq > 0 ? launch_vol_lr<SSD, true, 3>(a, st) : launch_vol_lr<SSD, false, 3>(a, st);
 }
 
