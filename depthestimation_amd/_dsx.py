@@ -32,7 +32,7 @@ EXPORTS = (
     "dsx_set_params", "dsx_compute_host", "dsx_compute_device", "dsx_compute_batch_device", "dsx_right_map_device",
     "dsx_postprocess_fast_device", "dsx_postprocess_workspace_bytes", "dsx_postprocess_full_device",
     "dsx_postprocess_full_ex_device", "dsx_fill_holes_workspace_bytes", "dsx_fill_holes_device",
-    "dsx_rectify_device",
+    "dsx_rectify_device", "dsx_fill_holes_status", "dsx_process_pair_device",
     "dsx_kernel_times", "dsx_reset_times", "dsx_workspace_bytes", "dsx_destroy", "dsx_last_error",
     "dsx_comm_init_all", "dsx_comm_size", "dsx_bcast", "dsx_comm_destroy",
 )
@@ -63,6 +63,30 @@ class DsxParams(ctypes.Structure):
         ("speckle_range", ctypes.c_int32),
         ("lr_form", ctypes.c_int32),
         ("reserved", ctypes.c_int32 * 3),
+    ]
+
+
+POST_MODE = {"fast": 1, "full": 2}  # DSX_POST_* (include/dsx.h)
+
+
+class DsxPostParams(ctypes.Structure):
+    """dsx_post_params (include/dsx.h): the post-processing of StereoCore._process_pair."""
+    _fields_ = [
+        ("max_diff", ctypes.c_double),
+        ("outlier_threshold", ctypes.c_double),
+        ("focal_length", ctypes.c_double),
+        ("baseline", ctypes.c_double),
+        ("doffs", ctypes.c_double),
+        ("eps", ctypes.c_double),
+        ("max_depth", ctypes.c_double),
+        ("mode", ctypes.c_int32),
+        ("max_speckle_size", ctypes.c_int32),
+        ("apply_outlier_removal", ctypes.c_int32),
+        ("outlier_kernel", ctypes.c_int32),
+        ("fill_radius", ctypes.c_int32),
+        ("has_depth", ctypes.c_int32),
+        ("has_max_depth", ctypes.c_int32),
+        ("reserved", ctypes.c_int32 * 5),
     ]
 
 
@@ -99,6 +123,9 @@ def _bind(lib):
         "dsx_postprocess_fast_device": (ctypes.c_int, [vp, i32, i32, i64, i32, vp, vp, ctypes.c_double,
                                                         ctypes.c_double, ctypes.c_double, ctypes.c_double,
                                                         ctypes.c_double, i32, vp]),
+        "dsx_fill_holes_status": (ctypes.c_int, []),
+        "dsx_process_pair_device": (ctypes.c_int, [vp, vp, vp, i32, i32, i64, ctypes.POINTER(DsxPostParams), vp, vp,
+                                                    vp]),
         "dsx_kernel_times": (ctypes.c_int, [vp, ctypes.c_char_p, ctypes.c_int, ctypes.POINTER(ctypes.c_float),
                                              ctypes.POINTER(ctypes.c_int), ctypes.c_int, ctypes.POINTER(ctypes.c_int)]),
         "dsx_reset_times": (ctypes.c_int, [vp]),

@@ -163,6 +163,9 @@ struct dsx_handle {
     int16_t *postIn = nullptr;  // sgbm_post: the matcher's int16 maps (postFrames frames)
     void *postWs = nullptr;     // sgbm_post: median | speckle components
     int postFrames = 0;
+    float *ppDisp = nullptr;    // dsx_process_pair_device: the matcher's float map (H x W)
+    void *ppWs = nullptr;       // dsx_process_pair_device: post-processing workspace
+    size_t ppWsBytes = 0;
     uint32_t *sgmS = nullptr;  // SGM path sums [H][W][Dp] u32 (sequential directions)
     uint16_t *sgmL = nullptr;  // SGM L_r per direction, ndir x [H][W][Dp] u16 (concurrent directions)
     // timing
@@ -192,6 +195,11 @@ void free_buffers(dsx_handle *h) {
     h->postFrames = 0;
     (void)hipFree(h->sgmS);
     h->sgmS = nullptr;
+    (void)hipFree(h->ppDisp);
+    (void)hipFree(h->ppWs);
+    h->ppDisp = nullptr;
+    h->ppWs = nullptr;
+    h->ppWsBytes = 0;
     (void)hipFree(h->sgmL);
     h->sgmL = nullptr;
     h->dL = h->dR = nullptr;
@@ -328,6 +336,32 @@ int collect_times(dsx_handle *h) {
     return DSX_OK;
 }
 
+// Records the handle's scratch event on `st` when it goes out of scope (any return path of a call
+// that may have enqueued launches touching handle scratch), so a later call on another stream
+// orders after them; finish() does it explicitly and reports a failure to record.
+struct ScratchRecord {
+    dsx_handle *h;
+    hipStream_t st;
+    bool active;
+    ScratchRecord(dsx_handle *h_, hipStream_t st_, bool active_) : h(h_), st(st_), active(active_) {}
+    int record() {
+        active = false;
+        if (!h->scratchDone) {
+            hipError_t e = hipEventCreateWithFlags(&h->scratchDone, hipEventDisableTiming);
+            if (e != hipSuccess) return fail(DSX_EHIP, std::string("hipEventCreate: ") + hipGetErrorString(e));
+        }
+        hipError_t e = hipEventRecord(h->scratchDone, st);
+        if (e != hipSuccess) return fail(DSX_EHIP, std::string("hipEventRecord: ") + hipGetErrorString(e));
+        h->scratchStream = st;
+        h->scratchPending = true;
+        return DSX_OK;
+    }
+    int finish() { return active ? record() : DSX_OK; }
+    ~ScratchRecord() {
+        if (active) (void)record();
+    }
+};
+
 dsx::Bm2Args base_args(dsx_handle *h, int H, int W, int64_t stride) {
     dsx::Bm2Args a{};
     a.stride = stride;
@@ -382,6 +416,30 @@ dsx::Bm2Args base_args(dsx_handle *h, int H, int W, int64_t stride) {
         }                                                                \
     } while (0)
 
+// The handle's per-kernel timing around the post-processing launch groups (launch_post_full).
+struct TimingHook : dsx::LaunchHook {
+    dsx_handle *h;
+    TimedLaunch t{};
+    int rc = DSX_OK;
+    bool open = false;
+    explicit TimingHook(dsx_handle *h_) : h(h_) {}
+    void before(const char *name, hipStream_t st) override {
+        if (rc == DSX_OK) rc = begin_timed(h, name, st, t);
+        open = rc == DSX_OK;
+    }
+    void after(hipStream_t st) override {
+        if (open && rc == DSX_OK) rc = end_timed(h, st, t);
+        open = false;
+    }
+};
+
+int sticky_inpaint_timeout() {
+    if (dsx::inpaint_take_timeout())
+        return fail(DSX_EHIP, "hole filling: a grid barrier of the persistent march timed out; the holes of that "
+                              "call were left unfilled (its results are invalid)");
+    return DSX_OK;
+}
+
 int run_right_pass(dsx_handle *h, const void *dL, const void *dR, int H, int W, int64_t stride, int16_t *out,
                    hipStream_t st) {
     if (h->p.cost == DSX_COST_BT) return fail(DSX_EINVAL, "the right-view map is a block-matching (SAD/SSD) pass");
@@ -406,6 +464,7 @@ int run(dsx_handle *h, const void *dL, const void *dR, int H, int W, int64_t str
     const bool fused = h->p.path == DSX_PATH_FUSED && !h->p.aggregation && !bt && h->p.lr_form == DSX_LR_FORM_BM;
     const bool scratch = h->p.disp12_max_diff >= 0 || !fused || h->p.sgbm_post;
     if (scratch && h->scratchPending && h->scratchStream != st) DSX_HIP(hipStreamWaitEvent(st, h->scratchDone, 0));
+    ScratchRecord rec_(h, st, scratch);  // on every exit once launches may have been enqueued
     if (h->p.sgbm_post) {
         outFixed = h->postIn;
         outFloat = nullptr;
@@ -584,13 +643,7 @@ int run(dsx_handle *h, const void *dL, const void *dR, int H, int W, int64_t str
                                              st));
         }
     }
-    if (scratch) {
-        if (!h->scratchDone) DSX_HIP(hipEventCreateWithFlags(&h->scratchDone, hipEventDisableTiming));
-        DSX_HIP(hipEventRecord(h->scratchDone, st));
-        h->scratchStream = st;
-        h->scratchPending = true;
-    }
-    return DSX_OK;
+    return rec_.finish();
 }
 
 int check_shape(int H, int W, int64_t stride) {
@@ -757,6 +810,10 @@ int dsx_postprocess_full_ex_device(const void *d_disp, int32_t H, int32_t W, int
     if ((int64_t)H * (W - crop) > 0x7FFFFFFF) return fail(DSX_EINVAL, "image too large for int32 labels");
     if (fill_radius > 0 && W - crop > dsx::kInpaintMaxW)
         return fail(DSX_EINVAL, "image too wide for hole filling (W > 19200)");
+    if (fill_radius > 0) {
+        const int rc = sticky_inpaint_timeout();
+        if (rc) return rc;
+    }
     dsx::PostFullArgs a{};
     a.disp = static_cast<const float *>(d_disp);
     a.in_pitch = in_pitch;
@@ -795,6 +852,8 @@ int dsx_fill_holes_device(const void *d_disp, int32_t H, int32_t W, int64_t in_p
     if (W > dsx::kInpaintMaxW) return fail(DSX_EINVAL, "image too wide for hole filling (W > 19200)");
     if (!d_workspace || workspace_bytes < dsx::inpaint_workspace(H, W))
         return fail(DSX_EINVAL, "workspace too small (dsx_fill_holes_workspace_bytes)");
+    const int rc = sticky_inpaint_timeout();
+    if (rc) return rc;
     DSX_HIP(dsx::launch_inpaint(static_cast<const float *>(d_disp), in_pitch, H, W, radius, static_cast<float *>(d_out),
                                 d_workspace, static_cast<hipStream_t>(hip_stream)));
     return DSX_OK;
@@ -878,6 +937,99 @@ int dsx_compute_host(dsx_handle *h, const uint8_t *L, const uint8_t *R, int32_t 
     if (out_float) DSX_HIP(hipMemcpyAsync(out_float, h->dFloat, (size_t)H * W * 4, hipMemcpyDeviceToHost, st));
     DSX_HIP(hipStreamSynchronize(st));
     return DSX_OK;
+}
+
+int dsx_fill_holes_status(void) {
+    g_err.clear();
+    return sticky_inpaint_timeout();
+}
+
+int dsx_process_pair_device(dsx_handle *h, const void *dL, const void *dR, int32_t H, int32_t W, int64_t stride_bytes,
+                            const dsx_post_params *pp, void *d_out_disp, void *d_out_depth, void *hip_stream) {
+    g_err.clear();
+    if (!h || !pp) return fail(DSX_EINVAL, "NULL handle or post parameters");
+    if (!dL || !dR) return fail(DSX_EINVAL, "input pointers are NULL");
+    int rc = check_shape(H, W, stride_bytes);
+    if (rc) return rc;
+    if (pp->mode != DSX_POST_FAST && pp->mode != DSX_POST_FULL)
+        return fail(DSX_EINVAL, "post mode must be DSX_POST_FAST or DSX_POST_FULL");
+    if (pp->mode == DSX_POST_FULL) {
+        if (pp->outlier_kernel < 1 || (pp->outlier_kernel & 1) == 0) return fail(DSX_EINVAL, "outlier_kernel must be odd");
+        if (pp->fill_radius < 0) return fail(DSX_EINVAL, "fill_radius must be >= 0");
+    }
+    if (h->p.float_mode != DSX_FLOAT_FIXED)
+        return fail(DSX_EINVAL, "process_pair needs float_mode DSX_FLOAT_FIXED (stereo_core.py:232: fixed / 16)");
+    const int crop = std::max(0, h->p.num_disp);  // stereo_core.py:168 crops num_disp columns
+    const int Wc = W - crop;
+    const bool depth = pp->has_depth != 0;
+    if (Wc <= 0 || (!d_out_disp && !(depth && d_out_depth))) return DSX_OK;  // disp[:, num_disp:] is empty
+    if (pp->mode == DSX_POST_FULL && pp->fill_radius > 0) {
+        if (Wc > dsx::kInpaintMaxW) return fail(DSX_EINVAL, "image too wide for hole filling (W > 19200)");
+        rc = sticky_inpaint_timeout();
+        if (rc) return rc;
+    }
+    DSX_HIP(hipSetDevice(h->device));
+    rc = ensure_buffers(h, H, W, false);
+    if (rc) return rc;
+    const size_t n = (size_t)H * W;
+    if (!h->ppDisp) DSX_HIP(hipMalloc(&h->ppDisp, n * 4));
+    const size_t wsb = dsx::post_full_workspace(H, W, crop);
+    if (pp->mode == DSX_POST_FULL && h->ppWsBytes < wsb) {
+        (void)hipFree(h->ppWs);
+        h->ppWs = nullptr;
+        h->ppWsBytes = 0;
+        DSX_HIP(hipMalloc(&h->ppWs, wsb));
+        h->ppWsBytes = wsb;
+    }
+    hipStream_t st = static_cast<hipStream_t>(hip_stream);
+    // the float map and the workspace are handle scratch: order after the previous call's use
+    if (h->scratchPending && h->scratchStream != st) DSX_HIP(hipStreamWaitEvent(st, h->scratchDone, 0));
+    ScratchRecord rec_(h, st, true);
+    rc = run(h, dL, dR, H, W, stride_bytes, nullptr, h->ppDisp, st);
+    if (rc) return rc;
+    rec_.active = true;  // run() recorded its own event; this call's kernels continue below
+    const float fB = (float)(pp->focal_length * pp->baseline);
+    if (pp->mode == DSX_POST_FULL) {
+        dsx::PostFullArgs a{};
+        a.disp = h->ppDisp;
+        a.in_pitch = W;
+        a.H = H;
+        a.W = W;
+        a.crop = crop;
+        a.max_speckle = pp->max_speckle_size;
+        a.max_diff16 = (int)(pp->max_diff * 16);  // int(max_diff * 16), postprocess.py:30
+        a.apply_outliers = pp->apply_outlier_removal ? 1 : 0;
+        a.kernel = pp->outlier_kernel;
+        a.thr = (float)pp->outlier_threshold;
+        a.out_disp = static_cast<float *>(d_out_disp);
+        a.out_depth = depth ? static_cast<float *>(d_out_depth) : nullptr;
+        a.fB = fB;
+        a.doffs = (float)pp->doffs;
+        a.eps = (float)pp->eps;
+        a.max_depth = (float)pp->max_depth;
+        a.has_max = pp->has_max_depth ? 1 : 0;
+        a.fill_radius = pp->fill_radius;
+        TimingHook hook(h);
+        hipError_t e = dsx::launch_post_full(a, h->ppWs, st, h->p.timing ? &hook : nullptr);
+        if (e != hipSuccess) return fail(DSX_EHIP, std::string("post-processing launch: ") + hipGetErrorString(e));
+        if (hook.rc) return hook.rc;
+    } else {
+        dsx::PostArgs a{};
+        a.disp = h->ppDisp;
+        a.in_pitch = W;
+        a.H = H;
+        a.W = W;
+        a.crop = crop;
+        a.out_disp = static_cast<float *>(d_out_disp);
+        a.out_depth = depth ? static_cast<float *>(d_out_depth) : nullptr;
+        a.fB = fB;
+        a.doffs = (float)pp->doffs;
+        a.eps = (float)pp->eps;
+        a.max_depth = (float)pp->max_depth;
+        a.has_max = pp->has_max_depth ? 1 : 0;
+        DSX_LAUNCH(h, "median_depth", st, dsx::launch_post_fast(a, st));
+    }
+    return rec_.finish();
 }
 
 int dsx_kernel_times(dsx_handle *h, char *names, int names_cap, float *ms, int *counts, int cap, int *n) {

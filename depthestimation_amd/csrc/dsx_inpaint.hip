@@ -32,6 +32,7 @@
 
 #include <algorithm>
 #include <cstdlib>
+#include <mutex>
 
 namespace dsx {
 
@@ -478,7 +479,8 @@ __global__ __launch_bounds__(256) void inp_layer(float *out, const int *layer, d
 // pollers never contend with the arrivals.  Then an acquire (invalidates this CU's caches) before any
 // wave reads pixels other blocks wrote.  Spins are bounded: on a timeout the block sets the timeout
 // word and every block leaves the march.
-__device__ __forceinline__ bool grid_barrier(unsigned *ctr, unsigned *gen, unsigned epoch, unsigned nblk, int *tmo) {
+__device__ __forceinline__ bool grid_barrier(unsigned *ctr, unsigned *gen, unsigned epoch, unsigned nblk, int *tmo,
+                                             unsigned spin_limit) {
     __shared__ int ok;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
@@ -493,8 +495,8 @@ __device__ __forceinline__ bool grid_barrier(unsigned *ctr, unsigned *gen, unsig
         } else {
             for (unsigned spins = 0; __hip_atomic_load(gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < epoch; ++spins) {
                 __builtin_amdgcn_s_sleep(1);
-                if ((spins & 255u) == 255u &&
-                    (spins > (1u << 23) || __hip_atomic_load(tmo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))) {
+                if (spins > spin_limit ||
+                    ((spins & 255u) == 255u && __hip_atomic_load(tmo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))) {
                     __hip_atomic_store(tmo, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     good = 0;
                     break;
@@ -509,11 +511,15 @@ __device__ __forceinline__ bool grid_barrier(unsigned *ctr, unsigned *gen, unsig
     return ok;
 }
 
-// Layers k0..K in one persistent launch (grid = one block per CU, all resident), a grid barrier
-// between layers.  Exits at once when the per-layer launches already reached K.
+// Layers k0..K in one persistent launch (a cooperative launch of one block per CU: the runtime
+// refuses it unless every block is co-resident), a grid barrier between layers.  Exits at once
+// when the per-layer launches already reached K.  A barrier that times out (spin_limit) leaves the
+// remaining layers unfilled; the block that saw it raises the sticky flag in mapped host memory
+// (htmo), which the next hole-filling call and dsx_fill_holes_status() report as an error.
 template <int G>
 __global__ __launch_bounds__(256) void inp_rest(float *out, const int *layer, double *T, int H, int W, int radius,
-                                                int k0, const int *list, const int *off, int *ctl) {
+                                                int k0, const int *list, const int *off, int *ctl, int *htmo,
+                                                unsigned spin_limit) {
     const int K = ctl[kCtlK];
     if (k0 > K) return;  // grid-uniform
     unsigned epoch = 0;
@@ -522,8 +528,10 @@ __global__ __launch_bounds__(256) void inp_rest(float *out, const int *layer, do
         if (k == K) break;
         ++epoch;
         if (!grid_barrier(reinterpret_cast<unsigned *>(ctl + kCtlBar), reinterpret_cast<unsigned *>(ctl + kCtlGen), epoch,
-                          gridDim.x, ctl + kCtlTmo))
+                          gridDim.x, ctl + kCtlTmo, spin_limit)) {
+            if (threadIdx.x == 0 && htmo) __hip_atomic_store(htmo, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             return;
+        }
     }
 }
 
@@ -566,16 +574,38 @@ Views views(void *ws, int H, int W) {
     return v;
 }
 
-// The deepest layer of the previous call (any device / stream): the device writes it into mapped
-// host memory; it only sizes the next call's run of per-layer launches.
-int *lastk_host() {
+// Mapped host words shared by every device / stream: [0] the deepest layer of the previous call
+// (written by the device; it only sizes the next call's run of per-layer launches), [16] the sticky
+// grid-barrier timeout flag of inp_rest (own cache line).
+constexpr int kHostLastK = 0, kHostTmo = 16;
+int *host_words() {
     static int *p = [] {
         int *h = nullptr;
-        if (hipHostMalloc(&h, 64, hipHostMallocMapped | hipHostMallocPortable) != hipSuccess) return (int *)nullptr;
-        *h = -1;
+        if (hipHostMalloc(&h, 128, hipHostMallocMapped | hipHostMallocPortable) != hipSuccess) return (int *)nullptr;
+        h[kHostLastK] = -1;
+        h[kHostTmo] = 0;
         return h;
     }();
     return p;
+}
+
+// per-device constants, set once (thread-per-GPU callers may race here)
+struct DeviceInfo {
+    int ncu = 0;
+    hipError_t err = hipSuccess;
+};
+DeviceInfo &device_info(int dev) {
+    static std::once_flag once[64];
+    static DeviceInfo info[64];
+    std::call_once(once[dev], [dev] {
+        DeviceInfo &d = info[dev];
+        int c = 0;
+        d.err = hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev);
+        if (d.err == hipSuccess)
+            d.err = hipFuncSetAttribute((const void *)inp_rows, hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024);
+        d.ncu = c > 0 ? c : 1;
+    });
+    return info[dev];
 }
 
 }  // namespace
@@ -591,21 +621,15 @@ hipError_t launch_inpaint(const float *in, int64_t pitch, int H, int W, int radi
     const Views v = views(ws, H, W);
     hipError_t e;
     if (W > kInpaintMaxW) return hipErrorInvalidValue;  // the row kernel stages a row in LDS
-    static bool attr[64] = {};
-    {
-        int dev = 0;
-        if ((e = hipGetDevice(&dev)) != hipSuccess) return e;
-        if (dev >= 0 && dev < 64 && !attr[dev]) {
-            if ((e = hipFuncSetAttribute((const void *)inp_rows, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                         150 * 1024)) != hipSuccess)
-                return e;
-            attr[dev] = true;
-        }
-    }
+    int dev = 0;
+    if ((e = hipGetDevice(&dev)) != hipSuccess) return e;
+    if (dev < 0 || dev >= 64) return hipErrorInvalidDevice;
+    const DeviceInfo &di = device_info(dev);
+    if (di.err != hipSuccess) return di.err;
     hipLaunchKernelGGL(inp_rows, dim3(H), dim3(256), (size_t)W * 8, st, in, pitch, H, W, out, v.g, v.cnt, v.ncnt, v.ctl);
     if ((e = dbg_sync("inp_rows", st)) != hipSuccess) return e;
     if (radius < 1) return hipSuccess;  // no neighbourhood: nothing changes (cv2 uses radius >= 1)
-    int *hk = lastk_host();
+    int *hk = host_words();
     int *hk_dev = nullptr;
     if (hk && hipHostGetDevicePointer(reinterpret_cast<void **>(&hk_dev), hk, 0) != hipSuccess) hk_dev = nullptr;
     const int SL = (H + kColS - 1) / kColS;
@@ -633,23 +657,34 @@ hipError_t launch_inpaint(const float *in, int64_t pitch, int H, int W, int radi
         if ((e = dbg_sync("inp_layer", st)) != hipSuccess) return e;
     }
     if (L0 < maxk) {
-        static int ncu[64] = {};
-        int dev = 0;
-        if ((e = hipGetDevice(&dev)) != hipSuccess) return e;
-        if (dev < 0 || dev >= 64) return hipErrorInvalidDevice;
-        if (!ncu[dev]) {
-            int c = 0;
-            if ((e = hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev)) != hipSuccess) return e;
-            ncu[dev] = c > 0 ? c : 1;
-        }
         auto rest = np == 8 ? inp_rest<8> : np == 16 ? inp_rest<16> : inp_rest<0>;
-        int rb = ncu[dev];
-        if (const char *fb = getenv("DSX_INPAINT_RB")) rb = std::max(1, std::min(ncu[dev], atoi(fb)));  // experiments
-        hipLaunchKernelGGL(rest, dim3(rb), dim3(256), 0, st, out, v.layer, v.T, H, W, radius, L0 + 1, v.list, v.off,
-                           v.ctl);
+        int rb = di.ncu;
+        if (const char *fb = getenv("DSX_INPAINT_RB")) rb = std::max(1, std::min(di.ncu, atoi(fb)));  // experiments
+        // barrier spin bound (polls with s_sleep 1); DSX_INPAINT_SPINS lowers it for the timeout test
+        const char *sp = getenv("DSX_INPAINT_SPINS");
+        const unsigned spins = sp ? (unsigned)strtoul(sp, nullptr, 10) : (1u << 23);
+        int *htmo = nullptr;
+        if (hk && hipHostGetDevicePointer(reinterpret_cast<void **>(&htmo), hk, 0) == hipSuccess) htmo += kHostTmo;
+        int k0 = L0 + 1;
+        float *o = out;
+        const int *lyr = v.layer, *lst = v.list, *of = v.off;
+        double *Tp = v.T;
+        int Hh = H, Ww = W, rad = radius;
+        int *ctl = v.ctl;
+        unsigned sl = spins;
+        void *args[] = {&o, &lyr, &Tp, &Hh, &Ww, &rad, &k0, &lst, &of, &ctl, &htmo, &sl};
+        if ((e = hipLaunchCooperativeKernel(reinterpret_cast<const void *>(rest), dim3(rb), dim3(256), args, 0, st)) !=
+            hipSuccess)
+            return e;
         if ((e = dbg_sync("inp_rest", st)) != hipSuccess) return e;
     }
     return hipSuccess;
+}
+
+// 1 if a persistent march timed out since the last call (and clears the flag), else 0
+int inpaint_take_timeout() {
+    int *h = host_words();
+    return h ? __atomic_exchange_n(h + kHostTmo, 0, __ATOMIC_ACQ_REL) : 0;
 }
 
 }  // namespace dsx

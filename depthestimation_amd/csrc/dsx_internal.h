@@ -154,21 +154,37 @@ struct PostFullArgs {
     const int16_t *in16;
     int newv;
     int16_t *out16;
+    // two-launch form (spk_tile + post_tail2): per-pixel codes and the per-tile pending-node pool
+    int *code, *pool;
+    // diagnostics (DSX_POST_TIMELINE): per block 16 u64 - s_memrealtime after each phase, hw / xcc id
+    uint64_t *tl_tile, *tl_tail;
 };
 size_t post_full_workspace(int H, int W, int crop);
+// Optional per-launch hook (the handle's HIP-event timing of dsx_process_pair_device): before(name)
+// right before a launch group, after() right after it.
+struct LaunchHook {
+    virtual void before(const char *name, hipStream_t st) = 0;
+    virtual void after(hipStream_t st) = 0;
+    virtual ~LaunchHook() = default;
+};
 // cv2.StereoSGBM::compute's own tail on an int16 x16 map: 3x3 median (BORDER_REPLICATE), then
 // filterSpeckles(newVal, maxSpeckleSize, maxDiff) when max_speckle > 0.  Writes out16 and / or
 // outf (= out16 / 16); `in` must not alias the outputs.
 size_t sgbm_post_workspace(int H, int W);
 hipError_t launch_sgbm_post(const int16_t *in, int H, int W, int newv, int max_speckle, int max_diff16, int16_t *out16,
                             float *outf, void *ws, hipStream_t st);
-hipError_t launch_post_full(PostFullArgs a, void *ws, hipStream_t st);
+hipError_t launch_post_full(PostFullArgs a, void *ws, hipStream_t st, LaunchHook *hook = nullptr);
+// true when launch_post_full runs the two-launch speckle form (else the four-launch union-find)
+bool post_full_two_launch(const PostFullArgs &a);
 
 // Hole filling (dsx_inpaint.hip): fill_holes(method='inpaint') on d <= 0, layered Telea marching.
 // Asynchronous: nothing is read back to the host.
 size_t inpaint_workspace(int H, int W);
 constexpr int kInpaintMaxW = 19200;  // the row pass stages a row (8 B / px) in LDS
 hipError_t launch_inpaint(const float *in, int64_t pitch, int H, int W, int radius, float *out, void *ws, hipStream_t st);
+// 1 if a persistent march (inp_rest) timed out in a grid barrier since the last call - its remaining
+// layers stayed unfilled - and clears the flag; else 0
+int inpaint_take_timeout();
 
 // Birchfield-Tomasi block costs into K1's volume layout (dsx_bt.hip, oracle/bt_cost.py)
 struct BtArgs {

@@ -9,6 +9,9 @@
 #include "dsx_internal.h"
 
 #include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
 
 namespace dsx {
 
@@ -422,16 +425,424 @@ __global__ __launch_bounds__(kTailTX *kTailTY) void post_tail(PostFullArgs a) {
     }
 }
 
-#pragma clang fp contract(on)
+// ---------------------------------------------------------------------------------------------
+// F2 in two launches (round 4).  The four-launch form above pays a global union-find for every
+// component and a three-deep dependent gather per pixel in its tail.  Most components never need
+// the global step: a component that does not leave its tile through a joining edge has its exact
+// size in the tile, and one with more than max_speckle pixels inside the tile is large whatever lies
+// outside.  Only the rest - "pending" pieces of <= max_speckle pixels with a joining edge into a
+// neighbour tile (0.4-1 % of the pixels of the C2 / C4 matcher maps) - depend on other tiles.
+//
+//  spk_tile    one 64 x 16 tile per block.  d16 = int16(trunc(d * 16)); the horizontal runs of a row
+//              come from one ballot (run starts = pixels without a joining left edge), so the LDS
+//              union-find only links runs vertically (one union per run pair), sizes are added per
+//              run.  A 1-pixel ring around the tile tells which components leave it.  Decided pixels
+//              get their final x16 value in code[p]; a pending piece gets a node in the tile's pool
+//              region {size, edge count, the outside pixel of each cross edge (one per border run)}
+//              and its pixels get code = kPend | node offset.
+//  post_tail2  post_tail on the codes: a pending node's fate comes from a breadth-first search of
+//              one wave over the pending-node graph (edges name outside pixels; an outside pixel with
+//              a decided code belongs to a large piece, so the component is large).  It stops as soon
+//              as the pieces seen can hold more than max_speckle pixels, so its visited list needs at
+//              most max_speckle + 1 entries.  On the C2 / C4 maps a search pops 1.5 pieces on average.
+// ---------------------------------------------------------------------------------------------
+constexpr int kSpTX = 64, kSpTY = 16, kSpN = kSpTX * kSpTY;
+// pool ints per tile: pending roots have a border pixel (<= 2*64 + 2*14 = 156), 2 header ints each,
+// plus at most one edge per border pixel side (64 + 64 + 16 + 16 = 160): <= 472
+constexpr int kSpPool = 512;
+constexpr int kPend = 0x40000000;  // codes >= kPend are pending nodes; decided codes are int16 values
+constexpr int kOpen = 1 << 20;     // tile component size word: leaves the tile (sizes <= 1024)
+constexpr int kBfsMaxSpeckle = 2047;  // visited lists of 4 waves x (max + 1) ints in LDS
+constexpr int kHash = 1024;           // pending-node table of a tail block (>= 2x its 16 x 40 region)
 
-size_t post_full_workspace(int H, int W, int crop) {
-    const size_t n = (size_t)H * (size_t)(W > crop ? W - crop : 0);
-    const auto r = [](size_t b) { return (b + 255) & ~(size_t)255; };
-    // parent, count, root, lsz | v16 | t0, t1 | hole filling
-    return r(n * 4) * 4 + r(n * 2) + r(n * 4) * 2 + inpaint_workspace(H, W > crop ? W - crop : 0);
+__device__ __forceinline__ int spk_val(const PostFullArgs &a, int Wc, int y, int x) {
+    if (y < 0 || y >= a.H || x < 0 || x >= Wc) return a.newv;
+    const int64_t q = (int64_t)y * a.in_pitch + a.crop + x;
+    if (a.in16) return a.in16[q];
+    return (int16_t)(int)__builtin_truncf(a.disp[q] * 16.0f);
 }
 
-hipError_t launch_post_full(PostFullArgs a, void *ws, hipStream_t st) {
+// DSX_POST_TIMELINE diagnostics: thread 0 stamps the 100 MHz real-time counter after phase `i`
+__device__ __forceinline__ void pstamp(uint64_t *tl, int i) {
+    if (tl && threadIdx.x == 0) {
+        const int b = blockIdx.y * gridDim.x + blockIdx.x;
+        tl[16 * b + i] = __builtin_amdgcn_s_memrealtime();
+        if (i == 0) {
+            tl[16 * b + 14] = (uint64_t)__builtin_amdgcn_s_getreg((4 << 0) | (0 << 6) | (31 << 11));   // HW_ID
+            tl[16 * b + 15] = (uint64_t)__builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (15 << 11));  // XCC_ID
+        }
+    }
+}
+
+__global__ __launch_bounds__(256) void spk_tile(PostFullArgs a) {
+    __shared__ int16_t vl[kSpN];   // d16
+    __shared__ int16_t lb[kSpN];   // run start (local index) of each pixel
+    __shared__ int16_t rt[kSpN];   // component root (local index), -1 for newv pixels
+    __shared__ int pl[kSpN];       // union-find parents of run starts; later the roots' pool offsets
+    __shared__ int cnt[kSpN];      // size | kOpen at roots
+    __shared__ int ecn[kSpN];      // pending roots: cross edges kept
+    __shared__ int16_t rg_t[kSpTX], rg_b[kSpTX], rg_l[kSpTY], rg_r[kSpTY];
+    __shared__ int used;
+    const int Wc = a.W - a.crop, H = a.H;
+    const int md = a.max_diff16, nv = a.newv, maxsp = a.max_speckle;
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int x0 = blockIdx.x * kSpTX, y0 = blockIdx.y * kSpTY;
+    const int gx = x0 + lane;
+    const int tbase = (blockIdx.y * gridDim.x + blockIdx.x) * kSpPool;
+    pstamp(a.tl_tile, 0);
+    int v[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) v[i] = spk_val(a, Wc, y0 + 4 * w + i, gx);
+    if (w == 0) {
+        rg_t[lane] = (int16_t)spk_val(a, Wc, y0 - 1, gx);
+    } else if (w == 1) {
+        rg_b[lane] = (int16_t)spk_val(a, Wc, y0 + kSpTY, gx);
+    } else if (w == 2) {
+        if (lane < kSpTY) rg_l[lane] = (int16_t)spk_val(a, Wc, y0 + lane, x0 - 1);
+    } else {
+        if (lane < kSpTY) rg_r[lane] = (int16_t)spk_val(a, Wc, y0 + lane, x0 + kSpTX);
+    }
+    if (threadIdx.x == 0) used = 0;
+    const uint64_t le = lane == 63 ? ~0ull : ((2ull << lane) - 1ull);  // lanes <= this one
+    uint64_t S[4];
+    int lab[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int r = 4 * w + i, li = r * kSpTX + lane;
+        const int left = __shfl_up(v[i], 1);
+        const bool hj = lane > 0 && joins(left, v[i], md, nv);
+        S[i] = __ballot(!hj);
+        lab[i] = r * kSpTX + 63 - __clzll((long long)(S[i] & le));
+        vl[li] = (int16_t)v[i];
+        lb[li] = (int16_t)lab[i];
+        pl[li] = lab[i];
+        cnt[li] = 0;
+        ecn[li] = 0;
+    }
+    __syncthreads();
+    pstamp(a.tl_tile, 1);
+    // vertical joins: one union per (run below, run above) pair (the first column of the pair)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int r = 4 * w + i;
+        if (r == 0) continue;
+        const int up = vl[(r - 1) * kSpTX + lane];
+        const int ul = lb[(r - 1) * kSpTX + lane];
+        const bool vj = joins(up, v[i], md, nv);
+        const int pvj = __shfl_up((int)vj, 1), pla = __shfl_up(lab[i], 1), pul = __shfl_up(ul, 1);
+        const bool dup = lane > 0 && pvj && pla == lab[i] && pul == ul;
+        if (vj && !dup) ufl_unite(pl, lab[i], ul);
+    }
+    __syncthreads();
+    pstamp(a.tl_tile, 2);
+    int root[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int r = 4 * w + i;
+        const bool start = (S[i] >> lane) & 1ull;
+        const bool live = v[i] != nv;
+        int rr = -1;
+        if (start && live) rr = ufl_find(pl, lab[i]);
+        rr = __shfl(rr, lab[i] - r * kSpTX);  // the run start's root
+        if (!live) rr = -1;
+        root[i] = rr;
+        rt[r * kSpTX + lane] = (int16_t)rr;
+        if (start && live) {
+            const uint64_t above = S[i] & ~le;
+            const int next = above ? __ffsll((long long)above) - 1 : 64;
+            atomicAdd(&cnt[rr], next - lane);  // the run's length
+        }
+    }
+    // components with a joining edge out of the tile
+    {
+        const int vt = w == 0 ? v[0] : v[3], rtb = w == 0 ? root[0] : root[3];
+        if ((w == 0 || w == 3) && rtb >= 0 && joins(vt, w == 0 ? rg_t[lane] : rg_b[lane], md, nv))
+            atomicOr(&cnt[rtb], kOpen);
+        if (lane == 0 || lane == 63) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int r = 4 * w + i;
+                if (root[i] >= 0 && joins(v[i], lane == 0 ? rg_l[r] : rg_r[r], md, nv)) atomicOr(&cnt[root[i]], kOpen);
+            }
+        }
+    }
+    __syncthreads();
+    pstamp(a.tl_tile, 3);
+    const auto pend = [&](int c) { return (c & kOpen) && (c & (kOpen - 1)) <= maxsp; };
+    // cross edges of pending pieces, one per run along a side: an edge is dropped when the previous
+    // pixel along the side has an edge of the same piece and the two outside pixels join (they lie
+    // in one neighbour tile, so they are in one of its pieces)
+    int tbSlot = -1, tbRoot = 0, tbQ = 0;
+    if (w == 0 || w == 3) {
+        const int vt = w == 0 ? v[0] : v[3], rtb = w == 0 ? root[0] : root[3];
+        const int16_t *rg = w == 0 ? rg_t : rg_b;
+        const int ring = rg[lane];
+        const bool e = rtb >= 0 && joins(vt, ring, md, nv);
+        const int pe = __shfl_up((int)e, 1), pr = __shfl_up(rtb, 1);
+        const bool dup = lane > 0 && pe && pr == rtb && joins(rg[lane - (lane > 0)], ring, md, nv);
+        if (e && !dup && pend(cnt[rtb])) {
+            tbSlot = atomicAdd(&ecn[rtb], 1);
+            tbRoot = rtb;
+            tbQ = (w == 0 ? y0 - 1 : y0 + kSpTY) * Wc + gx;
+        }
+    }
+    int sSlot[4], sRoot[4], sQ[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) sSlot[i] = -1, sRoot[i] = 0, sQ[i] = 0;
+    if (lane == 0 || lane == 63) {
+        const int16_t *rg = lane == 0 ? rg_l : rg_r;
+        const int xo = lane == 0 ? x0 - 1 : x0 + kSpTX;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int r = 4 * w + i;
+            const int ring = rg[r];
+            const bool e = root[i] >= 0 && joins(v[i], ring, md, nv);
+            bool dup = false;
+            if (r > 0) {
+                const int pli = (r - 1) * kSpTX + lane;
+                dup = rt[pli] == root[i] && joins(vl[pli], rg[r - 1], md, nv) && joins(rg[r - 1], ring, md, nv);
+            }
+            if (e && !dup && pend(cnt[root[i]])) {
+                sSlot[i] = atomicAdd(&ecn[root[i]], 1);
+                sRoot[i] = root[i];
+                sQ[i] = (y0 + r) * Wc + xo;
+            }
+        }
+    }
+    __syncthreads();
+    pstamp(a.tl_tile, 4);
+    // node records of the pending roots in the tile's pool region
+    for (int li = threadIdx.x; li < kSpN; li += 256) {
+        if (rt[li] == li && pend(cnt[li])) {
+            const int ne = ecn[li];
+            const int off = atomicAdd(&used, 2 + ne);
+            pl[li] = off;
+            a.pool[tbase + off] = cnt[li] & (kOpen - 1);
+            a.pool[tbase + off + 1] = ne;
+        }
+    }
+    __syncthreads();
+    pstamp(a.tl_tile, 5);
+    if (tbSlot >= 0) a.pool[tbase + pl[tbRoot] + 2 + tbSlot] = tbQ;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+        if (sSlot[i] >= 0) a.pool[tbase + pl[sRoot[i]] + 2 + sSlot[i]] = sQ[i];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int y = y0 + 4 * w + i;
+        if (y >= H || gx >= Wc) continue;
+        int c = v[i];
+        if (root[i] >= 0) {
+            const int cn = cnt[root[i]], sz = cn & (kOpen - 1);
+            if (!(cn & kOpen)) {
+                if (sz <= maxsp) c = nv;
+            } else if (sz <= maxsp) {
+                c = kPend | (tbase + pl[root[i]]);
+            }
+        }
+        a.code[(int64_t)y * Wc + gx] = c;
+    }
+    pstamp(a.tl_tile, 7);
+}
+
+// Breadth-first search of one wave over pending pieces from node k0 (a pool offset); true when the
+// component has at most max_speckle pixels.  `vis` holds max_speckle + 1 ints (see above).
+__device__ bool spk_small(const PostFullArgs &a, int k0, int *vis, int lane) {
+    const int maxsp = a.max_speckle;
+    if (lane == 0) vis[0] = k0;
+    int nvis = 1, head = 0, size = 0;
+    while (head < nvis) {
+        const int k = __builtin_amdgcn_readfirstlane(vis[head]);
+        ++head;
+        const int rec = a.pool[k + lane];  // lane 0: piece size, lane 1: edge count, lanes 2..: edges
+        size += __shfl(rec, 0);
+        const int ne = __shfl(rec, 1);
+        if (size + (nvis - head) > maxsp) return false;
+        for (int j0 = 0; j0 < ne; j0 += (j0 == 0 ? 62 : 64)) {
+            int q = -1;
+            if (j0 == 0) {
+                if (lane >= 2 && lane - 2 < ne) q = rec;
+            } else if (j0 + lane < ne) {
+                q = a.pool[k + 2 + j0 + lane];
+            }
+            int h = -1;
+            bool large = false;
+            if (q >= 0) {
+                const int c = a.code[q];
+                if (c < kPend) large = true;  // a decided piece with a joining edge: more than max pixels
+                else h = c - kPend;
+            }
+            if (__ballot(large)) return false;
+            while (true) {
+                const uint64_t m = __ballot(h >= 0);
+                if (!m) break;
+                const int u = __shfl(h, __ffsll((long long)m) - 1);
+                if (h == u) h = -1;
+                bool seen = false;
+                for (int j = lane; j < nvis; j += 64) seen |= vis[j] == u;
+                if (!__ballot(seen)) {
+                    if (lane == 0) vis[nvis] = u;
+                    ++nvis;
+                    if (size + (nvis - head) > maxsp) return false;  // every piece has >= 1 pixel
+                }
+            }
+        }
+    }
+    return true;
+}
+
+// post_tail on spk_tile's codes (outlier kernel k <= 7); dynamic LDS: 4 x (max_speckle + 1) ints
+__global__ __launch_bounds__(kTailTX *kTailTY) void post_tail2(PostFullArgs a) {
+    __shared__ float t0[kT0H][kT0W];
+    __shared__ double rs[kT0H][kT1W], rs2[kT0H][kT1W];
+    __shared__ float t1[kT1H][kT1W];
+    __shared__ int pk[kT0H * kT0W];  // pending entries of the region: node, then its table slot
+    __shared__ int hkey[kHash];
+    __shared__ int8_t hres[kHash];
+    extern __shared__ int vis[];
+    const int Wc = a.W - a.crop, H = a.H;
+    const int r = a.kernel / 2;
+    const int x0 = blockIdx.x * kTailTX, y0 = blockIdx.y * kTailTY;
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    const int th0 = kTailTY + 2 + 2 * r, tw0 = kTailTX + 2 + 2 * r;
+    pstamp(a.tl_tail, 0);
+    for (int q = tid; q < kHash; q += kTailTX * kTailTY) hkey[q] = -1;
+    int anyp = 0;
+    for (int q = tid; q < th0 * tw0; q += kTailTX * kTailTY) {
+        const int ty = q / tw0, tx = q - ty * tw0;
+        const int yy = reflect101(y0 - 1 - r + ty, H), xx = reflect101(x0 - 1 - r + tx, Wc);
+        const int c = a.code[(int64_t)yy * Wc + xx];
+        if (c >= kPend) {
+            pk[q] = c - kPend;
+            anyp = 1;
+        } else {
+            pk[q] = -1;
+            t0[ty][tx] = (float)c / 16.0f;
+        }
+    }
+    const int anyb = __syncthreads_or(anyp);
+    pstamp(a.tl_tail, 1);
+    if (anyb) {
+        for (int q = tid; q < th0 * tw0; q += kTailTX * kTailTY) {
+            const int key = pk[q];
+            if (key < 0) continue;
+            int h = (int)(((unsigned)key * 2654435761u) >> 22);
+            while (true) {
+                const int old = atomicCAS(&hkey[h], -1, key);
+                if (old == -1 || old == key) break;
+                h = (h + 1) & (kHash - 1);
+            }
+            pk[q] = h;
+        }
+        __syncthreads();
+        int *wvis = vis + wave * (a.max_speckle + 1);
+        for (int j0 = wave * 64; j0 < kHash; j0 += 256) {
+            const int key = hkey[j0 + lane];
+            uint64_t m = __ballot(key >= 0);
+            while (m) {
+                const int b = __ffsll((long long)m) - 1;
+                m &= m - 1;
+                const bool sm = spk_small(a, __shfl(key, b), wvis, lane);
+                if (lane == 0) hres[j0 + b] = sm ? 1 : 0;
+            }
+        }
+        __syncthreads();
+        for (int q = tid; q < th0 * tw0; q += kTailTX * kTailTY) {
+            const int slot = pk[q];
+            if (slot < 0) continue;
+            const int ty = q / tw0, tx = q - ty * tw0;
+            const int yy = reflect101(y0 - 1 - r + ty, H), xx = reflect101(x0 - 1 - r + tx, Wc);
+            const int v = hres[slot] ? a.newv : spk_val(a, Wc, yy, xx);
+            t0[ty][tx] = (float)v / 16.0f;
+        }
+    }
+    __syncthreads();
+    pstamp(a.tl_tail, 2);
+    const bool outl = a.apply_outliers != 0;
+    if (outl) {
+        for (int q = tid; q < th0 * kT1W; q += kTailTX * kTailTY) {
+            const int ty = q / kT1W, c = q - ty * kT1W;
+            double s = 0.0, s2 = 0.0;
+            for (int i = 0; i <= 2 * r; ++i) {
+                const float v = t0[ty][c + i];
+                s += (double)v;
+                s2 += (double)(v * v);
+            }
+            rs[ty][c] = s;
+            rs2[ty][c] = s2;
+        }
+        __syncthreads();
+    }
+    pstamp(a.tl_tail, 3);
+    const double scale = 1.0 / (double)(a.kernel * a.kernel);
+    for (int q = tid; q < kT1H * kT1W; q += kTailTX * kTailTY) {
+        const int ty = q / kT1W, c = q - ty * kT1W;
+        const float d = t0[ty + r][c + r];
+        float v = d;
+        if (outl) {
+            double s = 0.0, s2 = 0.0;
+            for (int j = 0; j <= 2 * r; ++j) {
+                s += rs[ty + j][c];
+                s2 += rs2[ty + j][c];
+            }
+            const float mean = (float)(s * scale), msq = (float)(s2 * scale);
+            const float var = msq - mean * mean;
+            const float sd = sqrtf(var > 0.0f ? var : 0.0f);
+            if (d > 0.0f && fabsf(d - mean) > a.thr * sd) v = 0.0f;
+        }
+        t1[ty][c] = v;
+    }
+    __syncthreads();
+    pstamp(a.tl_tail, 4);
+    const int lx = tid % kTailTX, ly = tid / kTailTX;
+    const int x = x0 + lx, y = y0 + ly;
+    if (tid == 0) pstamp(a.tl_tail, 5);  // (thread 0 stamps before it may leave)
+    if (x >= Wc || y >= H) return;
+    if (a.tail_t1) {
+        a.t1[(int64_t)y * Wc + x] = t1[ly + 1][lx + 1];
+        return;
+    }
+    auto tap = [&](int dy, int dx) __attribute__((always_inline)) -> float {
+        const int yy = min(max(y + dy, 0), H - 1), xx = min(max(x + dx, 0), Wc - 1);
+        return t1[yy - (y0 - 1)][xx - (x0 - 1)];
+    };
+    const float med = median9(tap(-1, -1), tap(-1, 0), tap(-1, 1), tap(0, -1), tap(0, 0), tap(0, 1), tap(1, -1),
+                              tap(1, 0), tap(1, 1));
+    const int64_t o = (int64_t)y * Wc + x;
+    if (a.out_disp) a.out_disp[o] = med;
+    if (a.out_depth) {
+        const float adj = med + a.doffs;
+        float z = adj > a.eps ? __fdiv_rn(a.fB, adj) : __builtin_inff();
+        if (a.has_max && z > a.max_depth) z = a.max_depth;
+        a.out_depth[o] = z;
+    }
+    pstamp(a.tl_tail, 6);
+}
+
+#pragma clang fp contract(on)
+
+namespace {
+size_t spk_pool_ints(int H, int Wc) {
+    const size_t tiles = (size_t)((Wc + kSpTX - 1) / kSpTX) * (size_t)((H + kSpTY - 1) / kSpTY);
+    return tiles * kSpPool + 64;  // + one wave's read past the last record (spk_small)
+}
+}  // namespace
+
+bool post_full_two_launch(const PostFullArgs &a) {
+    const int Wc = a.W - a.crop;
+    return a.kernel / 2 <= kTailR && a.max_speckle <= kBfsMaxSpeckle && !a.in16 && a.newv == 0 &&
+           spk_pool_ints(a.H, Wc) < (size_t)kPend && getenv("DSX_POST_LEGACY") == nullptr;
+}
+
+size_t post_full_workspace(int H, int W, int crop) {
+    const int Wc = W > crop ? W - crop : 0;
+    const size_t n = (size_t)H * (size_t)Wc;
+    const auto r = [](size_t b) { return (b + 255) & ~(size_t)255; };
+    // parent, count, root, lsz | v16 | t0, t1 | code | pool | hole filling
+    return r(n * 4) * 4 + r(n * 2) + r(n * 4) * 2 + r(n * 4) + r(spk_pool_ints(H, Wc) * 4) + inpaint_workspace(H, Wc);
+}
+
+hipError_t launch_post_full(PostFullArgs a, void *ws, hipStream_t st, LaunchHook *hook) {
     const int Wc = a.W - a.crop;
     const size_t n = (size_t)a.H * Wc;
     const auto r = [](size_t b) { return (b + 255) & ~(size_t)255; };
@@ -443,37 +854,92 @@ hipError_t launch_post_full(PostFullArgs a, void *ws, hipStream_t st) {
     a.v16 = reinterpret_cast<int16_t *>(w + 4 * r(n * 4));
     a.t0 = reinterpret_cast<float *>(w + 4 * r(n * 4) + r(n * 2));
     a.t1 = reinterpret_cast<float *>(w + 4 * r(n * 4) + r(n * 2) + r(n * 4));
-    const int grid = (int)std::min<size_t>((n + 255) / 256, 4096);
-    const int ntx = (Wc + kCcTX - 1) / kCcTX, nty = (a.H + kCcTY - 1) / kCcTY;
-    hipLaunchKernelGGL(speckle_local, dim3(ntx, nty), dim3(256), 0, st, a);
-    if (ntx > 1 || nty > 1) {
-        const int64_t nb = (int64_t)a.H * (ntx - 1) + (int64_t)(nty - 1) * Wc;
-        hipLaunchKernelGGL(speckle_merge, dim3((unsigned)std::min<int64_t>((nb + 255) / 256, 4096)), dim3(256), 0, st, a,
-                           ntx, nty);
-    }
-    hipLaunchKernelGGL(speckle_resolve, dim3(grid), dim3(256), 0, st, a);
-    const bool fill = a.fill_radius > 0;
-    if (a.kernel / 2 <= kTailR) {
-        a.tail_t1 = fill ? 1 : 0;
-        hipLaunchKernelGGL(post_tail, dim3((Wc + kTailTX - 1) / kTailTX, (a.H + kTailTY - 1) / kTailTY), dim3(kTailTX * kTailTY),
-                           0, st, a);
+    a.code = reinterpret_cast<int *>(w + 4 * r(n * 4) + r(n * 2) + 2 * r(n * 4));
+    a.pool = reinterpret_cast<int *>(w + 4 * r(n * 4) + r(n * 2) + 3 * r(n * 4));
+    uint8_t *inpaint_ws = w + 4 * r(n * 4) + r(n * 2) + 3 * r(n * 4) + r(spk_pool_ints(a.H, Wc) * 4);
+    const auto mark = [&](const char *name) {
+        if (hook) hook->before(name, st);
+    };
+    const auto done = [&]() -> hipError_t {
         hipError_t e = hipGetLastError();
+        if (hook) hook->after(st);
+        return e;
+    };
+    const int grid = (int)std::min<size_t>((n + 255) / 256, 4096);
+    const bool fill = a.fill_radius > 0;
+    if (post_full_two_launch(a)) {
+        const dim3 g1((Wc + kSpTX - 1) / kSpTX, (a.H + kSpTY - 1) / kSpTY);
+        const dim3 g2((Wc + kTailTX - 1) / kTailTX, (a.H + kTailTY - 1) / kTailTY);
+        const char *tlp = getenv("DSX_POST_TIMELINE");  // diagnostics: per-block phase stamps to a file
+        const size_t n1 = (size_t)g1.x * g1.y * 16, n2 = (size_t)g2.x * g2.y * 16;
+        a.tl_tile = a.tl_tail = nullptr;
+        if (tlp && *tlp) {
+            if (hipMalloc(&a.tl_tile, (n1 + n2) * 8) != hipSuccess) return hipErrorOutOfMemory;
+            a.tl_tail = a.tl_tile + n1;
+            if (hipMemsetAsync(a.tl_tile, 0, (n1 + n2) * 8, st) != hipSuccess) return hipErrorUnknown;
+        }
+        mark("speckle_tile");
+        hipLaunchKernelGGL(spk_tile, g1, dim3(256), 0, st, a);
+        hipError_t e = done();
+        if (e != hipSuccess) return e;
+        a.tail_t1 = fill ? 1 : 0;
+        mark("post_tail");
+        hipLaunchKernelGGL(post_tail2, g2, dim3(kTailTX * kTailTY), (size_t)4 * (a.max_speckle + 1) * sizeof(int), st, a);
+        e = done();
+        if (a.tl_tile) {
+            std::vector<uint64_t> host(n1 + n2 + 2);
+            host[0] = (uint64_t)g1.x * g1.y;
+            host[1] = (uint64_t)g2.x * g2.y;
+            if (hipStreamSynchronize(st) == hipSuccess &&
+                hipMemcpy(host.data() + 2, a.tl_tile, (n1 + n2) * 8, hipMemcpyDeviceToHost) == hipSuccess) {
+                if (FILE *f = fopen(tlp, "wb")) {
+                    fwrite(host.data(), 8, host.size(), f);
+                    fclose(f);
+                }
+            }
+            (void)hipFree(a.tl_tile);
+        }
         if (e != hipSuccess || !fill) return e;
+    } else {
+        mark("speckle_legacy");
+        const int ntx = (Wc + kCcTX - 1) / kCcTX, nty = (a.H + kCcTY - 1) / kCcTY;
+        hipLaunchKernelGGL(speckle_local, dim3(ntx, nty), dim3(256), 0, st, a);
+        if (ntx > 1 || nty > 1) {
+            const int64_t nb = (int64_t)a.H * (ntx - 1) + (int64_t)(nty - 1) * Wc;
+            hipLaunchKernelGGL(speckle_merge, dim3((unsigned)std::min<int64_t>((nb + 255) / 256, 4096)), dim3(256), 0, st,
+                               a, ntx, nty);
+        }
+        hipLaunchKernelGGL(speckle_resolve, dim3(grid), dim3(256), 0, st, a);
+        hipError_t e = done();
+        if (e != hipSuccess) return e;
+        if (a.kernel / 2 <= kTailR) {
+            a.tail_t1 = fill ? 1 : 0;
+            mark("post_tail");
+            hipLaunchKernelGGL(post_tail, dim3((Wc + kTailTX - 1) / kTailTX, (a.H + kTailTY - 1) / kTailTY),
+                               dim3(kTailTX * kTailTY), 0, st, a);
+            e = done();
+            if (e != hipSuccess || !fill) return e;
+        }
     }
     const float *med_in = a.t0;
     if (a.kernel / 2 > kTailR) {
+        mark("outliers");
         hipLaunchKernelGGL(speckle_apply, dim3(grid), dim3(256), 0, st, a);
         if (a.apply_outliers) {
             hipLaunchKernelGGL(outliers, dim3(grid), dim3(256), 0, st, a);
             med_in = a.t1;
         }
+        hipError_t e = done();
+        if (e != hipSuccess) return e;
     } else {
         med_in = a.t1;  // post_tail wrote the outlier-cleaned map (fill on)
     }
     if (fill) {
         // fill_holes (postprocess.py:160-166) on the cleaned map: t1 (or t0) -> t0, then the median
         float *dst = med_in == a.t0 ? a.t1 : a.t0;
-        hipError_t e = launch_inpaint(med_in, Wc, a.H, Wc, a.fill_radius, dst, w + 4 * r(n * 4) + r(n * 2) + 2 * r(n * 4), st);
+        mark("fill_holes");
+        hipError_t e = launch_inpaint(med_in, Wc, a.H, Wc, a.fill_radius, dst, inpaint_ws, st);
+        if (hook) hook->after(st);
         if (e != hipSuccess) return e;
         med_in = dst;
     }
@@ -490,7 +956,10 @@ hipError_t launch_post_full(PostFullArgs a, void *ws, hipStream_t st) {
     m.eps = a.eps;
     m.max_depth = a.max_depth;
     m.has_max = a.has_max;
-    return launch_post_fast(m, st);
+    mark("median_depth");
+    hipError_t e = launch_post_fast(m, st);
+    if (hook) hook->after(st);
+    return e;
 }
 
 size_t sgbm_post_workspace(int H, int W) {

@@ -202,6 +202,55 @@ class HipBlockMatcher:
                                                  H, W, left.stride(1), _ptr(out_fixed), _ptr(out_float), sptr)
         _dsx.check(rc, "dsx_compute_batch_device")
 
+    def process_pair_device(self, left, right, fast_mode=False, max_speckle_size=100, max_diff=1.0,
+                            apply_outlier_removal=True, outlier_threshold=2.5, outlier_kernel=5, fill_radius=0,
+                            focal_length=None, baseline=None, doffs=0.0, eps=1e-6, max_depth=None, out_disp=None,
+                            out_depth=None, stream=None):
+        """StereoCore._process_pair (stereo_core.py:162-200) in ONE C-ABI call
+        (dsx_process_pair_device): matcher -> crop [:, num_disp:] -> fast-mode median or
+        postprocess_disparity (speckles, outliers, Telea hole filling when ``fill_radius`` > 0,
+        median) -> depth when focal length and baseline are given.  ``left``/``right``: uint8 HIP
+        tensors H x W (unit column stride, equal row strides).  Returns float32 HIP tensors
+        (disparity H x (W - num_disp), depth or None); asynchronous on ``stream``."""
+        import torch
+        if left.dtype != right.dtype or left.shape != right.shape or left.dim() != 2:
+            raise ValueError("left and right must be uint8 H x W tensors of the same shape")
+        if str(left.dtype) != "torch.uint8" or left.stride(1) != 1 or right.stride(1) != 1 or \
+                left.stride(0) != right.stride(0):
+            raise ValueError("inputs must be uint8 with unit column stride and equal row strides")
+        _check_inputs_on(self.device, left, right)
+        H, W = left.shape
+        Wc = max(W - int(self._cfg["num_disp"]), 0)
+        want_depth = focal_length is not None and baseline is not None
+        if out_disp is None:
+            out_disp = torch.empty((H, Wc), dtype=torch.float32, device=left.device)
+        if want_depth and out_depth is None:
+            out_depth = torch.empty((H, Wc), dtype=torch.float32, device=left.device)
+        _check_out(out_disp, (H, Wc), "torch.float32", self.device, "out_disp")
+        if want_depth:
+            _check_out(out_depth, (H, Wc), "torch.float32", self.device, "out_depth")
+        pp = _dsx.DsxPostParams()
+        pp.mode = _dsx.POST_MODE["fast" if fast_mode else "full"]
+        pp.max_speckle_size = int(max_speckle_size)
+        pp.max_diff = float(max_diff)
+        pp.apply_outlier_removal = int(bool(apply_outlier_removal))
+        pp.outlier_threshold = float(outlier_threshold)
+        pp.outlier_kernel = int(outlier_kernel)
+        pp.fill_radius = int(fill_radius)
+        pp.has_depth = int(want_depth)
+        pp.focal_length = float(focal_length or 0.0)
+        pp.baseline = float(baseline or 0.0)
+        pp.doffs = float(doffs or 0.0)
+        pp.eps = float(eps)
+        pp.max_depth = float(max_depth or 0.0)
+        pp.has_max_depth = int(max_depth is not None)
+        sptr = None if stream is None else (stream if isinstance(stream, int) else stream.cuda_stream)
+        rc = _dsx.lib().dsx_process_pair_device(self._handle(), left.data_ptr(), right.data_ptr(), H, W,
+                                                left.stride(0), ctypes.byref(pp), _ptr(out_disp),
+                                                _ptr(out_depth) if want_depth else None, sptr)
+        _dsx.check(rc, "dsx_process_pair_device")
+        return out_disp, (out_depth if want_depth else None)
+
     def right_map_device(self, left, right, out_dR, stream=None):
         """Right-view winner map dR (int16 H x W, -1 where the search range is empty)."""
         if left.dim() != 2 or left.shape != right.shape or left.stride(0) != right.stride(0):
@@ -342,6 +391,12 @@ def postprocess_full_device(disp, crop, max_speckle_size=50, max_diff=1.0, apply
     _dsx.check(rc, "dsx_postprocess_full_ex_device")
     _keep_until_done(ws, stream)
     return out_disp, out_depth
+
+
+def fill_holes_status():
+    """Raise RuntimeError if a hole-filling call's persistent march timed out since the last check
+    (dsx_fill_holes_status: its remaining holes were left unfilled); the condition is cleared."""
+    _dsx.check(_dsx.lib().dsx_fill_holes_status(), "hole filling")
 
 
 def fill_holes_device(disp, radius=5, out=None, stream=None):

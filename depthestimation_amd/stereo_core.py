@@ -39,7 +39,8 @@ from typing import Dict, Optional, Tuple
 
 import numpy as np
 
-from .matcher import HipBlockMatcher, postprocess_fast_device, postprocess_full_device, rectify_device
+from .matcher import (HipBlockMatcher, fill_holes_status, postprocess_fast_device, postprocess_full_device,
+                      rectify_device)
 from .postprocess import median_blur3, postprocess_disparity
 from .rectify import RectificationCache, rectify_images, to_grayscale_bgr
 
@@ -277,10 +278,19 @@ class StereoCore:
         (SURVEY.md 8f row F1); otherwise speckle filter + outlier removal (+ Telea hole filling
         with ``hole_filling``) + median (row F2).  Returns float32 HIP tensors
         (disparity_px, depth_m or None)."""
-        disp = self.compute_disparity_device(left, right, stream=stream)
         p = self.sgbm_params
         f, B = p.get('focal_length'), p.get('baseline')
         doffs, eps, max_depth = p.get('doffs', 0.0), p.get('min_disp', 5.0), p.get('max_depth')
+        if 'compute_disparity_device' not in self.__dict__ and self.sgbm is not None and \
+                getattr(self.sgbm, 'process_pair_device', None) is not None:
+            # one C-ABI call per frame (dsx_process_pair_device): the handle owns the float map and
+            # the post-processing workspace
+            return self.sgbm.process_pair_device(
+                left, right, fast_mode=self.fast_mode, max_speckle_size=int(100 * self.downscale_factor),
+                max_diff=1.0, apply_outlier_removal=True, outlier_threshold=2.5, outlier_kernel=5,
+                fill_radius=3 if p.get('hole_filling', False) else 0, focal_length=f, baseline=B, doffs=doffs,
+                eps=eps, max_depth=max_depth, stream=stream)
+        disp = self.compute_disparity_device(left, right, stream=stream)
         if self.fast_mode:
             return postprocess_fast_device(disp, p['num_disp'], f, B, doffs, eps, max_depth, stream=stream)
         # fill_kernel 3: postprocess_disparity's default as _process_pair calls it (postprocess.py:165)
@@ -312,13 +322,15 @@ class StereoCore:
         if self._device_pipeline_ok(left_source, right_source):
             import torch
             dev = torch.device("cuda", int(self.sgbm_params.get('device', 0)))
-            tl = torch.from_numpy(np.ascontiguousarray(left_source)).to(dev)
-            tr = torch.from_numpy(np.ascontiguousarray(right_source)).to(dev)
+            tl = torch.from_numpy(np.require(left_source, requirements=('C', 'W'))).to(dev)
+            tr = torch.from_numpy(np.require(right_source, requirements=('C', 'W'))).to(dev)
             d, z = self.estimate_depth_device(tl, tr)
             self.left_rectified = _HostView(self.left_rectified)
             self.right_rectified = _HostView(self.right_rectified)
             self.disparity_map = d.cpu().numpy()
             self.depth_map = None if z is None else z.cpu().numpy()
+            if self.sgbm_params.get('hole_filling', False) and not self.fast_mode:
+                fill_holes_status()  # the copies above waited for the march: a timed-out fill raises
             return self.disparity_map, self.depth_map
         self.left_rectified, self.right_rectified = self._prepare_rectified(left_source, right_source)
         return self._process_pair(self.left_rectified, self.right_rectified)

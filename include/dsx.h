@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define DSX_VERSION 102 /* 1.0.2: dsx_params.lr_form (OpenCV StereoSGBM left-right check form) */
+#define DSX_VERSION 103 /* 1.0.3: dsx_process_pair_device (the per-frame _process_pair in one call), dsx_fill_holes_status */
 
 #define DSX_OK 0
 #define DSX_EINVAL (-1) /* bad argument (mirrors ValueError / cv2.error on bad input) */
@@ -209,6 +209,47 @@ int dsx_postprocess_full_ex_device(const void *d_disp, int32_t H, int32_t W, int
 size_t dsx_fill_holes_workspace_bytes(int32_t H, int32_t W);
 int dsx_fill_holes_device(const void *d_disp, int32_t H, int32_t W, int64_t in_pitch, int32_t radius, void *d_out,
                           void *d_workspace, size_t workspace_bytes, void *hip_stream);
+
+/* 1 if a hole-filling call's persistent march timed out in a grid barrier (its remaining holes were
+ * left unfilled) since the last check: returns DSX_EHIP with a message and clears the condition;
+ * DSX_OK otherwise.  The next hole-filling call (dsx_fill_holes_device, dsx_postprocess_full_ex_device
+ * or dsx_process_pair_device with fill_radius > 0) checks it too and fails the same way.  The march
+ * runs asynchronously, so the condition is known once the stream has passed that call. */
+int dsx_fill_holes_status(void);
+
+/* The per-frame call of the drop-in path, StereoCore._process_pair on the device (stereo_core.py:
+ * 162-200): compute_disparity (:165, the matcher with this handle's parameters, float = fixed / 16,
+ * :232) -> crop [:, num_disp:] (:168) -> fast mode: 3x3 median (:171-173), or postprocess_disparity
+ * (:175-184 -> postprocess.py:120-171: speckles, outliers, optional Telea hole filling, median) ->
+ * disparity_to_depth (:186-196, :234-272) when has_depth.  One C-ABI call per frame; the handle owns
+ * the float map and the post-processing workspace (no allocation when the size matches).  Per-kernel
+ * times go to dsx_kernel_times when params.timing is set. */
+#define DSX_POST_FAST 1 /* fast_mode=True:  crop + medianBlur(3)                        */
+#define DSX_POST_FULL 2 /* fast_mode=False: crop + postprocess_disparity (the default)   */
+typedef struct dsx_post_params {
+    double max_diff;           /* 1.0   (stereo_core.py:179)                                        */
+    double outlier_threshold;  /* 2.5   (stereo_core.py:180)                                        */
+    double focal_length;       /* sgbm_params['focal_length'] (used when has_depth)                 */
+    double baseline;           /* sgbm_params['baseline']                                           */
+    double doffs;              /* sgbm_params['doffs']                                              */
+    double eps;                /* sgbm_params['min_disp'] (stereo_core.py:189: eps = min_disparity) */
+    double max_depth;          /* sgbm_params['max_depth'] (used when has_max_depth)               */
+    int32_t mode;              /* DSX_POST_FAST | DSX_POST_FULL                                     */
+    int32_t max_speckle_size;  /* int(100 * downscale_factor) (stereo_core.py:178)                  */
+    int32_t apply_outlier_removal; /* 1 (stereo_core.py:182)                                        */
+    int32_t outlier_kernel;    /* 5 (postprocess.py:158 default kernel_size)                        */
+    int32_t fill_radius;       /* 0, or 3 with hole_filling=True (postprocess.py:165 fill_kernel 3) */
+    int32_t has_depth;         /* focal_length and baseline are set (stereo_core.py:186)            */
+    int32_t has_max_depth;
+    int32_t reserved[5];
+} dsx_post_params;
+
+/* dL, dR: device uint8 H x W (row stride `stride_bytes`), rectified.  d_out_disp / d_out_depth:
+ * contiguous float32 H x (W - num_disp) device buffers (either may be NULL; depth is written only when
+ * has_depth).  Needs float_mode DSX_FLOAT_FIXED.  Asynchronous on hip_stream. */
+int dsx_process_pair_device(dsx_handle *h, const void *dL, const void *dR, int32_t H, int32_t W,
+                            int64_t stride_bytes, const dsx_post_params *pp, void *d_out_disp,
+                            void *d_out_depth, void *hip_stream);
 
 /* Per-frame rectification on the device, replacing cv2.cvtColor(BGR2GRAY)
  * + cv2.remap(INTER_LINEAR) of rectify.py:183-186 (cached-maps path) and stereo_core.py:155-159:

@@ -47,9 +47,22 @@ def test_params_struct_layout():
     assert ctypes.sizeof(_dsx.DsxParams) == 22 * 4
 
 
+def test_post_params_struct_layout_matches_c(tmp_path):
+    """dsx_post_params as gcc lays it out equals the ctypes mirror (size and every offset)."""
+    fields = [f for f, _ in _dsx.DsxPostParams._fields_]
+    c = tmp_path / "probe.c"
+    c.write_text('#include <stdio.h>\n#include <stddef.h>\n#include "dsx.h"\nint main(void){printf("%zu", sizeof(dsx_post_params));'
+                 + "".join(f'printf(" %zu", offsetof(dsx_post_params, {f}));' for f in fields) + "return 0;}\n")
+    exe = tmp_path / "probe"
+    subprocess.run(["gcc", "-std=c99", "-I", os.path.join(ROOT, "include"), str(c), "-o", str(exe)], check=True)
+    got = [int(x) for x in subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout.split()]
+    want = [ctypes.sizeof(_dsx.DsxPostParams)] + [getattr(_dsx.DsxPostParams, f).offset for f in fields]
+    assert got == want
+
+
 def test_version_and_defaults():
     lib = _dsx.lib()
-    assert lib.dsx_version() == 102
+    assert lib.dsx_version() == 103
     p = _dsx.default_params()
     # StereoCore.sgbm_params defaults (stereo_core.py:16-39) + build keys
     assert (p.min_disp, p.num_disp, p.block_size, p.uniqueness_ratio, p.disp12_max_diff) == (0, 128, 5, 10, 1)
@@ -91,6 +104,11 @@ def test_null_arguments_are_errors_not_crashes():
     assert lib.dsx_create(0, None, None) == _dsx.DSX_EINVAL
     assert lib.dsx_destroy(None) in (_dsx.DSX_OK, _dsx.DSX_EINVAL)
     assert lib.dsx_compute_host(None, None, None, 4, 4, 4, None, None) == _dsx.DSX_EINVAL
+    assert lib.dsx_process_pair_device(None, None, None, 4, 4, 4, None, None, None, None) == _dsx.DSX_EINVAL
+
+
+def test_fill_holes_status_clean_without_gpu():
+    assert _dsx.lib().dsx_fill_holes_status() == _dsx.DSX_OK
 
 
 def test_device_count_without_gpu(gpu_available):

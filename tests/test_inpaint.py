@@ -246,3 +246,34 @@ def test_fill_holes_device_on_matcher_output(config):
     c = clean.cpu().numpy()
     assert (c <= 0).sum() > 1000
     np.testing.assert_array_equal(got.cpu().numpy(), pp.fill_holes(c, method="inpaint", kernel_size=3))
+
+
+@pytest.mark.gpu
+def test_fill_holes_timeout_is_reported_not_silent(monkeypatch):
+    """A persistent march whose grid barrier times out (forced: spin bound 0, every layer in the
+    persistent kernel) leaves holes unfilled; that must surface as an error - from
+    dsx_fill_holes_status and from the next hole-filling call - never as a silent success."""
+    import torch
+    from depthestimation_amd.matcher import fill_holes_device, fill_holes_status
+    d = np.zeros((160, 240), np.float32)
+    d[7, 200] = 5.0  # ~390 layers: hundreds of barriers
+    fill_holes_status()  # clean state
+    monkeypatch.setenv("DSX_INPAINT_L0", "0")
+    monkeypatch.setenv("DSX_INPAINT_SPINS", "0")
+    got = fill_holes_device(torch.from_numpy(d).cuda(), radius=3)
+    torch.cuda.synchronize()
+    assert (got.cpu().numpy() <= 0).any()  # the march stopped early
+    with pytest.raises(RuntimeError, match="timed out"):
+        fill_holes_status()
+    fill_holes_status()  # cleared by the report
+    # the sticky flag also fails the next hole-filling call
+    fill_holes_device(torch.from_numpy(d).cuda(), radius=3)
+    torch.cuda.synchronize()
+    monkeypatch.delenv("DSX_INPAINT_SPINS")
+    with pytest.raises(RuntimeError, match="timed out"):
+        fill_holes_device(torch.from_numpy(d).cuda(), radius=3)
+    # with the normal bound everything is filled again and equals the host
+    got = fill_holes_device(torch.from_numpy(d).cuda(), radius=3)
+    torch.cuda.synchronize()
+    fill_holes_status()
+    np.testing.assert_array_equal(got.cpu().numpy(), pp.fill_holes(d, method="inpaint", kernel_size=3))
