@@ -207,13 +207,16 @@ class Ranks:
     device local_rank % device_count, collectives on host tensors) that runs the whole N-rank body
     on a box with fewer GPUs (tests/test_bench_multirank.py)."""
 
-    def __init__(self, backend: str):
+    def __init__(self, backend: str, single_rank_group: bool = True):
         import torch
         import torch.distributed as dist
         from depthestimation_amd import sharding
         self.torch, self.dist = torch, dist
         self.backend = backend
-        env = sharding.init_distributed(backend)
+        # at N = 1 a one-rank group as well (RCCL under "nccl"): the calibration broadcast, the
+        # max-over-ranks all_reduce and the frame-index all_gather run through the backend at every N
+        env = sharding.init_distributed(backend, single_rank_group=single_rank_group)
+        self.pg = dist.is_available() and dist.is_initialized()
         self.ws, self.rank, self.local = env.world_size, env.rank, env.local_rank
         self.ndev = torch.cuda.device_count()
         if backend == "nccl" and self.ws > self.ndev:
@@ -225,12 +228,12 @@ class Ranks:
         self.coll_dev = self.dev if backend == "nccl" else torch.device("cpu")
 
     def barrier(self):
-        if self.ws > 1:
+        if self.pg:
             self.dist.barrier()
 
     def allreduce(self, x, op="max"):
         """max / sum of a scalar over ranks (float64 for times, int64 for counts)."""
-        if self.ws == 1:
+        if not self.pg:
             return x
         torch, dist = self.torch, self.dist
         t = torch.tensor([x], dtype=torch.int64 if isinstance(x, int) else torch.float64, device=self.coll_dev)
@@ -238,14 +241,14 @@ class Ranks:
         return type(x)(t.item())
 
     def gather(self, obj):
-        if self.ws == 1:
+        if not self.pg:
             return [obj]
         out = [None] * self.ws
         self.dist.all_gather_object(out, obj)
         return out
 
     def close(self):
-        if self.ws > 1:
+        if self.pg:
             self.dist.barrier()
             self.dist.destroy_process_group()
 
@@ -276,6 +279,10 @@ def main():
                     help="skip the secondary C2 measurement with the reference's uniqueness/LR defaults")
     ap.add_argument("--sgm", default=None, choices=["sgbm_3way", "hh4", "sgbm", "hh"],
                     help="SGM aggregation mode (SURVEY 8f F4; volume path + path passes); not the headline")
+    ap.add_argument("--no-process-group", action="store_true",
+                    help="at N = 1, skip the one-rank process group (collectives become local no-ops)")
+    ap.add_argument("--no-dropin", action="store_true",
+                    help="skip the drop-in pipeline secondary (StereoCore defaults, one call per frame)")
     ap.add_argument("--selftest-launch", action="store_true", help=argparse.SUPPRESS)
     args = ap.parse_args()
 
@@ -293,7 +300,7 @@ def main():
 
     if not torch.cuda.is_available():
         raise RuntimeError("bench.py needs a HIP device")
-    rk = Ranks(args.dist_backend)
+    rk = Ranks(args.dist_backend, single_rank_group=not args.no_process_group)
     ws, rank, local, dev = rk.ws, rk.rank, rk.dev_index, rk.dev
 
     cfg = CONFIGS[args.config]
@@ -324,8 +331,12 @@ def main():
     flat = sorted(g for o in owned for g in o)
     sharding_info = {"frames_per_rank": nres, "global_frames": len(flat),
                      "disjoint_and_complete": flat == list(range(ws * nres)),
-                     "assignment": "global frame g on rank g mod N", "calibration_broadcast": "verified on every rank",
-                     "backend": "RCCL (torch.distributed nccl)" if args.dist_backend == "nccl" else "gloo"}
+                     "assignment": "global frame g on rank g mod N",
+                     "calibration_broadcast": ("verified on every rank" if rk.pg else
+                                               "none ran (no process group: --no-process-group)"),
+                     "backend": (("RCCL (torch.distributed nccl)" if args.dist_backend == "nccl" else "gloo")
+                                 + (f", {ws}-rank process group: the broadcast, all_reduce and all_gather_object "
+                                    "calls executed" if rk.pg else "") if rk.pg else "none (world 1, no process group)")}
     if not sharding_info["disjoint_and_complete"]:
         raise RuntimeError("frame sharding is not a partition of the global frame set")
     allL = torch.from_numpy(np.stack(hostL)).to(dev)
@@ -387,6 +398,23 @@ def main():
     # ~80 us against 72.4 us once settled (profiles/r03x_warmup_ab.txt, r03y kernel trace).  So the
     # headline step runs back to back for --settle seconds first; the W warmup and K timed steps follow
     # exactly as specified.
+    # the same K steps once before clock settling (the settled headline is not comparable
+    # with round-1/2 lines, which had no settling; this figure is)
+    unsettled = None
+    if args.steps > 0:
+        torch.cuda.synchronize(dev)
+        rk.barrier()
+        tu = time.perf_counter()
+        for i in range(args.steps):
+            step(i)
+        torch.cuda.synchronize(dev)
+        rk.barrier()
+        tu = rk.allreduce(float(time.perf_counter() - tu), "max")
+        unsettled = {"value": round(H * W * B * args.steps * ws / tu / 1e6, 1), "unit": "Mpix/s",
+                     "ms_per_step": round(tu / args.steps * 1e3, 5),
+                     "note": "the K timed steps run once right after the secondary figures, before --settle and the "
+                             "warmup (no clock settling: the form of rounds 1-2); not `value`"}
+
     settle_steps = 0
     t_settle = time.perf_counter()
     while time.perf_counter() - t_settle < args.settle:
@@ -494,9 +522,10 @@ def main():
             "roofline": roofline,
             "parity": parity,
             "sharding": sharding_info,
-            "order": "parity check -> secondary measurements -> clock settling -> warmup -> timed region -> "
-                     "breakdown pass -> CPU baseline",
+            "order": "parity check -> secondary measurements -> the K steps unsettled -> clock settling -> warmup "
+                     "-> timed region -> breakdown pass -> CPU baseline",
             "settle": {"seconds": args.settle, "steps": settle_steps, "timed": False},
+            "unsettled": unsettled,
         }
         if args.dist_backend == "gloo":
             result["oversubscribed"] = {"ranks": ws, "visible_gpus": rk.ndev,
@@ -637,6 +666,9 @@ def secondaries(args, cfg, rk, matcher, frames, hostL, hostR, allL, allR, out_fi
                         "default mode: speckles + outliers + median + depth; hole filling: Telea radius 3 on the "
                         "default-mode map's holes), stream events, median of 30 (10)"}
 
+    if args.config == "c2" and args.path == "fused" and B == 1 and not args.sgm and not args.no_dropin:
+        out["dropin"] = dropin_figures(rk, dev, stream)
+
     if B == 1 and args.path == "fused" and not args.no_batched and rk.rank == 0:
         # the same workload with 4 frame pairs per launch (video streams)
         Bb = 4
@@ -689,6 +721,78 @@ def secondaries(args, cfg, rk, matcher, frames, hostL, hostR, allL, allR, out_fi
         out["roofline_volume"] = rv
         vm.close()
     return out
+
+
+def dropin_figures(rk, dev, stream) -> dict:
+    """The pipeline a StereoCore() user runs: StereoCore at the reference's
+    defaults (uniqueness_ratio 10, disp12_max_diff 1, fast_mode False; stereo_core.py:16-39) with
+    focal length and baseline set, one estimate_depth_device per resident frame - gray input ->
+    matcher -> crop -> speckles -> outliers -> median -> depth, one dsx_process_pair_device call
+    (stereo_core.py:162-200, postprocess.py:120-171).  Per config: whole-job Mpix/s over back-to-back
+    frames (max time over ranks), the GPU time per frame, the per-kernel HIP-event breakdown of a
+    timing handle, and frame 0's disparity against the C oracle + host post-processing, bit for bit."""
+    import torch
+    from depthestimation_amd.matcher import HipBlockMatcher
+    from depthestimation_amd.postprocess import postprocess_disparity
+    from depthestimation_amd.stereo_core import StereoCore
+    from depthestimation_amd.synthetic import stereo_pair
+    from oracle.cref import CRef
+    res = {}
+    for name, key in (("c2", "c2r"), ("c4", "c4")):
+        cfg = CONFIGS[key]
+        H, W, D = cfg["H"], cfg["W"], cfg["num_disp"]
+        pairs = []
+        for i in range(2):
+            L, R, _ = stereo_pair(H, W, 0, D, seed=4321 + rk.rank + rk.ws * i)
+            pairs.append((L, R, torch.from_numpy(L).to(dev), torch.from_numpy(R).to(dev)))
+        core = StereoCore()
+        core.configure_sgbm(num_disp=D, block_size=cfg["block_size"], device=rk.dev_index, focal_length=700.0,
+                            baseline=0.1)
+        with torch.cuda.stream(stream):
+            d0, _ = core.estimate_depth_device(pairs[0][2], pairs[0][3], stream=stream)
+            torch.cuda.synchronize(dev)
+            got = d0.cpu().numpy()
+            want = postprocess_disparity(CRef()(pairs[0][0], pairs[0][1], **matcher_kwargs(cfg))["disp"][:, D:],
+                                         max_speckle_size=100, max_diff=1.0, outlier_threshold=2.5,
+                                         apply_outlier_removal=True, apply_hole_filling=False)
+            mism = rk.allreduce(int(np.count_nonzero(got != want)), "sum")
+            for i in range(20):
+                core.estimate_depth_device(pairs[i % 2][2], pairs[i % 2][3], stream=stream)
+            torch.cuda.synchronize(dev)
+            n = 200
+            rk.barrier()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            t0 = time.perf_counter()
+            e0.record(stream)
+            for i in range(n):
+                core.estimate_depth_device(pairs[i % 2][2], pairs[i % 2][3], stream=stream)
+            e1.record(stream)
+            torch.cuda.synchronize(dev)
+            dt = rk.allreduce(float(time.perf_counter() - t0), "max")
+            gpu_ms = e0.elapsed_time(e1) / n
+            core.sgbm = HipBlockMatcher(**dict(core.sgbm.params, timing=True))
+            for i in range(10):
+                core.estimate_depth_device(pairs[i % 2][2], pairs[i % 2][3], stream=stream)
+            torch.cuda.synchronize(dev)
+            core.sgbm.reset_times()
+            for i in range(50):
+                core.estimate_depth_device(pairs[i % 2][2], pairs[i % 2][3], stream=stream)
+            torch.cuda.synchronize(dev)
+            kt = {k: round(v[0], 5) for k, v in core.sgbm.kernel_times().items()}
+            core.sgbm.close()
+        post = round(sum(v for k, v in kt.items() if k not in ("bm_pass_left", "lr_fixup")), 5)
+        res[name] = {"value": round(H * W * n * rk.ws / dt / 1e6, 1), "unit": "Mpix/s",
+                     "ms_per_frame": round(dt / n * 1e3, 5), "gpu_ms_per_frame": round(gpu_ms, 5),
+                     "kernels_ms": kt, "post_processing_ms": post,
+                     "config": {"H": H, "W": W, "num_disp": D, "block_size": cfg["block_size"], "uniqueness_ratio": 10,
+                                "disp12_max_diff": 1, "fast_mode": False, "depth": True},
+                     "parity": {"mismatches": mism, "frames_checked": rk.ws,
+                                "compared": "float32 disparity (cropped, post-processed) of each rank's frame 0 against "
+                                            "oracle/bm_ref.c + the host restatement of postprocess_disparity"}}
+    res["note"] = ("secondary: the drop-in per-frame path at the reference defaults (StereoCore(), estimate_depth_device: "
+                   "matcher + lr_fixup + crop + speckles + outliers + median + depth in one C-ABI call); "
+                   "post_processing_ms = the kernels after the matcher (HIP events)")
+    return res
 
 
 def cpu_baseline(args, cfg, L, R) -> dict:

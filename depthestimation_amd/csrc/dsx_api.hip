@@ -163,7 +163,8 @@ struct dsx_handle {
     int16_t *postIn = nullptr;  // sgbm_post: the matcher's int16 maps (postFrames frames)
     void *postWs = nullptr;     // sgbm_post: median | speckle components
     int postFrames = 0;
-    float *ppDisp = nullptr;    // dsx_process_pair_device: the matcher's float map (H x W)
+    float *ppDisp = nullptr;    // dsx_process_pair_device: the matcher's float map (H x W, fast mode)
+    int16_t *ppFixed = nullptr; // dsx_process_pair_device: the matcher's x16 map (H x W, full mode)
     void *ppWs = nullptr;       // dsx_process_pair_device: post-processing workspace
     size_t ppWsBytes = 0;
     uint32_t *sgmS = nullptr;  // SGM path sums [H][W][Dp] u32 (sequential directions)
@@ -196,8 +197,10 @@ void free_buffers(dsx_handle *h) {
     (void)hipFree(h->sgmS);
     h->sgmS = nullptr;
     (void)hipFree(h->ppDisp);
+    (void)hipFree(h->ppFixed);
     (void)hipFree(h->ppWs);
     h->ppDisp = nullptr;
+    h->ppFixed = nullptr;
     h->ppWs = nullptr;
     h->ppWsBytes = 0;
     (void)hipFree(h->sgmL);
@@ -972,7 +975,9 @@ int dsx_process_pair_device(dsx_handle *h, const void *dL, const void *dR, int32
     rc = ensure_buffers(h, H, W, false);
     if (rc) return rc;
     const size_t n = (size_t)H * W;
-    if (!h->ppDisp) DSX_HIP(hipMalloc(&h->ppDisp, n * 4));
+    const bool full = pp->mode == DSX_POST_FULL;
+    if (!full && !h->ppDisp) DSX_HIP(hipMalloc(&h->ppDisp, n * 4));
+    if (full && !h->ppFixed) DSX_HIP(hipMalloc(&h->ppFixed, n * 2));
     const size_t wsb = dsx::post_full_workspace(H, W, crop);
     if (pp->mode == DSX_POST_FULL && h->ppWsBytes < wsb) {
         (void)hipFree(h->ppWs);
@@ -985,13 +990,15 @@ int dsx_process_pair_device(dsx_handle *h, const void *dL, const void *dR, int32
     // the float map and the workspace are handle scratch: order after the previous call's use
     if (h->scratchPending && h->scratchStream != st) DSX_HIP(hipStreamWaitEvent(st, h->scratchDone, 0));
     ScratchRecord rec_(h, st, true);
-    rc = run(h, dL, dR, H, W, stride_bytes, nullptr, h->ppDisp, st);
+    // full mode reads the x16 map itself (postprocess.py:27 computes int16(d * 16) of d = fixed / 16,
+    // which is `fixed` again): 2 B per pixel written by the matcher and read by the speckle pass
+    rc = run(h, dL, dR, H, W, stride_bytes, full ? h->ppFixed : nullptr, full ? nullptr : h->ppDisp, st);
     if (rc) return rc;
     rec_.active = true;  // run() recorded its own event; this call's kernels continue below
     const float fB = (float)(pp->focal_length * pp->baseline);
     if (pp->mode == DSX_POST_FULL) {
         dsx::PostFullArgs a{};
-        a.disp = h->ppDisp;
+        a.in16 = h->ppFixed;
         a.in_pitch = W;
         a.H = H;
         a.W = W;

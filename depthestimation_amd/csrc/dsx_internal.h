@@ -154,7 +154,9 @@ struct PostFullArgs {
     const int16_t *in16;
     int newv;
     int16_t *out16;
-    // two-launch form (spk_tile + post_tail2): per-pixel codes and the per-tile pending-node pool
+    // two-launch form (spk_tile + post_tail3): per-pixel 16-bit codes (the final x16 value, or
+    // kSent: see `code` = the full 32-bit code), and the per-tile pending-node pool
+    int16_t *code16;
     int *code, *pool;
     // diagnostics (DSX_POST_TIMELINE): per block 16 u64 - s_memrealtime after each phase, hw / xcc id
     uint64_t *tl_tile, *tl_tail;

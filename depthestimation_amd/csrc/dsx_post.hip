@@ -451,6 +451,7 @@ constexpr int kSpTX = 64, kSpTY = 16, kSpN = kSpTX * kSpTY;
 // plus at most one edge per border pixel side (64 + 64 + 16 + 16 = 160): <= 472
 constexpr int kSpPool = 512;
 constexpr int kPend = 0x40000000;  // codes >= kPend are pending nodes; decided codes are int16 values
+constexpr int kSent = -32768;      // code16 of a pending pixel (and of the value -32768): read code[p]
 constexpr int kOpen = 1 << 20;     // tile component size word: leaves the tile (sizes <= 1024)
 constexpr int kBfsMaxSpeckle = 2047;  // visited lists of 4 waves x (max + 1) ints in LDS
 constexpr int kHash = 1024;           // pending-node table of a tail block (>= 2x its 16 x 40 region)
@@ -474,6 +475,18 @@ __device__ __forceinline__ void pstamp(uint64_t *tl, int i) {
     }
 }
 
+// the value one lane up (lane 0: its own) - DPP wave_shr:1, no LDS round trip
+__device__ __forceinline__ int lane_up(int v) { return __builtin_amdgcn_update_dpp(v, v, 0x138, 0xF, 0xF, false); }
+
+// spk_val without branches around the load: clamped address, newv outside the image (all loads of a
+// thread issue back to back)
+__device__ __forceinline__ int spk_val_nb(const PostFullArgs &a, int Wc, int y, int x) {
+    const bool in = y >= 0 && y < a.H && x >= 0 && x < Wc;
+    const int64_t q = (int64_t)min(max(y, 0), a.H - 1) * a.in_pitch + a.crop + min(max(x, 0), Wc - 1);
+    const int v = a.in16 ? (int)a.in16[q] : (int)(int16_t)(int)__builtin_truncf(a.disp[q] * 16.0f);
+    return in ? v : a.newv;
+}
+
 __global__ __launch_bounds__(256) void spk_tile(PostFullArgs a) {
     __shared__ int16_t vl[kSpN];   // d16
     __shared__ int16_t lb[kSpN];   // run start (local index) of each pixel
@@ -483,25 +496,23 @@ __global__ __launch_bounds__(256) void spk_tile(PostFullArgs a) {
     __shared__ int ecn[kSpN];      // pending roots: cross edges kept
     __shared__ int16_t rg_t[kSpTX], rg_b[kSpTX], rg_l[kSpTY], rg_r[kSpTY];
     __shared__ int used;
-    const int Wc = a.W - a.crop, H = a.H;
+    const int Wc = a.W - a.crop;
     const int md = a.max_diff16, nv = a.newv, maxsp = a.max_speckle;
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int x0 = blockIdx.x * kSpTX, y0 = blockIdx.y * kSpTY;
     const int gx = x0 + lane;
     const int tbase = (blockIdx.y * gridDim.x + blockIdx.x) * kSpPool;
     pstamp(a.tl_tile, 0);
+    // the ring pixel of this lane (wave 0: row above, 1: row below, 2: column left, 3: column right)
+    const int ry = w == 0 ? y0 - 1 : w == 1 ? y0 + kSpTY : y0 + (lane & (kSpTY - 1));
+    const int rx = w < 2 ? gx : w == 2 ? x0 - 1 : x0 + kSpTX;
     int v[4];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) v[i] = spk_val(a, Wc, y0 + 4 * w + i, gx);
-    if (w == 0) {
-        rg_t[lane] = (int16_t)spk_val(a, Wc, y0 - 1, gx);
-    } else if (w == 1) {
-        rg_b[lane] = (int16_t)spk_val(a, Wc, y0 + kSpTY, gx);
-    } else if (w == 2) {
-        if (lane < kSpTY) rg_l[lane] = (int16_t)spk_val(a, Wc, y0 + lane, x0 - 1);
-    } else {
-        if (lane < kSpTY) rg_r[lane] = (int16_t)spk_val(a, Wc, y0 + lane, x0 + kSpTX);
-    }
+    for (int i = 0; i < 4; ++i) v[i] = spk_val_nb(a, Wc, y0 + 4 * w + i, gx);
+    const int ring = spk_val_nb(a, Wc, ry, rx);
+    if (w == 0) rg_t[lane] = (int16_t)ring;
+    else if (w == 1) rg_b[lane] = (int16_t)ring;
+    else if (lane < kSpTY) (w == 2 ? rg_l : rg_r)[lane] = (int16_t)ring;
     if (threadIdx.x == 0) used = 0;
     const uint64_t le = lane == 63 ? ~0ull : ((2ull << lane) - 1ull);  // lanes <= this one
     uint64_t S[4];
@@ -509,7 +520,7 @@ __global__ __launch_bounds__(256) void spk_tile(PostFullArgs a) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
         const int r = 4 * w + i, li = r * kSpTX + lane;
-        const int left = __shfl_up(v[i], 1);
+        const int left = lane_up(v[i]);  // outside any lane-dependent branch: DPP needs its source lane active
         const bool hj = lane > 0 && joins(left, v[i], md, nv);
         S[i] = __ballot(!hj);
         lab[i] = r * kSpTX + 63 - __clzll((long long)(S[i] & le));
@@ -521,15 +532,16 @@ __global__ __launch_bounds__(256) void spk_tile(PostFullArgs a) {
     }
     __syncthreads();
     pstamp(a.tl_tile, 1);
-    // vertical joins: one union per (run below, run above) pair (the first column of the pair)
+    // vertical joins: one union per (run below, run above) pair (the first column of the pair); the
+    // row above is this wave's previous row except for the wave's first row
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
         const int r = 4 * w + i;
         if (r == 0) continue;
-        const int up = vl[(r - 1) * kSpTX + lane];
-        const int ul = lb[(r - 1) * kSpTX + lane];
+        const int up = i ? v[i - 1] : vl[(r - 1) * kSpTX + lane];
+        const int ul = i ? lab[i - 1] : lb[(r - 1) * kSpTX + lane];
         const bool vj = joins(up, v[i], md, nv);
-        const int pvj = __shfl_up((int)vj, 1), pla = __shfl_up(lab[i], 1), pul = __shfl_up(ul, 1);
+        const int pvj = lane_up((int)vj), pla = lane_up(lab[i]), pul = lane_up(ul);
         const bool dup = lane > 0 && pvj && pla == lab[i] && pul == ul;
         if (vj && !dup) ufl_unite(pl, lab[i], ul);
     }
@@ -553,7 +565,8 @@ __global__ __launch_bounds__(256) void spk_tile(PostFullArgs a) {
             atomicAdd(&cnt[rr], next - lane);  // the run's length
         }
     }
-    // components with a joining edge out of the tile
+    // components with a joining edge out of the tile (the ring values: wave 0 / 3 read their own
+    // top / bottom ring from LDS written before the first barrier)
     {
         const int vt = w == 0 ? v[0] : v[3], rtb = w == 0 ? root[0] : root[3];
         if ((w == 0 || w == 3) && rtb >= 0 && joins(vt, w == 0 ? rg_t[lane] : rg_b[lane], md, nv))
@@ -569,85 +582,111 @@ __global__ __launch_bounds__(256) void spk_tile(PostFullArgs a) {
     __syncthreads();
     pstamp(a.tl_tile, 3);
     const auto pend = [&](int c) { return (c & kOpen) && (c & (kOpen - 1)) <= maxsp; };
-    // cross edges of pending pieces, one per run along a side: an edge is dropped when the previous
-    // pixel along the side has an edge of the same piece and the two outside pixels join (they lie
-    // in one neighbour tile, so they are in one of its pieces)
-    int tbSlot = -1, tbRoot = 0, tbQ = 0;
-    if (w == 0 || w == 3) {
-        const int vt = w == 0 ? v[0] : v[3], rtb = w == 0 ? root[0] : root[3];
-        const int16_t *rg = w == 0 ? rg_t : rg_b;
-        const int ring = rg[lane];
-        const bool e = rtb >= 0 && joins(vt, ring, md, nv);
-        const int pe = __shfl_up((int)e, 1), pr = __shfl_up(rtb, 1);
-        const bool dup = lane > 0 && pe && pr == rtb && joins(rg[lane - (lane > 0)], ring, md, nv);
-        if (e && !dup && pend(cnt[rtb])) {
-            tbSlot = atomicAdd(&ecn[rtb], 1);
-            tbRoot = rtb;
-            tbQ = (w == 0 ? y0 - 1 : y0 + kSpTY) * Wc + gx;
-        }
+    int cn[4];
+    bool mine = false;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        cn[i] = root[i] >= 0 ? cnt[root[i]] : 0;
+        mine |= root[i] >= 0 && pend(cn[i]);
     }
-    int sSlot[4], sRoot[4], sQ[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) sSlot[i] = -1, sRoot[i] = 0, sQ[i] = 0;
-    if (lane == 0 || lane == 63) {
-        const int16_t *rg = lane == 0 ? rg_l : rg_r;
-        const int xo = lane == 0 ? x0 - 1 : x0 + kSpTX;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const int r = 4 * w + i;
-            const int ring = rg[r];
-            const bool e = root[i] >= 0 && joins(v[i], ring, md, nv);
-            bool dup = false;
-            if (r > 0) {
-                const int pli = (r - 1) * kSpTX + lane;
-                dup = rt[pli] == root[i] && joins(vl[pli], rg[r - 1], md, nv) && joins(rg[r - 1], ring, md, nv);
-            }
-            if (e && !dup && pend(cnt[root[i]])) {
-                sSlot[i] = atomicAdd(&ecn[root[i]], 1);
-                sRoot[i] = root[i];
-                sQ[i] = (y0 + r) * Wc + xo;
+    if (__syncthreads_or(mine)) {  // this tile has pending pieces (rare): node records and edges
+        // cross edges of pending pieces, one per run along a side: an edge is dropped when the
+        // previous pixel along the side has an edge of the same piece and the two outside pixels
+        // join (they lie in one neighbour tile, so they are in one of its pieces)
+        int tbSlot = -1, tbRoot = 0, tbQ = 0;
+        if (w == 0 || w == 3) {
+            const int vt = w == 0 ? v[0] : v[3], rtb = w == 0 ? root[0] : root[3];
+            const int16_t *rg = w == 0 ? rg_t : rg_b;
+            const int rv = rg[lane];
+            const bool e = rtb >= 0 && joins(vt, rv, md, nv);
+            const int pe = lane_up((int)e), pr = lane_up(rtb), prv = lane_up(rv);
+            const bool dup = lane > 0 && pe && pr == rtb && joins(prv, rv, md, nv);
+            if (e && !dup && pend(cnt[rtb])) {
+                tbSlot = atomicAdd(&ecn[rtb], 1);
+                tbRoot = rtb;
+                tbQ = ((w == 0 ? y0 - 1 : y0 + kSpTY) << 16) | gx;  // outside pixel (y << 16 | x)
             }
         }
+        int sSlot[4], sRoot[4], sQ[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) sSlot[i] = -1, sRoot[i] = 0, sQ[i] = 0;
+        if (lane == 0 || lane == 63) {
+            const int16_t *rg = lane == 0 ? rg_l : rg_r;
+            const int xo = lane == 0 ? x0 - 1 : x0 + kSpTX;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int r = 4 * w + i;
+                const int rv = rg[r];
+                const bool e = root[i] >= 0 && joins(v[i], rv, md, nv);
+                bool dup = false;
+                if (r > 0) {
+                    const int pli = (r - 1) * kSpTX + lane;
+                    dup = rt[pli] == root[i] && joins(vl[pli], rg[r - 1], md, nv) && joins(rg[r - 1], rv, md, nv);
+                }
+                if (e && !dup && pend(cnt[root[i]])) {
+                    sSlot[i] = atomicAdd(&ecn[root[i]], 1);
+                    sRoot[i] = root[i];
+                    sQ[i] = ((y0 + r) << 16) | xo;
+                }
+            }
+        }
+        __syncthreads();
+        // node records of the pending roots in the tile's pool region
+        for (int li = threadIdx.x; li < kSpN; li += 256) {
+            if (rt[li] == li && pend(cnt[li])) {
+                const int ne = ecn[li];
+                const int off = atomicAdd(&used, 2 + ne);
+                pl[li] = off;
+                a.pool[tbase + off] = cnt[li] & (kOpen - 1);
+                a.pool[tbase + off + 1] = ne;
+            }
+        }
+        __syncthreads();
+        if (tbSlot >= 0) a.pool[tbase + pl[tbRoot] + 2 + tbSlot] = tbQ;
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+            if (sSlot[i] >= 0) a.pool[tbase + pl[sRoot[i]] + 2 + sSlot[i]] = sQ[i];
     }
-    __syncthreads();
     pstamp(a.tl_tile, 4);
-    // node records of the pending roots in the tile's pool region
-    for (int li = threadIdx.x; li < kSpN; li += 256) {
-        if (rt[li] == li && pend(cnt[li])) {
-            const int ne = ecn[li];
-            const int off = atomicAdd(&used, 2 + ne);
-            pl[li] = off;
-            a.pool[tbase + off] = cnt[li] & (kOpen - 1);
-            a.pool[tbase + off + 1] = ne;
-        }
-    }
-    __syncthreads();
-    pstamp(a.tl_tile, 5);
-    if (tbSlot >= 0) a.pool[tbase + pl[tbRoot] + 2 + tbSlot] = tbQ;
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-        if (sSlot[i] >= 0) a.pool[tbase + pl[sRoot[i]] + 2 + sSlot[i]] = sQ[i];
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
         const int y = y0 + 4 * w + i;
-        if (y >= H || gx >= Wc) continue;
+        if (y >= a.H || gx >= Wc) continue;
         int c = v[i];
         if (root[i] >= 0) {
-            const int cn = cnt[root[i]], sz = cn & (kOpen - 1);
-            if (!(cn & kOpen)) {
+            const int sz = cn[i] & (kOpen - 1);
+            if (!(cn[i] & kOpen)) {
                 if (sz <= maxsp) c = nv;
             } else if (sz <= maxsp) {
-                c = kPend | (tbase + pl[root[i]]);
+                c = kPend | (pl[root[i]] << 16) | (c & 0xFFFF);  // node offset in the tile's pool, d16
             }
         }
-        a.code[(int64_t)y * Wc + gx] = c;
+        const int64_t o = (int64_t)y * Wc + gx;
+        if (c == (int)(int16_t)c && c != kSent) {
+            a.code16[o] = (int16_t)c;
+        } else {
+            a.code16[o] = (int16_t)kSent;
+            a.code[o] = c;
+        }
     }
     pstamp(a.tl_tile, 7);
 }
 
-// Breadth-first search of one wave over pending pieces from node k0 (a pool offset); true when the
+__device__ __forceinline__ int spk_code(const PostFullArgs &a, int64_t p) {
+    const int c = a.code16[p];
+    return c != kSent ? c : a.code[p];
+}
+
+// Pending codes: kPend | (node offset in its tile's pool region) << 16 | (d16 & 0xFFFF); a node's
+// global pool index is its tile's base + that offset.  Cross edges name the outside pixel as
+// (y << 16) | x.
+__device__ __forceinline__ int spk_node(int code, int y, int x, int ntx) {
+    return ((y >> 4) * ntx + (x >> 6)) * kSpPool + ((code >> 16) & (kSpPool - 1));
+}
+
+// Breadth-first search of one wave over pending pieces from node k0 (a pool index); true when the
 // component has at most max_speckle pixels.  `vis` holds max_speckle + 1 ints (see above).
-__device__ bool spk_small(const PostFullArgs &a, int k0, int *vis, int lane) {
+__device__ bool spk_small(const PostFullArgs &a, int k0, int *vis, int lane, int Wc, int ntx) {
     const int maxsp = a.max_speckle;
     if (lane == 0) vis[0] = k0;
     int nvis = 1, head = 0, size = 0;
@@ -659,18 +698,19 @@ __device__ bool spk_small(const PostFullArgs &a, int k0, int *vis, int lane) {
         const int ne = __shfl(rec, 1);
         if (size + (nvis - head) > maxsp) return false;
         for (int j0 = 0; j0 < ne; j0 += (j0 == 0 ? 62 : 64)) {
-            int q = -1;
+            int e = -1;
             if (j0 == 0) {
-                if (lane >= 2 && lane - 2 < ne) q = rec;
+                if (lane >= 2 && lane - 2 < ne) e = rec;
             } else if (j0 + lane < ne) {
-                q = a.pool[k + 2 + j0 + lane];
+                e = a.pool[k + 2 + j0 + lane];
             }
             int h = -1;
             bool large = false;
-            if (q >= 0) {
-                const int c = a.code[q];
+            if (e >= 0) {
+                const int y = (int)((unsigned)e >> 16), x = e & 0xFFFF;
+                const int c = spk_code(a, (int64_t)y * Wc + x);
                 if (c < kPend) large = true;  // a decided piece with a joining edge: more than max pixels
-                else h = c - kPend;
+                else h = spk_node(c, y, x, ntx);
             }
             if (__ballot(large)) return false;
             while (true) {
@@ -691,130 +731,252 @@ __device__ bool spk_small(const PostFullArgs &a, int k0, int *vis, int lane) {
     return true;
 }
 
-// post_tail on spk_tile's codes (outlier kernel k <= 7); dynamic LDS: 4 x (max_speckle + 1) ints
-__global__ __launch_bounds__(kTailTX *kTailTY) void post_tail2(PostFullArgs a) {
-    __shared__ float t0[kT0H][kT0W];
-    __shared__ double rs[kT0H][kT1W], rs2[kT0H][kT1W];
-    __shared__ float t1[kT1H][kT1W];
-    __shared__ int pk[kT0H * kT0W];  // pending entries of the region: node, then its table slot
-    __shared__ int hkey[kHash];
-    __shared__ int8_t hres[kHash];
+// post_tail3: the tail of post_tail on spk_tile's codes, with about half its instructions per pixel.
+//  * templated on the outlier radius (constant region shape: no integer division, unrolled sums);
+//  * 32 x 16 output pixels per 256-thread block (2 per thread): less halo per output;
+//  * the k x k box sums in integers: t0 = v / 16 with v the int16 x16 value, so sum(t0) = sum(v) / 16
+//    and float32(t0 * t0) = fsq(v) / 256 with fsq(v) = float32(v) * float32(v) (an integer < 2^31),
+//    so the host's exact float64 sums are sum(v) / 16 and sum(fsq) / 256 - one float64 multiply each
+//    reproduces mean and mean of squares bit for bit.  unsigned 32-bit sums are exact while
+//    |v| <= 8191 (49 * 8191^2 < 2^32); a block holding a larger value takes float64 sums;
+//  * the t1 ring is stored with the median's BORDER_REPLICATE already applied (a ring position
+//    outside the image holds t1 of the clamped position), so the median reads 3 x 3 without clamps,
+//    and the median of 9 is med3(max3 of column minima, med3 of column medians, min3 of column maxima)
+//    of the three sorted columns (v_min3 / v_med3 / v_max3).
+constexpr int kT3X = 32, kT3Y = 16;
+constexpr int kSqMax = 8191;
+
+template <int R>
+struct T3 {
+    static constexpr int RH = kT3Y + 2 + 2 * R, RW = kT3X + 2 + 2 * R;  // code region
+    static constexpr int H1 = kT3Y + 2, W1 = kT3X + 2;                    // t1 tile (ring of 1)
+    static constexpr int K = 2 * R + 1;
+};
+
+__device__ __forceinline__ int refl(int i, int n) {  // reflect101 for i in [-(n - 1), 2n - 2]
+    i = i < 0 ? -i : i;
+    return i >= n ? 2 * (n - 1) - i : i;
+}
+
+__device__ __forceinline__ float med3f(float a, float b, float c) { return __builtin_amdgcn_fmed3f(a, b, c); }
+__device__ __forceinline__ float min3f(float a, float b, float c) { return fminf(fminf(a, b), c); }
+__device__ __forceinline__ float max3f(float a, float b, float c) { return fmaxf(fmaxf(a, b), c); }
+
+__device__ __forceinline__ float median9_cols(float a0, float a1, float a2, float b0, float b1, float b2, float c0,
+                                              float c1, float c2) {
+    // columns (a, b, c), each three rows: median of the nine
+    const float lo = max3f(min3f(a0, a1, a2), min3f(b0, b1, b2), min3f(c0, c1, c2));
+    const float md = med3f(med3f(a0, a1, a2), med3f(b0, b1, b2), med3f(c0, c1, c2));
+    const float hi = min3f(max3f(a0, a1, a2), max3f(b0, b1, b2), max3f(c0, c1, c2));
+    return med3f(lo, md, hi);
+}
+
+template <int R>
+__global__ __launch_bounds__(256, 8) void post_tail3(PostFullArgs a) {
+    using G = T3<R>;
+    constexpr int RH = G::RH, RW = G::RW, H1 = G::H1, W1 = G::W1, K = G::K;
+    __shared__ int iv[RH][RW];            // x16 values after the speckle filter
+    __shared__ unsigned sqv[RH][RW];      // fsq(v)
+    __shared__ union {
+        struct {
+            int hs[RH][W1];               // horizontal K-sums of iv
+            unsigned hs2[RH][W1];         // ... of sqv
+            float t1[H1][W1];
+        } s;
+        struct {
+            int pk[RH * RW];              // pending entries: node, then its table slot
+            int hkey[kHash];              // pending nodes of the region (open addressing)
+            int16_t hlist[kHash];         // occupied slots in insertion order
+            int8_t hres[kHash];           // 0 large (keep), 1 small (newv), 2 undecided by the first level
+        } p;
+    } u;
+    __shared__ int bigs, hn;
     extern __shared__ int vis[];
-    const int Wc = a.W - a.crop, H = a.H;
-    const int r = a.kernel / 2;
-    const int x0 = blockIdx.x * kTailTX, y0 = blockIdx.y * kTailTY;
+    const int Wc = a.W - a.crop, H = a.H, nv = a.newv;
+    const int ntx = (Wc + kSpTX - 1) / kSpTX;
+    const int x0 = blockIdx.x * kT3X, y0 = blockIdx.y * kT3Y;
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-    const int th0 = kTailTY + 2 + 2 * r, tw0 = kTailTX + 2 + 2 * r;
+    const bool fastref = H >= R + 3 && Wc >= R + 3;  // refl() covers offsets up to R + 1
+    const auto ry = [&](int k) { const int y = y0 - 1 - R + k; return fastref ? refl(y, H) : reflect101(y, H); };
+    const auto rx = [&](int k) { const int x = x0 - 1 - R + k; return fastref ? refl(x, Wc) : reflect101(x, Wc); };
     pstamp(a.tl_tail, 0);
-    for (int q = tid; q < kHash; q += kTailTX * kTailTY) hkey[q] = -1;
-    int anyp = 0;
-    for (int q = tid; q < th0 * tw0; q += kTailTX * kTailTY) {
-        const int ty = q / tw0, tx = q - ty * tw0;
-        const int yy = reflect101(y0 - 1 - r + ty, H), xx = reflect101(x0 - 1 - r + tx, Wc);
-        const int c = a.code[(int64_t)yy * Wc + xx];
-        if (c >= kPend) {
-            pk[q] = c - kPend;
+    for (int q = tid; q < kHash; q += 256) u.p.hkey[q] = -1;
+    if (tid == 0) hn = 0;
+    int anyp = 0, big = 0;
+    constexpr int NQ = (RH * RW + 255) / 256;
+    int cv[NQ];
+#pragma unroll
+    for (int j = 0; j < NQ; ++j) {  // every load of the thread in flight at once
+        const int q = min(tid + 256 * j, RH * RW - 1);
+        const int ty = q / RW, tx = q - ty * RW;
+        cv[j] = a.code16[(int64_t)ry(ty) * Wc + rx(tx)];
+    }
+#pragma unroll
+    for (int j = 0; j < NQ; ++j) {
+        const int q = tid + 256 * j;
+        if (q >= RH * RW) break;
+        const int ty = q / RW, tx = q - ty * RW;
+        int c = cv[j];
+        if (c == kSent) c = a.code[(int64_t)ry(ty) * Wc + rx(tx)];  // pending (rare): the full code
+        if (c >= kPend) {  // pending: the node, and its x16 value (kept unless the piece is small)
+            u.p.pk[q] = spk_node(c, ry(ty), rx(tx), ntx);
             anyp = 1;
+            c = (int)(int16_t)(c & 0xFFFF);
         } else {
-            pk[q] = -1;
-            t0[ty][tx] = (float)c / 16.0f;
+            u.p.pk[q] = -1;
         }
+        iv[ty][tx] = c;
+        sqv[ty][tx] = (unsigned)((float)c * (float)c);
+        big |= (c > kSqMax) | (c < -kSqMax);
     }
     const int anyb = __syncthreads_or(anyp);
+    int wide = __syncthreads_or(big);
     pstamp(a.tl_tail, 1);
     if (anyb) {
-        for (int q = tid; q < th0 * tw0; q += kTailTX * kTailTY) {
-            const int key = pk[q];
+        if (tid == 0) bigs = wide;
+        for (int q = tid; q < RH * RW; q += 256) {
+            const int key = u.p.pk[q];
             if (key < 0) continue;
             int h = (int)(((unsigned)key * 2654435761u) >> 22);
             while (true) {
-                const int old = atomicCAS(&hkey[h], -1, key);
-                if (old == -1 || old == key) break;
+                const int old = atomicCAS(&u.p.hkey[h], -1, key);
+                if (old == -1) {
+                    u.p.hlist[atomicAdd(&hn, 1)] = (int16_t)h;
+                    break;
+                }
+                if (old == key) break;
                 h = (h + 1) & (kHash - 1);
             }
-            pk[q] = h;
+            u.p.pk[q] = h;
         }
         __syncthreads();
-        int *wvis = vis + wave * (a.max_speckle + 1);
-        for (int j0 = wave * 64; j0 < kHash; j0 += 256) {
-            const int key = hkey[j0 + lane];
-            uint64_t m = __ballot(key >= 0);
-            while (m) {
-                const int b = __ffsll((long long)m) - 1;
-                m &= m - 1;
-                const bool sm = spk_small(a, __shfl(key, b), wvis, lane);
-                if (lane == 0) hres[j0 + b] = sm ? 1 : 0;
+        const int n = hn;
+        // first level for 16 nodes at a time, 16 lanes per node: the record (size, edge count,
+        // 14 edges) in one load, the codes behind its edges in one more; a decided code = large
+        {
+            const int g = tid >> 4, gl = tid & 15, gs = lane & 48;
+            for (int j = g; j < n; j += 16) {
+                const int h = u.p.hlist[j];
+                const int node = u.p.hkey[h];
+                const int rec = a.pool[node + gl];
+                const int ne = __shfl(rec, 1, 16);
+                bool large = false, more = false;
+                if (gl >= 2 && gl - 2 < ne) {
+                    const int y = (int)((unsigned)rec >> 16), x = rec & 0xFFFF;
+                    const int c = spk_code(a, (int64_t)y * Wc + x);
+                    large = c < kPend;
+                    more = !large;
+                }
+                const bool glarge = (__ballot(large) >> gs) & 0xFFFFull;
+                const bool gmore = ((__ballot(more) >> gs) & 0xFFFFull) || ne > 14;
+                if (gl == 0) u.p.hres[h] = glarge ? 0 : (gmore ? 2 : 1);
             }
         }
         __syncthreads();
-        for (int q = tid; q < th0 * tw0; q += kTailTX * kTailTY) {
-            const int slot = pk[q];
-            if (slot < 0) continue;
-            const int ty = q / tw0, tx = q - ty * tw0;
-            const int yy = reflect101(y0 - 1 - r + ty, H), xx = reflect101(x0 - 1 - r + tx, Wc);
-            const int v = hres[slot] ? a.newv : spk_val(a, Wc, yy, xx);
-            t0[ty][tx] = (float)v / 16.0f;
+        // the rest: a breadth-first search of one wave per undecided node
+        int *wvis = vis + wave * (a.max_speckle + 1);
+        for (int j = wave; j < n; j += 4) {
+            const int h = u.p.hlist[j];
+            if (u.p.hres[h] != 2) continue;  // wave-uniform
+            const bool sm = spk_small(a, u.p.hkey[h], wvis, lane, Wc, ntx);
+            if (lane == 0) u.p.hres[h] = sm ? 1 : 0;
         }
+        __syncthreads();
+        for (int q = tid; q < RH * RW; q += 256) {
+            const int slot = u.p.pk[q];
+            if (slot < 0 || u.p.hres[slot] != 1) continue;
+            const int ty = q / RW, tx = q - ty * RW;
+            iv[ty][tx] = nv;  // a small component: newVal
+            sqv[ty][tx] = (unsigned)((float)nv * (float)nv);
+            if (nv > kSqMax || nv < -kSqMax) bigs = 1;
+        }
+        __syncthreads();
+        wide = bigs;
     }
-    __syncthreads();
     pstamp(a.tl_tail, 2);
     const bool outl = a.apply_outliers != 0;
-    if (outl) {
-        for (int q = tid; q < th0 * kT1W; q += kTailTX * kTailTY) {
-            const int ty = q / kT1W, c = q - ty * kT1W;
-            double s = 0.0, s2 = 0.0;
-            for (int i = 0; i <= 2 * r; ++i) {
-                const float v = t0[ty][c + i];
-                s += (double)v;
-                s2 += (double)(v * v);
+    if (outl && !wide) {
+        for (int q = tid; q < RH * W1; q += 256) {
+            const int k = q / W1, c = q - k * W1;
+            int s = 0;
+            unsigned s2 = 0;
+#pragma unroll
+            for (int i = 0; i < K; ++i) {
+                s += iv[k][c + i];
+                s2 += sqv[k][c + i];
             }
-            rs[ty][c] = s;
-            rs2[ty][c] = s2;
+            u.s.hs[k][c] = s;
+            u.s.hs2[k][c] = s2;
         }
         __syncthreads();
     }
     pstamp(a.tl_tail, 3);
-    const double scale = 1.0 / (double)(a.kernel * a.kernel);
-    for (int q = tid; q < kT1H * kT1W; q += kTailTX * kTailTY) {
-        const int ty = q / kT1W, c = q - ty * kT1W;
-        const float d = t0[ty + r][c + r];
+    const double scale = 1.0 / (double)(K * K);
+    for (int q = tid; q < H1 * W1; q += 256) {
+        const int ty = q / W1, c = q - ty * W1;
+        // the median's replicated border: a ring position outside the image takes the clamped one
+        const int cy = min(max(y0 - 1 + ty, 0), H - 1) - (y0 - 1);
+        const int cx = min(max(x0 - 1 + c, 0), Wc - 1) - (x0 - 1);
+        const float d = (float)iv[cy + R][cx + R] / 16.0f;
         float v = d;
         if (outl) {
-            double s = 0.0, s2 = 0.0;
-            for (int j = 0; j <= 2 * r; ++j) {
-                s += rs[ty + j][c];
-                s2 += rs2[ty + j][c];
+            double S, S2;
+            if (!wide) {
+                int s = 0;
+                unsigned s2 = 0;
+#pragma unroll
+                for (int j = 0; j < K; ++j) {
+                    s += u.s.hs[cy + j][cx];
+                    s2 += u.s.hs2[cy + j][cx];
+                }
+                S = (double)s * 0.0625;
+                S2 = (double)s2 * 0.00390625;
+            } else {  // |v| > 8191 somewhere in the block: float64 window sums (exact), as the host
+                S = 0.0;
+                S2 = 0.0;
+                for (int j = 0; j < K; ++j)
+                    for (int i = 0; i < K; ++i) {
+                        const float t = (float)iv[cy + j][cx + i] / 16.0f;
+                        S += (double)t;
+                        S2 += (double)(t * t);
+                    }
             }
-            const float mean = (float)(s * scale), msq = (float)(s2 * scale);
+            const float mean = (float)(S * scale), msq = (float)(S2 * scale);
             const float var = msq - mean * mean;
             const float sd = sqrtf(var > 0.0f ? var : 0.0f);
             if (d > 0.0f && fabsf(d - mean) > a.thr * sd) v = 0.0f;
         }
-        t1[ty][c] = v;
+        u.s.t1[ty][c] = v;
     }
     __syncthreads();
     pstamp(a.tl_tail, 4);
-    const int lx = tid % kTailTX, ly = tid / kTailTX;
+    const int lx = tid & 31, ly = 2 * (tid >> 5);
     const int x = x0 + lx, y = y0 + ly;
-    if (tid == 0) pstamp(a.tl_tail, 5);  // (thread 0 stamps before it may leave)
+    if (tid == 0) pstamp(a.tl_tail, 5);
     if (x >= Wc || y >= H) return;
     if (a.tail_t1) {
-        a.t1[(int64_t)y * Wc + x] = t1[ly + 1][lx + 1];
+        a.t1[(int64_t)y * Wc + x] = u.s.t1[ly + 1][lx + 1];
+        if (y + 1 < H) a.t1[(int64_t)(y + 1) * Wc + x] = u.s.t1[ly + 2][lx + 1];
         return;
     }
-    auto tap = [&](int dy, int dx) __attribute__((always_inline)) -> float {
-        const int yy = min(max(y + dy, 0), H - 1), xx = min(max(x + dx, 0), Wc - 1);
-        return t1[yy - (y0 - 1)][xx - (x0 - 1)];
-    };
-    const float med = median9(tap(-1, -1), tap(-1, 0), tap(-1, 1), tap(0, -1), tap(0, 0), tap(0, 1), tap(1, -1),
-                              tap(1, 0), tap(1, 1));
-    const int64_t o = (int64_t)y * Wc + x;
-    if (a.out_disp) a.out_disp[o] = med;
-    if (a.out_depth) {
-        const float adj = med + a.doffs;
-        float z = adj > a.eps ? __fdiv_rn(a.fB, adj) : __builtin_inff();
-        if (a.has_max && z > a.max_depth) z = a.max_depth;
-        a.out_depth[o] = z;
+    float t[4][3];
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int i = 0; i < 3; ++i) t[j][i] = u.s.t1[ly + j][lx + i];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        if (y + h >= H) break;
+        const float med = median9_cols(t[h][0], t[h + 1][0], t[h + 2][0], t[h][1], t[h + 1][1], t[h + 2][1], t[h][2],
+                                       t[h + 1][2], t[h + 2][2]);
+        const int64_t o = (int64_t)(y + h) * Wc + x;
+        if (a.out_disp) a.out_disp[o] = med;
+        if (a.out_depth) {
+            const float adj = med + a.doffs;
+            float z = adj > a.eps ? __fdiv_rn(a.fB, adj) : __builtin_inff();
+            if (a.has_max && z > a.max_depth) z = a.max_depth;
+            a.out_depth[o] = z;
+        }
     }
     pstamp(a.tl_tail, 6);
 }
@@ -830,7 +992,7 @@ size_t spk_pool_ints(int H, int Wc) {
 
 bool post_full_two_launch(const PostFullArgs &a) {
     const int Wc = a.W - a.crop;
-    return a.kernel / 2 <= kTailR && a.max_speckle <= kBfsMaxSpeckle && !a.in16 && a.newv == 0 &&
+    return a.kernel / 2 <= kTailR && a.max_speckle <= kBfsMaxSpeckle && a.newv == 0 && a.H < 65536 && Wc < 65536 &&
            spk_pool_ints(a.H, Wc) < (size_t)kPend && getenv("DSX_POST_LEGACY") == nullptr;
 }
 
@@ -838,8 +1000,9 @@ size_t post_full_workspace(int H, int W, int crop) {
     const int Wc = W > crop ? W - crop : 0;
     const size_t n = (size_t)H * (size_t)Wc;
     const auto r = [](size_t b) { return (b + 255) & ~(size_t)255; };
-    // parent, count, root, lsz | v16 | t0, t1 | code | pool | hole filling
-    return r(n * 4) * 4 + r(n * 2) + r(n * 4) * 2 + r(n * 4) + r(spk_pool_ints(H, Wc) * 4) + inpaint_workspace(H, Wc);
+    // parent, count, root, lsz | v16 | t0, t1 | code | pool | code16 | hole filling
+    return r(n * 4) * 4 + r(n * 2) + r(n * 4) * 2 + r(n * 4) + r(spk_pool_ints(H, Wc) * 4) + r(n * 2) +
+           inpaint_workspace(H, Wc);
 }
 
 hipError_t launch_post_full(PostFullArgs a, void *ws, hipStream_t st, LaunchHook *hook) {
@@ -856,7 +1019,8 @@ hipError_t launch_post_full(PostFullArgs a, void *ws, hipStream_t st, LaunchHook
     a.t1 = reinterpret_cast<float *>(w + 4 * r(n * 4) + r(n * 2) + r(n * 4));
     a.code = reinterpret_cast<int *>(w + 4 * r(n * 4) + r(n * 2) + 2 * r(n * 4));
     a.pool = reinterpret_cast<int *>(w + 4 * r(n * 4) + r(n * 2) + 3 * r(n * 4));
-    uint8_t *inpaint_ws = w + 4 * r(n * 4) + r(n * 2) + 3 * r(n * 4) + r(spk_pool_ints(a.H, Wc) * 4);
+    a.code16 = reinterpret_cast<int16_t *>(w + 4 * r(n * 4) + r(n * 2) + 3 * r(n * 4) + r(spk_pool_ints(a.H, Wc) * 4));
+    uint8_t *inpaint_ws = w + 4 * r(n * 4) + r(n * 2) + 3 * r(n * 4) + r(spk_pool_ints(a.H, Wc) * 4) + r(n * 2);
     const auto mark = [&](const char *name) {
         if (hook) hook->before(name, st);
     };
@@ -869,7 +1033,7 @@ hipError_t launch_post_full(PostFullArgs a, void *ws, hipStream_t st, LaunchHook
     const bool fill = a.fill_radius > 0;
     if (post_full_two_launch(a)) {
         const dim3 g1((Wc + kSpTX - 1) / kSpTX, (a.H + kSpTY - 1) / kSpTY);
-        const dim3 g2((Wc + kTailTX - 1) / kTailTX, (a.H + kTailTY - 1) / kTailTY);
+        const dim3 g2((Wc + kT3X - 1) / kT3X, (a.H + kT3Y - 1) / kT3Y);
         const char *tlp = getenv("DSX_POST_TIMELINE");  // diagnostics: per-block phase stamps to a file
         const size_t n1 = (size_t)g1.x * g1.y * 16, n2 = (size_t)g2.x * g2.y * 16;
         a.tl_tile = a.tl_tail = nullptr;
@@ -884,7 +1048,10 @@ hipError_t launch_post_full(PostFullArgs a, void *ws, hipStream_t st, LaunchHook
         if (e != hipSuccess) return e;
         a.tail_t1 = fill ? 1 : 0;
         mark("post_tail");
-        hipLaunchKernelGGL(post_tail2, g2, dim3(kTailTX * kTailTY), (size_t)4 * (a.max_speckle + 1) * sizeof(int), st, a);
+        const size_t dyn = (size_t)4 * (a.max_speckle + 1) * sizeof(int);
+        const int rr = a.kernel / 2;
+        auto tail = rr == 0 ? post_tail3<0> : rr == 1 ? post_tail3<1> : rr == 2 ? post_tail3<2> : post_tail3<3>;
+        hipLaunchKernelGGL(tail, g2, dim3(256), dyn, st, a);
         e = done();
         if (a.tl_tile) {
             std::vector<uint64_t> host(n1 + n2 + 2);

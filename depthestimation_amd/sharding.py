@@ -39,11 +39,28 @@ class DistEnv:
                    int(os.environ.get("WORLD_SIZE", 1)))
 
 
-def init_distributed(backend: Optional[str] = None) -> DistEnv:
+def _free_port() -> int:
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def init_distributed(backend: Optional[str] = None, single_rank_group: bool = False) -> DistEnv:
     """Initialise the default process group when WORLD_SIZE > 1 (RCCL when a GPU is
-    present, gloo otherwise). Idempotent."""
+    present, gloo otherwise). With ``single_rank_group`` a one-rank group is created as well
+    (outside torch.distributed.run too: a local rendezvous on 127.0.0.1), so the job's
+    collectives run through the same backend at N = 1 (bench.py). Idempotent."""
     env = DistEnv.from_env()
-    if env.world_size > 1:
+    if single_rank_group and env.world_size == 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", str(_free_port()))
+        os.environ.setdefault("RANK", "0")
+        os.environ.setdefault("LOCAL_RANK", "0")
+        os.environ.setdefault("WORLD_SIZE", "1")
+    if env.world_size > 1 or single_rank_group:
         import torch
         import torch.distributed as dist
         if not dist.is_initialized():
@@ -94,7 +111,7 @@ def broadcast_calibration(params: Optional[Dict], device=None, src: int = 0) -> 
     import torch
     import torch.distributed as dist
     vec = pack_calibration(params or {})
-    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+    if not (dist.is_available() and dist.is_initialized()):
         return unpack_calibration(vec)
     t = torch.from_numpy(vec).to(device if device is not None else "cpu")
     dist.broadcast(t, src=src)

@@ -182,3 +182,13 @@ def test_process_pair_timing_breakdown():
     m.close()
     for k in ("bm_pass_left", "lr_fixup", "speckle_tile", "post_tail"):
         assert k in kt and kt[k][1] == 3, kt
+
+
+def test_sentinel_value_round_trips():
+    """x16 values of exactly -32768 (the 16-bit code's escape) keep their value."""
+    d = np.full((40, 130), -2048.0, np.float32)
+    d[:, 60:] = 7.0
+    d[5:9, 5:9] = 3.0
+    for maxsp in (10, 100):
+        got, _ = _dev_post(d, 0, maxsp, outl=False)
+        np.testing.assert_array_equal(got, _host(d, 0, maxsp, outl=False))

@@ -390,3 +390,24 @@ def test_gloo_world2_calibration_and_sharding():
     assert f0 == f1 == 700.0 and w0 == w1 == 64
     assert l0 == [0, 2, 4, 6, 8] and l1 == [1, 3, 5, 7]
     assert all0 == [2.0 * i for i in range(9)] and all1 is None
+
+
+def test_single_rank_group_runs_the_collectives_gloo():
+    """sharding.init_distributed(single_rank_group=True) outside torch.distributed.run: a one-rank
+    group on 127.0.0.1, so broadcast_calibration really runs the collective (bench.py at N = 1)."""
+    import subprocess
+    import sys
+    code = (
+        "import os\n"
+        "for k in ('WORLD_SIZE','RANK','LOCAL_RANK','MASTER_PORT','MASTER_ADDR'): os.environ.pop(k, None)\n"
+        "import torch.distributed as dist\n"
+        "from depthestimation_amd import sharding\n"
+        "env = sharding.init_distributed('gloo', single_rank_group=True)\n"
+        "assert dist.is_initialized() and dist.get_world_size() == 1 and env.world_size == 1\n"
+        "c = sharding.broadcast_calibration({'image_width': 640, 'baseline': 0.25})\n"
+        "assert c['image_width'] == 640 and c['baseline'] == 0.25\n"
+        "dist.destroy_process_group()\n"
+        "print('ok')\n")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    p = subprocess.run([sys.executable, "-c", code], cwd=root, capture_output=True, text=True, timeout=120)
+    assert p.returncode == 0 and "ok" in p.stdout, p.stderr[-2000:]

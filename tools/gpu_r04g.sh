@@ -1,0 +1,13 @@
+#!/bin/bash
+set -o pipefail
+mkdir -p gpurun_out
+T=${TAG:-r04g}
+timeout -k 10 600 python -u -m pytest -x -q --timeout 150 --timeout-method thread tests/test_gpu_post2.py tests/test_inpaint.py tests/test_gpu_host_api.py > gpurun_out/${T}_tests.txt 2>&1
+rc=$?; tail -3 gpurun_out/${T}_tests.txt; [ $rc -eq 0 ] || exit $rc
+for x in 0 1; do
+DSX_TAIL_XCD=$x timeout -k 10 240 python3 tools/post_timeline.py c4 c2r > gpurun_out/${T}_post_tl_x$x.json 2>&1 || { tail gpurun_out/${T}_post_tl_x$x.json; exit 1; }
+grep post_tail gpurun_out/${T}_post_tl_x$x.json | cut -c1-400
+DSX_TAIL_XCD=$x timeout -k 10 300 python3 tools/dropin_bench.py --configs c2r c4 > gpurun_out/${T}_dropin_x$x.json 2> gpurun_out/${T}_dropin.err || { tail -20 gpurun_out/${T}_dropin.err; exit 1; }
+cat gpurun_out/${T}_dropin_x$x.json | cut -c1-100,250-600
+done
+grep spk_tile gpurun_out/${T}_post_tl_x0.json

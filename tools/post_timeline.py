@@ -15,8 +15,8 @@ from depthestimation_amd.configs import CONFIGS, matcher_kwargs  # noqa: E402
 from depthestimation_amd.matcher import HipBlockMatcher, postprocess_full_device  # noqa: E402
 from depthestimation_amd.synthetic import stereo_pair  # noqa: E402
 
-PH = {"spk_tile": ["load+runs", "unions", "roots+open", "edges", "pool", "?", "codes"],
-      "post_tail2": ["codes", "pending", "rowsums", "t1", "->median", "median+store"]}
+PH = {"spk_tile": {1: "load+runs", 2: "unions", 3: "roots+open", 4: "pending", 7: "codes"},
+      "post_tail2": {1: "codes", 2: "pending", 3: "rowsums", 4: "t1", 5: "->median", 6: "median+store"}}
 
 
 def summarize(name, t):
@@ -30,8 +30,24 @@ def summarize(name, t):
            "start_spread_us": round((st.max() - t0) / 100, 2),
            "block_us_median": round(float(np.median(en - st)) / 100, 2),
            "block_us_p90": round(float(np.percentile(en - st, 90)) / 100, 2), "phases": {}}
+    # start-time histogram (1 us bins) and peak co-resident blocks per CU (XCC, SE, SH, CU from HW_ID)
+    rel = (st - t0) / 100.0
+    out["starts_per_us"] = np.bincount(np.minimum(rel.astype(int), 40)).tolist()
+    hw, xcc = t[:, 14], t[:, 15] & 0xF
+    cu = (xcc << 16) | (((hw >> 13) & 0x7) << 8) | (((hw >> 12) & 1) << 4) | ((hw >> 8) & 0xF)
+    peak = []
+    for c in np.unique(cu):
+        m = cu == c
+        ev = sorted([(s_, 1) for s_ in st[m]] + [(e_, -1) for e_ in en[m]], key=lambda x: (x[0], x[1]))
+        cur = best = 0
+        for _, d in ev:
+            cur += d
+            best = max(best, cur)
+        peak.append(best)
+    out["cus"] = int(len(peak))
+    out["peak_blocks_per_cu"] = [int(np.min(peak)), float(np.median(peak)), int(np.max(peak))]
     prev = t[:, 0]
-    for i, ph in enumerate(PH[name], 1):
+    for i, ph in PH[name].items():
         cur = t[:, i]
         ok = cur > 0
         if not ok.any():
