@@ -293,6 +293,13 @@ def main():
         selftest_launch(args)
         return
 
+    # exactly one line on stdout: libraries (RCCL's version banner at communicator init, ROCm
+    # warnings) write to fd 1 too, so fd 1 becomes stderr for the run and the JSON line goes to a
+    # duplicate of the original stdout
+    sys.stdout.flush()
+    json_out = os.fdopen(os.dup(1), "w")
+    os.dup2(2, 1)
+
     import torch
     from depthestimation_amd import sharding
     from depthestimation_amd.matcher import HipBlockMatcher
@@ -534,7 +541,7 @@ def main():
         result.update(sec)
         if not args.no_cpu_baseline and ws == 1:
             result["cpu_baseline"] = cpu_baseline(args, cfg, hostL[0], hostR[0])
-        print(json.dumps(result), flush=True)
+        print(json.dumps(result), file=json_out, flush=True)
 
     matcher.close()
     tmatcher.close()
