@@ -50,7 +50,7 @@ bool pick_geometry(const dsx_params &p, dsx::Geometry &g) {
         return e && *e == '1';
     }();
     const bool sad1 = !no_sad1 && cost == DSX_COST_SAD && D <= 64 && p.path == DSX_PATH_FUSED &&
-                      p.aggregation == DSX_AGG_NONE && p.lr_form == DSX_LR_FORM_BM;
+                      p.aggregation == DSX_AGG_NONE;
     const bool lane1 = cost == DSX_COST_SSD || sad1;  // one disparity per lane
     g.kind = cost == DSX_COST_SSD ? dsx::BM_SSD : (sad1 ? dsx::BM_SAD1 : dsx::BM_SAD);
     const int unit = lane1 ? 64 : 128;
@@ -243,9 +243,9 @@ int ensure_buffers(dsx_handle *h, int H, int W, bool host_staging, int nframes =
         DSX_HIP(hipMalloc(&h->dFixed, n * 2));
         DSX_HIP(hipMalloc(&h->dFloat, n * 4));
     }
-    const bool fused = h->p.path == DSX_PATH_FUSED && !h->p.aggregation && h->p.cost != DSX_COST_BT &&
-                       h->p.lr_form == DSX_LR_FORM_BM;
-    if (h->p.disp12_max_diff >= 0 && fused && h->lrFrames < nframes) {
+    const bool fused = h->p.path == DSX_PATH_FUSED && !h->p.aggregation && h->p.cost != DSX_COST_BT;
+    const bool lr_any = h->p.disp12_max_diff >= 0 || h->p.lr_form == DSX_LR_FORM_SGBM;  // OpenCV's form: always on
+    if (lr_any && fused && h->lrFrames < nframes) {
         (void)hipFree(h->lrKeys);
         (void)hipFree(h->dStar);
         h->lrKeys = nullptr;
@@ -464,8 +464,9 @@ int run(dsx_handle *h, const void *dL, const void *dR, int H, int W, int64_t str
     const bool bt = h->p.cost == DSX_COST_BT;  // BT costs exist only as a volume
     // sgbm_post: the matcher writes int16 maps into postIn, the tail then writes the outputs
     void *const finalFixed = outFixed, *const finalFloat = outFloat;
-    const bool fused = h->p.path == DSX_PATH_FUSED && !h->p.aggregation && !bt && h->p.lr_form == DSX_LR_FORM_BM;
-    const bool scratch = h->p.disp12_max_diff >= 0 || !fused || h->p.sgbm_post;
+    const bool fused = h->p.path == DSX_PATH_FUSED && !h->p.aggregation && !bt;
+    const bool lr_sg = h->p.lr_form == DSX_LR_FORM_SGBM;  // OpenCV's LR form (always on)
+    const bool scratch = h->p.disp12_max_diff >= 0 || lr_sg || !fused || h->p.sgbm_post;
     if (scratch && h->scratchPending && h->scratchStream != st) DSX_HIP(hipStreamWaitEvent(st, h->scratchDone, 0));
     ScratchRecord rec_(h, st, scratch);  // on every exit once launches may have been enqueued
     if (h->p.sgbm_post) {
@@ -473,7 +474,7 @@ int run(dsx_handle *h, const void *dL, const void *dR, int H, int W, int64_t str
         outFloat = nullptr;
     }
     if (fused) {
-        const bool lr = h->p.disp12_max_diff >= 0;
+        const bool lr = h->p.disp12_max_diff >= 0 && !lr_sg;
         dsx::Bm2Args a = base_args(h, H, W, stride);
         a.side = dsx::SIDE_LEFT;
         a.ref = static_cast<const uint8_t *>(dL);
@@ -494,8 +495,18 @@ int run(dsx_handle *h, const void *dL, const void *dR, int H, int W, int64_t str
             a.dstar = h->dStar;
             a.kshift = h->g.kind != dsx::BM_SAD ? h->g.DB : 16;  // u32 layouts: (C << DB) | d
         } else {
+            if (lr_sg) {
+                // OpenCV's form: unique winners scatter (cost, d) into this call's key half, which
+                // lr_fixup_sgbm tests afterwards; the pass resets the other half (consumed by the
+                // previous call's fix-up) for the next call, and keeps its x16 outputs in dStar
+                a.sg_keys = h->lrKeys + (size_t)h->lrParity * H * W * h->lrFrames;
+                a.lr_reset = h->lrKeys + (size_t)(h->lrParity ^ 1) * H * W * h->lrFrames;
+                a.lr_reset_n = (int64_t)H * W * h->lrDirty[h->lrParity ^ 1];
+                a.dstar = h->dStar;
+                a.kshift = h->g.kind != dsx::BM_SAD ? h->g.DB : 16;
+            }
             // only strips meeting the valid band [m + D - 1, W - 1 + m] need a search
-            // (stereo_core.py:168 crops the rest)
+            // (stereo_core.py:168 crops the rest; OpenCV's band lies inside it)
             const int xlo = std::max(0, h->p.min_disp + h->p.num_disp - 1);
             const int xhi = std::min(W - 1, W - 1 + h->p.min_disp);
             if (xlo > xhi) {
@@ -512,6 +523,15 @@ int run(dsx_handle *h, const void *dL, const void *dR, int H, int W, int64_t str
         if (tl) DSX_HIP(hipMemsetAsync(tl, 0, 12 * 8 * 65536, st));
         a.timeline = tl;
         DSX_LAUNCH(h, "bm_pass_left", st, dsx::launch_bm2(radius, h->g.kind, h->g.NW, a, st));
+        if (lr_sg) {
+            const int P = h->lrParity;
+            DSX_LAUNCH(h, "lr_fixup_sgbm", st,
+                       dsx::launch_lr_fixup_sgbm(h->dStar, a.sg_keys, H * nframes, W, h->p.min_disp,
+                                                 h->p.disp12_max_diff, a.kshift, a.out_fixed, a.out_float, st));
+            h->lrDirty[P ^ 1] = 0;
+            h->lrDirty[P] = nframes;
+            h->lrParity = P ^ 1;
+        }
         if (lr) {
             // this call dirties nframes frames of half P; its left pass has reset every dirty frame
             // of the other half (consumed by the previous call), however many frames that call had

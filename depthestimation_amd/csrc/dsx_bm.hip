@@ -909,7 +909,9 @@ __device__ __forceinline__ void bm2_segment(const Bm2Args &a_in, uint8_t *smem, 
             if constexpr (side == 1) {
                 if (h == 0 && x < W) a.out_dR[o] = cb == padv ? (int16_t)-1 : (int16_t)b;
             } else {
-                bool valid = x < W && x >= m + D - 1 && x <= W - 1 + m;
+                // valid band: A5' [m + D - 1, W - 1 + m]; OpenCV's form (sg_keys) [max(m + D, 0), W + min(m, 0))
+                bool valid = a.sg_keys ? (x < W && x >= max(m + D, 0) && x < W + min(m, 0))
+                                       : (x < W && x >= m + D - 1 && x <= W - 1 + m);
                 if (a.uniq > 0) {
                     const int rel = b - h * DSL;
                     uint32_t nm = 0xFFFFFFFFu;
@@ -969,6 +971,14 @@ __device__ __forceinline__ void bm2_segment(const Bm2Args &a_in, uint8_t *smem, 
                 if (h == 0 && x < W) {
                     if (lr_on && !(DSX_EXP & 8)) a.dstar[o] = valid ? (int16_t)b : (int16_t)-1;  // LR check: lr_fixup
                     const int16_t fx = valid ? (int16_t)(m * 16 + f) : (int16_t)((m - 1) * 16);
+                    if (side == 0 && a.sg_keys) {
+                        // OpenCV's LR form: a unique winner offers (cost, d) to right pixel x - m - d
+                        // (min cost, then max d); lr_fixup_sgbm tests against them afterwards
+                        a.dstar[o] = fx;
+                        if (valid)
+                            atomicMin(a.sg_keys + fout + (long)y * W + (x - m - b),
+                                      (cb << a.kshift) | (((1u << a.kshift) - 1u) - (uint32_t)b));
+                    }
                     if (a.out_fixed) a.out_fixed[o] = fx;
                     if (a.out_float) a.out_float[o] = a.float_mode == 0 ? (float)fx * 0.0625f : (valid ? pf : (float)(m - 1));
                 }
@@ -1014,11 +1024,12 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu((SSD &&
             const long o = (long)y * W + x;
             if (a.out_fixed) a.out_fixed[o] = fi;
             if (a.out_float) a.out_float[o] = (float)(m - 1);
+            if (side == 0 && a.sg_keys) a.dstar[o] = fi;  // lr_fixup_sgbm reads every pixel
         }
     }
 
     // ---- LR pass: reset the other key half (the previous call's keys, already checked) ----
-    if (side == 3 && a.lr_reset_n > 0) {
+    if ((side == 3 || side == 0) && a.lr_reset_n > 0) {
         uint32_t *kr = a.lr_reset;
         const int64_t n = a.lr_reset_n, stride = (int64_t)gridDim.x * NT;
         const int64_t t0 = (int64_t)blockIdx.x * NT + tid;

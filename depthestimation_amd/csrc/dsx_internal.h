@@ -42,7 +42,9 @@ struct Bm2Args {
     const int *part;     // device: block b owns linear (frame, strip, row) units [part[b], part[b+1])
     uint32_t *lr_keys;     // left pass with LR: per-pixel right-view winner keys (C << kshift | d),
     int kshift;            //   filled by atomicMin (memset to ~0 first)
-    int16_t *dstar;        // left pass with LR: winning d (or -1) for lr_fixup
+    int16_t *dstar;        // left pass with LR: winning d (or -1) for lr_fixup; with sg_keys: the x16 output
+    uint32_t *sg_keys;     // left pass (side 0), OpenCV's LR form: per right pixel the min key
+                           //   (cost << kshift | (kmask - d)) over the unique left winners mapping to it
     uint32_t *lr_reset;    // left pass with LR: the other key half, reset to ~0 here for the next call
     int64_t lr_reset_n;    //   (keys the previous call's lr_fixup consumed)
     int16_t *out_fixed;    // left pass outputs (either may be null)
@@ -91,6 +93,12 @@ hipError_t launch_volume_wta(int TX, bool ssd, const VolArgs &a, hipStream_t st)
 // pass resets the other half).
 hipError_t launch_lr_fixup(const int16_t *dstar, const uint32_t *keys, uint32_t *keys_next, int reset_rows, int rows,
                            int W, int m, int lr, int kshift, int16_t *out_fixed, float *out_float, hipStream_t st);
+// OpenCV's LR form after a side-0 left pass with sg_keys (DSX_LR_FORM_SGBM on the fused path): the floor
+// and the ceiling of each sub-pixel disparity (fixed, the pass's x16 output kept in `fixed`) are tested
+// against disp2 from the keys; a pixel is dropped when both land inside the image on a disp2 entry
+// differing by more than max(lr, 1).  Writes out_fixed / out_float of the dropped pixels only.
+hipError_t launch_lr_fixup_sgbm(const int16_t *fixed, const uint32_t *keys, int rows, int W, int m, int lr,
+                                int kshift, int16_t *out_fixed, float *out_float, hipStream_t st);
 
 size_t volume_smem_bytes(int TX, bool ssd, int Dp, int TPP, int W);
 

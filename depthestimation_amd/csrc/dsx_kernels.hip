@@ -353,6 +353,66 @@ hipError_t launch_lr_fixup(const int16_t *dstar, const uint32_t *keys, uint32_t 
     return hipGetLastError();
 }
 
+// OpenCV's LR form on the fused path (after a side-0 pass with sg_keys), 8 pixels per thread: the
+// 16-B load of the x16 outputs, then the floor / ceiling key gathers of all 8 in flight together.
+// The keys are this call's half (never written here); the next left pass resets the other half.
+__global__ __launch_bounds__(256) void lr_fixup_sgbm(const int16_t *__restrict__ fixed, const uint32_t *__restrict__ keys,
+                                                   int64_t n, int W, int m, int lr, int kshift, int16_t *out_fixed,
+                                                   float *out_float) {
+    const uint32_t mask = (1u << kshift) - 1u;
+    const int inv = (m - 1) * 16, d12 = lr > 0 ? lr : 1;
+    const int64_t i0 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 8;
+    if (i0 >= n) return;
+    int f8[8];
+    if (i0 + 8 <= n) {
+        const uint4 v = *reinterpret_cast<const uint4 *>(fixed + i0);
+        const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            f8[2 * j] = (int16_t)(w[j] & 0xFFFFu);
+            f8[2 * j + 1] = (int16_t)(w[j] >> 16);
+        }
+    } else {
+        for (int j = 0; j < 8; ++j) f8[j] = i0 + j < n ? fixed[i0 + j] : inv;
+    }
+    uint32_t kl[8], kh[8];
+    int xs[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        const int64_t i = i0 + j;
+        const int x = (int)(i % W);
+        xs[j] = x;
+        const int xl = x - (f8[j] >> 4), xh = x - ((f8[j] + 15) >> 4);
+        const bool on = f8[j] != inv;
+        kl[j] = on && xl >= 0 && xl < W ? keys[i - x + xl] : 0xFFFFFFFFu;
+        kh[j] = on && xh >= 0 && xh < W ? keys[i - x + xh] : 0xFFFFFFFFu;
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        if (f8[j] == inv) continue;
+        const int lo = f8[j] >> 4, hi = (f8[j] + 15) >> 4;
+        auto fails = [&](uint32_t key, int dq) __attribute__((always_inline)) {
+            if (key == 0xFFFFFFFFu) return false;  // no winner maps there (or outside the image)
+            const int d2 = m + (int)(mask - (key & mask));
+            return d2 - dq > d12 || dq - d2 > d12;
+        };
+        if (fails(kl[j], lo) && fails(kh[j], hi)) {
+            if (out_fixed) out_fixed[i0 + j] = (int16_t)inv;
+            if (out_float) out_float[i0 + j] = (float)(m - 1);
+        }
+    }
+    (void)xs;
+}
+
+hipError_t launch_lr_fixup_sgbm(const int16_t *fixed, const uint32_t *keys, int rows, int W, int m, int lr, int kshift,
+                                int16_t *out_fixed, float *out_float, hipStream_t st) {
+    const int64_t n = (int64_t)rows * W;
+    const int64_t work = (n + 7) / 8;
+    hipLaunchKernelGGL(lr_fixup_sgbm, dim3((unsigned)((work + 255) / 256)), dim3(256), 0, st, fixed, keys, n, W, m, lr,
+                       kshift, out_fixed, out_float);
+    return hipGetLastError();
+}
+
 // ---------------------------------------------------------------------------------------
 // Host-side dispatch
 // ---------------------------------------------------------------------------------------

@@ -11,8 +11,10 @@ import pytest
 from depthestimation_amd import postprocess as pp
 
 
-def _loop_inpaint(img, hole, radius):
-    """Per-pixel, per-layer loop form of the layered Telea marching (plain Python floats)."""
+def _loop_inpaint(img, hole, radius, row_sums=True):
+    """Per-pixel, per-layer loop form of the layered Telea marching (plain Python floats).
+    row_sums=False: the round-2 summation order (every window cell in row-major order into one
+    float64 sum), kept as a second, independent oracle for the sums."""
     H, W = img.shape
     out = [[float(v) for v in row] for row in np.asarray(img, np.float32)]
     INF = 1 << 40
@@ -48,11 +50,11 @@ def _loop_inpaint(img, hole, radius):
             gx = (tr - tl) * 0.5 if (orr and ol) else (tr - tp if orr else (tp - tl if ol else 0.0))
             gy = (td - tu) * 0.5 if (od and ou) else (td - tp if od else (tp - tu if ou else 0.0))
             num = den = 0.0
-            for oyr in range(-radius, radius + 1):  # window rows, each summed from 0.0
+            for oyr in (range(-radius, radius + 1) if row_sums else [None]):  # window rows, each from 0.0
                 rn = rd = 0.0
                 for oy, ox in offs:
                     qy, qx = y + oy, x + ox
-                    if oy != oyr or not (0 <= qy < H and 0 <= qx < W) or layer[qy][qx] >= k:
+                    if (row_sums and oy != oyr) or not (0 <= qy < H and 0 <= qx < W) or layer[qy][qx] >= k:
                         continue
                     ry, rx = -oy, -ox
                     d2 = ry * ry + rx * rx
@@ -82,6 +84,24 @@ def test_layered_inpaint_matches_loop_restatement(shape, radius, seed):
     d = _holey(*shape, seed)
     np.testing.assert_array_equal(pp.fill_holes(d, method="inpaint", kernel_size=radius),
                                   _loop_inpaint(d, d <= 0, radius))
+
+
+def _ulps(a, b):
+    a = np.asarray(a, np.float32).view(np.int32).astype(np.int64)
+    b = np.asarray(b, np.float32).view(np.int32).astype(np.int64)
+    return np.abs(a - b)
+
+
+@pytest.mark.parametrize("shape,radius,seed", [((12, 17), 3, 1), ((9, 23), 5, 2), ((15, 11), 1, 3), ((20, 30), 3, 5),
+                                               ((25, 19), 3, 6)])
+def test_row_sum_order_within_one_ulp_of_offset_order(shape, radius, seed):
+    """The row-blocked float64 sums the GPU reproduces (lane per window row) against the round-2
+    offset-order sums: at most 1 float32 ulp apart on every filled pixel (the oracle was
+    reordered to match the kernel; this keeps the old order as an independent check)."""
+    d = _holey(*shape, seed)
+    a = pp.fill_holes(d, method="inpaint", kernel_size=radius)
+    b = _loop_inpaint(d, d <= 0, radius, row_sums=False)
+    assert _ulps(a, b).max() <= 1
 
 
 def test_inpaint_edge_cases():
@@ -114,6 +134,16 @@ def test_fill_holes_device_matches_host(shape, radius, seed):
     ref = pp.fill_holes(d, method="inpaint", kernel_size=radius)
     got = fill_holes_device(torch.from_numpy(d).cuda(), radius=radius)
     np.testing.assert_array_equal(got.cpu().numpy(), ref)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("shape,radius,seed", [((20, 30), 3, 5), ((25, 19), 3, 6), ((9, 23), 5, 2)])
+def test_fill_holes_device_within_one_ulp_of_offset_order(shape, radius, seed):
+    import torch
+    from depthestimation_amd.matcher import fill_holes_device
+    d = _holey(*shape, seed)
+    got = fill_holes_device(torch.from_numpy(d).cuda(), radius=radius).cpu().numpy()
+    assert _ulps(got, _loop_inpaint(d, d <= 0, radius, row_sums=False)).max() <= 1
 
 
 @pytest.mark.gpu

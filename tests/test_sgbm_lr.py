@@ -128,3 +128,66 @@ def test_gpu_sgbm_shaped_matcher_with_tail():
     C = aggregate(cost_volume_bt(L, R, 0, 64, 5, 31), "sgbm_3way", 200, 800)
     want = sgbm_post(wta_sgbm(C, 0, 10, 1, True)["fixed"], 0, 50, 2)
     np.testing.assert_array_equal(got, want.astype(np.float32) / 16.0)
+
+
+FUSED_CASES = [  # H, W, m, D, bs, cost, uniqueness, disp12 - every fused layout: SAD1 (D <= 64), SAD pairs
+    (40, 150, 0, 64, 5, "sad", 10, 1),       # (1 and 2 waves), SSD (1, 2, 4 waves), min_disp offsets
+    (33, 260, 0, 128, 9, "sad", 10, 1),
+    (21, 300, 2, 160, 7, "sad", 0, 2),
+    (30, 140, -3, 48, 11, "ssd", 10, 0),
+    (25, 330, 0, 200, 5, "ssd", 15, 1),
+    (18, 120, 5, 16, 3, "sad", 10, -1),
+    (9, 40, 0, 64, 5, "sad", 10, 1),         # D > W: nothing valid
+]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", FUSED_CASES, ids=lambda c: f"{c[5]}_{c[0]}x{c[1]}_m{c[2]}_D{c[3]}_bs{c[4]}")
+@pytest.mark.parametrize("fmode", ["fixed", "parabola"])
+def test_gpu_sgbm_lr_form_fused_pass(case, fmode):
+    """OpenCV's LR form on the fused pass (side-0 scatter of the unique winners + lr_fixup_sgbm),
+    bit for bit with oracle/sgbm_post.wta_sgbm on the same block costs; twice through one handle
+    (the key halves alternate and are reset by the next pass)."""
+    _gpu()
+    import torch
+    from depthestimation_amd.matcher import HipBlockMatcher
+    H, W, m, D, bs, cost, u, d12 = case
+    L, R, _ = stereo_pair(H, W, m, D, seed=H * 7 + W)
+    want = wta_sgbm(cost_volume(L, R, m, D, bs, cost), m, u, d12, True)["fixed"]
+    mm = HipBlockMatcher(min_disp=m, num_disp=D, block_size=bs, cost=cost, uniqueness_ratio=u, disp12_max_diff=d12,
+                         lr_form="sgbm", path="fused", float_mode=fmode, timing=True)
+    dL, dR = torch.from_numpy(L).cuda(), torch.from_numpy(R).cuda()
+    for _ in range(3):
+        fx = torch.empty((H, W), dtype=torch.int16, device="cuda")
+        mm.compute_device(dL, dR, out_fixed=fx)
+        torch.cuda.synchronize()
+        np.testing.assert_array_equal(fx.cpu().numpy(), want)
+    kt = mm.kernel_times()
+    mm.close()
+    assert "bm_pass_left" in kt and "lr_fixup_sgbm" in kt and "volume_wta" not in kt
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("config", ["c4", "c2r"])
+def test_gpu_sgbm_lr_form_fused_at_config_width(config):
+    """A 24-row band of a BASELINE-size frame (full width, the config's D and window) through the
+    fused OpenCV form, and a 3-frame batch of it, against the oracle."""
+    _gpu()
+    import torch
+    from depthestimation_amd.configs import CONFIGS
+    from depthestimation_amd.matcher import HipBlockMatcher
+    cfg = CONFIGS[config]
+    W, D, bs = cfg["W"], cfg["num_disp"], cfg["block_size"]
+    L, R, _ = stereo_pair(24, W, 0, D, seed=5)
+    want = wta_sgbm(cost_volume(L, R, 0, D, bs, "sad"), 0, 10, 1, True)["fixed"]
+    mm = HipBlockMatcher(num_disp=D, block_size=bs, uniqueness_ratio=10, disp12_max_diff=1, lr_form="sgbm")
+    got = mm.compute(L, R)
+    np.testing.assert_array_equal(got, want)
+    bL = torch.from_numpy(np.stack([L, L, L])).cuda()
+    bR = torch.from_numpy(np.stack([R, R, R])).cuda()
+    out = torch.empty((3, 24, W), dtype=torch.int16, device="cuda")
+    mm.compute_batch_device(bL, bR, out_fixed=out)
+    torch.cuda.synchronize()
+    mm.close()
+    for f in range(3):
+        np.testing.assert_array_equal(out[f].cpu().numpy(), want)

@@ -1,0 +1,58 @@
+"""The heap-ordered Telea oracle (oracle/telea_heap.py): cv2.inpaint's march
+order (depthlib/postprocess.py:102-105) restated with the per-pixel arithmetic of the layered form
+the GPU runs.  Pinned here by an independent queue form and by the single-layer case, where the two
+orders must agree with the layered restatement bit for bit."""
+from __future__ import annotations
+
+import numpy as np
+import pytest
+
+from depthestimation_amd import postprocess as pp
+from oracle.telea_heap import telea_heap, telea_heap_list
+
+
+def _holey(H, W, seed, frac=0.15):
+    rng = np.random.default_rng(seed)
+    d = (20 + 10 * np.sin(np.arange(W) / 7.0)[None, :] + rng.integers(0, 4, (H, W)) / 16.0).astype(np.float32)
+    d[rng.random((H, W)) < frac] = 0.0
+    d[H // 3:H // 3 + 4, W // 4:W // 4 + 6] = 0.0
+    return d
+
+
+@pytest.mark.parametrize("seed,radius", [(0, 3), (1, 1), (2, 5), (3, 3), (4, 2)])
+def test_heap_forms_agree(seed, radius):
+    d = _holey(14, 23, seed)
+    np.testing.assert_array_equal(telea_heap(d, d <= 0, radius), telea_heap_list(d, d <= 0, radius))
+
+
+@pytest.mark.parametrize("radius", [1, 3])
+def test_single_layer_equals_layered(radius):
+    """Isolated hole pixels more than 2r apart: one distance layer, no hole pixel sees another, so
+    the heap order and the layered march compute the same thing."""
+    rng = np.random.default_rng(7)
+    d = (10 + rng.integers(0, 64, (30, 41)) / 16.0).astype(np.float32)
+    for y in range(3, 30, 2 * radius + 3):
+        for x in range(2, 41, 2 * radius + 4):
+            d[y, x] = 0.0
+    hole = d <= 0
+    np.testing.assert_array_equal(telea_heap(d, hole, radius), pp._telea_inpaint(d, hole, radius))
+
+
+def test_known_answers_and_edges():
+    d = np.full((5, 5), 7.5, np.float32)
+    d[2, 2] = 0.0
+    assert telea_heap(d, d <= 0, 3)[2, 2] == np.float32(7.5)  # constant surroundings
+    z = np.zeros((4, 6), np.float32)
+    np.testing.assert_array_equal(telea_heap(z, z <= 0, 3), z)  # nothing known: nothing filled
+    k = np.arange(12, dtype=np.float32).reshape(3, 4) + 1
+    np.testing.assert_array_equal(telea_heap(k, k <= 0, 3), k)  # no hole
+
+
+def test_orders_differ_inside_a_layer():
+    """A wide hole: the heap order fills pixels of one distance layer from each other, so it can
+    differ from the layered march (the divergence tools/telea_divergence.py measures)."""
+    d = _holey(24, 30, 11, frac=0.0)
+    d[4:20, 5:25] = 0.0
+    h, lay = telea_heap(d, d <= 0, 3), pp._telea_inpaint(d, d <= 0, 3)
+    assert (h[d > 0] == lay[d > 0]).all()
+    assert np.all(np.isfinite(h)) and np.abs(h - lay).max() < 5.0

@@ -16,7 +16,7 @@ for c in ${CONFIGS:-c2r c4 c3}; do
   for v in $LIBS; do
     if [ $v = new ]; then L=$GRAFT_REPO_ROOT/depthestimation_amd/libdsx.so; else L=$GRAFT_REPO_ROOT/$v; fi
     n=$(basename $v .so)
-    r=$(DSX_LIB=$L timeout -k 5 180 python bench.py --config $c --steps ${STEPS:-500} --warmup 300 --no-cpu-baseline --no-volume-roofline --no-e2e --no-post --no-batched --no-ref-defaults $EXTRA 2>$O/err_${c}_$n.txt) || { echo "FAIL $c $v"; tail -5 $O/err_${c}_$n.txt; exit 1; }
+    r=$(DSX_LIB=$L timeout -k 5 180 python bench.py --config $c --steps ${STEPS:-500} --warmup 300 --no-cpu-baseline --no-volume-roofline --no-e2e --no-post --no-batched --no-ref-defaults --no-dropin $EXTRA 2>$O/err_${c}_$n.txt) || { echo "FAIL $c $v"; tail -5 $O/err_${c}_$n.txt; exit 1; }
     echo "$c $n $(echo "$r" | python -c "import json,sys;d=json.loads(sys.stdin.read().strip().splitlines()[-1]);print(d['value'], d['parity']['mismatches'], d['roofline'].get('kernels_ms'))")" | tee -a $O/ab.txt
   done
 done
