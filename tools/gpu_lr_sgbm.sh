@@ -1,9 +1,11 @@
 #!/bin/bash
+# OpenCV's LR form on the fused pass: its GPU tests + the full-size config and parity suites, a same-box
+# A/B of the headline configs against tools/explib/libdsx_base.so, and bm-vs-sgbm LR kernel times.
 set -o pipefail
 mkdir -p gpurun_out
-timeout -k 10 600 python -u -m pytest -x -q --timeout 150 --timeout-method thread tests/test_sgbm_lr.py tests/test_gpu_configs.py tests/test_gpu_parity.py > gpurun_out/r04i_tests.txt 2>&1
-rc=$?; tail -3 gpurun_out/r04i_tests.txt; [ $rc -eq 0 ] || exit $rc
-CONFIGS="c2 c2r c4" REPS=2 STEPS=1000 bash tools/lib_ab.sh r04i_ab tools/explib/libdsx_base.so
+timeout -k 10 600 python -u -m pytest -x -q --timeout 150 --timeout-method thread tests/test_sgbm_lr.py tests/test_gpu_configs.py tests/test_gpu_parity.py > gpurun_out/lr_sgbm_tests.txt 2>&1
+rc=$?; tail -3 gpurun_out/lr_sgbm_tests.txt; [ $rc -eq 0 ] || exit $rc
+CONFIGS="c2 c2r c4" REPS=2 STEPS=1000 bash tools/lib_ab.sh lr_sgbm_ab tools/explib/libdsx_base.so
 for lf in sgbm; do
 python3 - <<'PY'
 import torch, time, json, sys
