@@ -165,6 +165,9 @@ struct dsx_handle {
     int postFrames = 0;
     float *ppDisp = nullptr;    // dsx_process_pair_device: the matcher's float map (H x W, fast mode)
     int16_t *ppFixed = nullptr; // dsx_process_pair_device: the matcher's x16 map (H x W, full mode)
+    const uint32_t *lastKeys = nullptr;  // the last fused call's LR key half (run, defer_lr)
+    const int16_t *lastDstar = nullptr;
+    int lastKshift = 0;
     void *ppWs = nullptr;       // dsx_process_pair_device: post-processing workspace
     size_t ppWsBytes = 0;
     uint32_t *sgmS = nullptr;  // SGM path sums [H][W][Dp] u32 (sequential directions)
@@ -457,8 +460,11 @@ int run_right_pass(dsx_handle *h, const void *dL, const void *dR, int H, int W, 
 }
 
 // nframes frames: inputs frame_stride bytes apart, outputs (and LR buffers) H * W elements apart
+// defer_lr (dsx_process_pair_device): the fused pass's left-right check is left to the caller's next
+// kernel (spk_tile applies it while loading the map): no lr_fixup launch; h->lastKeys / lastDstar
+// name this call's key half and winners.
 int run(dsx_handle *h, const void *dL, const void *dR, int H, int W, int64_t stride, void *outFixed, void *outFloat,
-        hipStream_t st, int nframes = 1, int64_t frame_stride = 0) {
+        hipStream_t st, int nframes = 1, int64_t frame_stride = 0, bool defer_lr = false) {
     const int radius = h->p.block_size / 2;
     const bool ssd = h->p.cost == DSX_COST_SSD;
     const bool bt = h->p.cost == DSX_COST_BT;  // BT costs exist only as a volume
@@ -523,11 +529,15 @@ int run(dsx_handle *h, const void *dL, const void *dR, int H, int W, int64_t str
         if (tl) DSX_HIP(hipMemsetAsync(tl, 0, 12 * 8 * 65536, st));
         a.timeline = tl;
         DSX_LAUNCH(h, "bm_pass_left", st, dsx::launch_bm2(radius, h->g.kind, h->g.NW, a, st));
+        h->lastKeys = lr_sg ? a.sg_keys : (lr ? a.lr_keys : nullptr);
+        h->lastDstar = h->dStar;
+        h->lastKshift = a.kshift;
         if (lr_sg) {
             const int P = h->lrParity;
-            DSX_LAUNCH(h, "lr_fixup_sgbm", st,
-                       dsx::launch_lr_fixup_sgbm(h->dStar, a.sg_keys, H * nframes, W, h->p.min_disp,
-                                                 h->p.disp12_max_diff, a.kshift, a.out_fixed, a.out_float, st));
+            if (!defer_lr)
+                DSX_LAUNCH(h, "lr_fixup_sgbm", st,
+                           dsx::launch_lr_fixup_sgbm(h->dStar, a.sg_keys, H * nframes, W, h->p.min_disp,
+                                                     h->p.disp12_max_diff, a.kshift, a.out_fixed, a.out_float, st));
             h->lrDirty[P ^ 1] = 0;
             h->lrDirty[P] = nframes;
             h->lrParity = P ^ 1;
@@ -536,10 +546,12 @@ int run(dsx_handle *h, const void *dL, const void *dR, int H, int W, int64_t str
             // this call dirties nframes frames of half P; its left pass has reset every dirty frame
             // of the other half (consumed by the previous call), however many frames that call had
             const int P = h->lrParity;
-            DSX_LAUNCH(h, "lr_fixup", st,
-                       dsx::launch_lr_fixup(h->dStar, a.lr_keys, a.lr_reset,
-                                            DSX_RESET_LEFT ? 0 : H * h->lrDirty[P ^ 1], H * nframes, W, h->p.min_disp,
-                                            h->p.disp12_max_diff, a.kshift, a.out_fixed, a.out_float, st));
+            if (!defer_lr || !DSX_RESET_LEFT)
+                DSX_LAUNCH(h, "lr_fixup", st,
+                           dsx::launch_lr_fixup(h->dStar, a.lr_keys, a.lr_reset,
+                                                DSX_RESET_LEFT ? 0 : H * h->lrDirty[P ^ 1], H * nframes, W,
+                                                h->p.min_disp, h->p.disp12_max_diff, a.kshift, a.out_fixed,
+                                                a.out_float, st));
             h->lrDirty[P ^ 1] = 0;
             h->lrDirty[P] = nframes;
             h->lrParity = P ^ 1;
@@ -1010,23 +1022,40 @@ int dsx_process_pair_device(dsx_handle *h, const void *dL, const void *dR, int32
     // the float map and the workspace are handle scratch: order after the previous call's use
     if (h->scratchPending && h->scratchStream != st) DSX_HIP(hipStreamWaitEvent(st, h->scratchDone, 0));
     ScratchRecord rec_(h, st, true);
-    // full mode reads the x16 map itself (postprocess.py:27 computes int16(d * 16) of d = fixed / 16,
-    // which is `fixed` again): 2 B per pixel written by the matcher and read by the speckle pass
-    rc = run(h, dL, dR, H, W, stride_bytes, full ? h->ppFixed : nullptr, full ? nullptr : h->ppDisp, st);
-    if (rc) return rc;
-    rec_.active = true;  // run() recorded its own event; this call's kernels continue below
     const float fB = (float)(pp->focal_length * pp->baseline);
-    if (pp->mode == DSX_POST_FULL) {
-        dsx::PostFullArgs a{};
+    dsx::PostFullArgs a{};
+    bool defer = false;
+    if (full) {
+        // full mode reads the x16 map itself (postprocess.py:27 computes int16(d * 16) of d = fixed / 16,
+        // which is `fixed` again): 2 B per pixel written by the matcher and read by the speckle pass
         a.in16 = h->ppFixed;
         a.in_pitch = W;
         a.H = H;
         a.W = W;
         a.crop = crop;
         a.max_speckle = pp->max_speckle_size;
+        a.kernel = pp->outlier_kernel;
+        // the fused pass's LR check moves into the speckle pass's loads (no lr_fixup launch) when that
+        // pass is the two-launch form and the matcher is the fused pass with a check
+        const bool fusedp = h->p.path == DSX_PATH_FUSED && !h->p.aggregation && h->p.cost != DSX_COST_BT &&
+                            !h->p.sgbm_post;
+        const bool lrc = h->p.lr_form == DSX_LR_FORM_SGBM || h->p.disp12_max_diff >= 0;
+        defer = fusedp && lrc && dsx::post_full_two_launch(a) && getenv("DSX_NO_DEFER_LR") == nullptr;
+    }
+    rc = run(h, dL, dR, H, W, stride_bytes, full ? h->ppFixed : nullptr, full ? nullptr : h->ppDisp, st, 1, 0, defer);
+    if (rc) return rc;
+    rec_.active = true;  // run() recorded its own event; this call's kernels continue below
+    if (full) {
+        if (defer) {
+            a.lr_keys = h->lastKeys;
+            a.lr_dstar = h->lastDstar;
+            a.lr_form = h->p.lr_form == DSX_LR_FORM_SGBM ? 1 : 0;
+            a.lr_m = h->p.min_disp;
+            a.lr_max = h->p.disp12_max_diff;
+            a.lr_kshift = h->lastKshift;
+        }
         a.max_diff16 = (int)(pp->max_diff * 16);  // int(max_diff * 16), postprocess.py:30
         a.apply_outliers = pp->apply_outlier_removal ? 1 : 0;
-        a.kernel = pp->outlier_kernel;
         a.thr = (float)pp->outlier_threshold;
         a.out_disp = static_cast<float *>(d_out_disp);
         a.out_depth = depth ? static_cast<float *>(d_out_depth) : nullptr;

@@ -166,6 +166,12 @@ struct PostFullArgs {
     // kSent: see `code` = the full 32-bit code), and the per-tile pending-node pool
     int16_t *code16;
     int *code, *pool;
+    // the matcher's left-right check applied while the speckle pass loads the x16 map (the drop-in call
+    // skips the lr_fixup launch): lr_keys != null -> A5' form (lr_form 0: lr_dstar = winner d or -1,
+    // |key d - d| > lr_max drops the pixel) or OpenCV's form (1: floor / ceiling test, lr_dstar unused)
+    const int16_t *lr_dstar;
+    const uint32_t *lr_keys;
+    int lr_form, lr_m, lr_max, lr_kshift;
     // diagnostics (DSX_POST_TIMELINE): per block 16 u64 - s_memrealtime after each phase, hw / xcc id
     uint64_t *tl_tile, *tl_tail;
 };

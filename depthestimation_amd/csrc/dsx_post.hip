@@ -482,8 +482,33 @@ __device__ __forceinline__ int lane_up(int v) { return __builtin_amdgcn_update_d
 // thread issue back to back)
 __device__ __forceinline__ int spk_val_nb(const PostFullArgs &a, int Wc, int y, int x) {
     const bool in = y >= 0 && y < a.H && x >= 0 && x < Wc;
-    const int64_t q = (int64_t)min(max(y, 0), a.H - 1) * a.in_pitch + a.crop + min(max(x, 0), Wc - 1);
-    const int v = a.in16 ? (int)a.in16[q] : (int)(int16_t)(int)__builtin_truncf(a.disp[q] * 16.0f);
+    const int yc = min(max(y, 0), a.H - 1), xc = a.crop + min(max(x, 0), Wc - 1);  // xc: uncropped column
+    const int64_t row = (int64_t)yc * a.in_pitch, q = row + xc;
+    int v = a.in16 ? (int)a.in16[q] : (int)(int16_t)(int)__builtin_truncf(a.disp[q] * 16.0f);
+    if (a.lr_keys) {
+        // the left-right check of lr_fixup / lr_fixup_sgbm on this pixel (keys of its row, uncropped)
+        const uint32_t mask = (1u << a.lr_kshift) - 1u;
+        const int inv = (a.lr_m - 1) * 16;
+        if (a.lr_form == 0) {
+            const int b = a.lr_dstar[q];
+            if (b >= 0) {
+                const int df = (int)(a.lr_keys[row + xc - a.lr_m - b] & mask) - b;
+                if (df > a.lr_max || df < -a.lr_max) v = inv;
+            }
+        } else if (v != inv) {
+            const int d12 = a.lr_max > 0 ? a.lr_max : 1;
+            const int lo = v >> 4, hi = (v + 15) >> 4, xl = xc - lo, xh = xc - hi;
+            const int W = a.W;
+            const uint32_t kl = xl >= 0 && xl < W ? a.lr_keys[row + xl] : 0xFFFFFFFFu;
+            const uint32_t kh = xh >= 0 && xh < W ? a.lr_keys[row + xh] : 0xFFFFFFFFu;
+            auto fails = [&](uint32_t key, int dq) __attribute__((always_inline)) {
+                if (key == 0xFFFFFFFFu) return false;
+                const int d2 = a.lr_m + (int)(mask - (key & mask));
+                return d2 - dq > d12 || dq - d2 > d12;
+            };
+            if (fails(kl, lo) && fails(kh, hi)) v = inv;
+        }
+    }
     return in ? v : a.newv;
 }
 

@@ -96,6 +96,6 @@ def test_bench_default_n1_dropin_and_unsettled():
         r = d["dropin"][c]
         assert r["parity"]["mismatches"] == 0, r
         assert r["value"] > 0 and r["post_processing_ms"] > 0
-        for k in ("bm_pass_left", "lr_fixup", "speckle_tile", "post_tail"):
+        for k in ("bm_pass_left", "speckle_tile", "post_tail"):
             assert k in r["kernels_ms"], r["kernels_ms"]
     assert d["unsettled"]["value"] > 0

@@ -180,8 +180,29 @@ def test_process_pair_timing_breakdown():
     torch.cuda.synchronize()
     kt = m.kernel_times()
     m.close()
-    for k in ("bm_pass_left", "lr_fixup", "speckle_tile", "post_tail"):
+    for k in ("bm_pass_left", "speckle_tile", "post_tail"):
         assert k in kt and kt[k][1] == 3, kt
+    assert "lr_fixup" not in kt  # the LR check runs inside speckle_tile's loads (deferred)
+
+
+@pytest.mark.parametrize("lr_form", ["bm", "sgbm"])
+@pytest.mark.parametrize("defer", ["1", "0"])
+def test_process_pair_lr_check_deferred_into_speckle_pass(lr_form, defer, monkeypatch):
+    """The drop-in call applies the matcher's LR check (A5' or OpenCV's form) in spk_tile's loads
+    instead of an lr_fixup launch; with DSX_NO_DEFER_LR the fix-up kernel runs: both equal the host
+    _process_pair, over several calls through one handle (alternating key halves)."""
+    import torch
+    if defer == "0":
+        monkeypatch.setenv("DSX_NO_DEFER_LR", "1")
+    core = StereoCore()
+    core.configure_sgbm(num_disp=64, block_size=5, focal_length=700.0, baseline=0.1, lr_form=lr_form)
+    for seed in (71, 72, 73):
+        L, R, _ = stereo_pair(80, 280, 0, 64, seed=seed)
+        hd, hz = core._process_pair(L, R)
+        dd, dz = core.process_pair_device(torch.from_numpy(L).cuda(), torch.from_numpy(R).cuda())
+        torch.cuda.synchronize()
+        np.testing.assert_array_equal(dd.cpu().numpy(), hd)
+        np.testing.assert_array_equal(dz.cpu().numpy(), hz)
 
 
 def test_sentinel_value_round_trips():
