@@ -634,6 +634,34 @@ def secondaries(args, cfg, rk, matcher, frames, hostL, hostR, allL, allR, out_fi
                 refdef["roofline"] = vr
         mr.close()
         mrt.close()
+        # the same checks in cv2.StereoSGBM's own LR form (lr_form 'sgbm', stereo_core.py:69): the unique
+        # winners scatter into disp2 from the fused pass's epilogue, then lr_fixup_sgbm (floor / ceiling)
+        ms = HipBlockMatcher(device=rk.dev_index, path="fused", lr_form="sgbm", **kwr)
+        mst = HipBlockMatcher(device=rk.dev_index, path="fused", timing=True, lr_form="sgbm", **kwr)
+        for i in range(100):
+            fl, fr = frames[i % len(frames)]
+            ms.compute_device(fl, fr, out_fixed=out_fixed[0], out_float=out_float[0], stream=stream)
+        torch.cuda.synchronize(dev)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        for i in range(nr):
+            fl, fr = frames[i % len(frames)]
+            ms.compute_device(fl, fr, out_fixed=out_fixed[0], out_float=out_float[0], stream=stream)
+        e1.record(stream)
+        torch.cuda.synchronize(dev)
+        for i in range(30):
+            fl, fr = frames[i % len(frames)]
+            mst.compute_device(fl, fr, out_fixed=out_fixed[0], out_float=out_float[0], stream=stream)
+        torch.cuda.synchronize(dev)
+        gms = e0.elapsed_time(e1) / nr
+        refdef["lr_form_sgbm"] = {
+            "gpu_ms_per_step": round(gms, 5), "value": round(H * W / (gms * 1e-3) / 1e6, 1),
+            "unit": "Mpix/s (GPU time per step)",
+            "kernels_ms": {k: round(v[0], 5) for k, v in mst.kernel_times().items()},
+            "note": "the same checks in OpenCV's left-right form (disp2 from the unique left winners, floor/ceiling "
+                    "test; lr_form 'sgbm'): fused pass + lr_fixup_sgbm; kernels_ms from a timing handle"}
+        ms.close()
+        mst.close()
         out["c2_reference_defaults"] = refdef
 
     # the reference's per-frame steps after the matcher on the device (SURVEY 8f F1/F2 and hole
