@@ -513,8 +513,6 @@ __device__ __forceinline__ int spk_val_nb(const PostFullArgs &a, int Wc, int y, 
 }
 
 __global__ __launch_bounds__(256) void spk_tile(PostFullArgs a) {
-    __shared__ int16_t vl[kSpN];   // d16
-    __shared__ int16_t lb[kSpN];   // run start (local index) of each pixel
     __shared__ int16_t rt[kSpN];   // component root (local index), -1 for newv pixels
     __shared__ int pl[kSpN];       // union-find parents of run starts; later the roots' pool offsets
     __shared__ int cnt[kSpN];      // size | kOpen at roots
@@ -531,40 +529,48 @@ __global__ __launch_bounds__(256) void spk_tile(PostFullArgs a) {
     // the ring pixel of this lane (wave 0: row above, 1: row below, 2: column left, 3: column right)
     const int ry = w == 0 ? y0 - 1 : w == 1 ? y0 + kSpTY : y0 + (lane & (kSpTY - 1));
     const int rx = w < 2 ? gx : w == 2 ? x0 - 1 : x0 + kSpTX;
+    // every load in flight at once: the wave's 4 rows, the row above them (the previous wave's last
+    // row - its runs are recomputed here, so the unions need no LDS copy of another wave's labels) and
+    // the ring pixel
     int v[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) v[i] = spk_val_nb(a, Wc, y0 + 4 * w + i, gx);
+    const int vprev = spk_val_nb(a, Wc, y0 + 4 * w - 1, gx);
     const int ring = spk_val_nb(a, Wc, ry, rx);
-    if (w == 0) rg_t[lane] = (int16_t)ring;
-    else if (w == 1) rg_b[lane] = (int16_t)ring;
-    else if (lane < kSpTY) (w == 2 ? rg_l : rg_r)[lane] = (int16_t)ring;
-    if (threadIdx.x == 0) used = 0;
-    const uint64_t le = lane == 63 ? ~0ull : ((2ull << lane) - 1ull);  // lanes <= this one
-    uint64_t S[4];
-    int lab[4];
+    // identity parents (unions only ever link run starts, finds only start at run starts): no value
+    // dependency, so this overlaps the loads
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-        const int r = 4 * w + i, li = r * kSpTX + lane;
-        const int left = lane_up(v[i]);  // outside any lane-dependent branch: DPP needs its source lane active
-        const bool hj = lane > 0 && joins(left, v[i], md, nv);
-        S[i] = __ballot(!hj);
-        lab[i] = r * kSpTX + 63 - __clzll((long long)(S[i] & le));
-        vl[li] = (int16_t)v[i];
-        lb[li] = (int16_t)lab[i];
-        pl[li] = lab[i];
+        const int li = (4 * w + i) * kSpTX + lane;
+        pl[li] = li;
         cnt[li] = 0;
         ecn[li] = 0;
     }
-    __syncthreads();
+    if (threadIdx.x == 0) used = 0;
+    if (w == 0) rg_t[lane] = (int16_t)ring;
+    else if (w == 1) rg_b[lane] = (int16_t)ring;
+    else if (lane < kSpTY) (w == 2 ? rg_l : rg_r)[lane] = (int16_t)ring;
+    const uint64_t le = lane == 63 ? ~0ull : ((2ull << lane) - 1ull);  // lanes <= this one
+    auto run_label = [&](int val, int r, uint64_t &Sr) __attribute__((always_inline)) {
+        const int left = lane_up(val);  // outside any lane-dependent branch: DPP needs its source lane active
+        const bool hj = lane > 0 && joins(left, val, md, nv);
+        Sr = __ballot(!hj);
+        return r * kSpTX + 63 - __clzll((long long)(Sr & le));
+    };
+    uint64_t S[4], Sp;
+    int lab[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) lab[i] = run_label(v[i], 4 * w + i, S[i]);
+    const int labp = run_label(vprev, 4 * w - 1, Sp);  // wave 0: the ring row (never used)
+    __syncthreads();  // parents initialised
     pstamp(a.tl_tile, 1);
-    // vertical joins: one union per (run below, run above) pair (the first column of the pair); the
-    // row above is this wave's previous row except for the wave's first row
+    // vertical joins: one union per (run below, run above) pair (the first column of the pair)
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
         const int r = 4 * w + i;
         if (r == 0) continue;
-        const int up = i ? v[i - 1] : vl[(r - 1) * kSpTX + lane];
-        const int ul = i ? lab[i - 1] : lb[(r - 1) * kSpTX + lane];
+        const int up = i ? v[i - 1] : vprev;
+        const int ul = i ? lab[i - 1] : labp;
         const bool vj = joins(up, v[i], md, nv);
         const int pvj = lane_up((int)vj), pla = lane_up(lab[i]), pul = lane_up(ul);
         const bool dup = lane > 0 && pvj && pla == lab[i] && pul == ul;
@@ -646,7 +652,8 @@ __global__ __launch_bounds__(256) void spk_tile(PostFullArgs a) {
                 bool dup = false;
                 if (r > 0) {
                     const int pli = (r - 1) * kSpTX + lane;
-                    dup = rt[pli] == root[i] && joins(vl[pli], rg[r - 1], md, nv) && joins(rg[r - 1], rv, md, nv);
+                    const int pv = i ? v[i - 1] : vprev;  // this lane's pixel of the previous row
+                    dup = rt[pli] == root[i] && joins(pv, rg[r - 1], md, nv) && joins(rg[r - 1], rv, md, nv);
                 }
                 if (e && !dup && pend(cnt[root[i]])) {
                     sSlot[i] = atomicAdd(&ecn[root[i]], 1);

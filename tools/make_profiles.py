@@ -25,8 +25,14 @@ SIDES = {"0": "bm_pass_left", "3": "bm_pass_left", "1": "bm_pass_right", "2": "c
 def short(k):
     if "vol_wta" in k:
         return "volume_wta"
+    if "lr_fixup_sgbm" in k:
+        return "lr_fixup_sgbm"
     if "lr_fixup" in k:
         return "lr_fixup"
+    if "spk_tile" in k:
+        return "speckle_tile"
+    if "post_tail3" in k:
+        return "post_tail"
     m = re.search(r"bm2<\s*\d+,\s*\w+,\s*\d+,\s*(\d)", k)
     return SIDES[m.group(1)] if m else k
 
