@@ -456,13 +456,6 @@ constexpr int kOpen = 1 << 20;     // tile component size word: leaves the tile 
 constexpr int kBfsMaxSpeckle = 2047;  // visited lists of 4 waves x (max + 1) ints in LDS
 constexpr int kHash = 1024;           // pending-node table of a tail block (>= 2x its 16 x 40 region)
 
-__device__ __forceinline__ int spk_val(const PostFullArgs &a, int Wc, int y, int x) {
-    if (y < 0 || y >= a.H || x < 0 || x >= Wc) return a.newv;
-    const int64_t q = (int64_t)y * a.in_pitch + a.crop + x;
-    if (a.in16) return a.in16[q];
-    return (int16_t)(int)__builtin_truncf(a.disp[q] * 16.0f);
-}
-
 // DSX_POST_TIMELINE diagnostics: thread 0 stamps the 100 MHz real-time counter after phase `i`
 __device__ __forceinline__ void pstamp(uint64_t *tl, int i) {
     if (tl && threadIdx.x == 0) {
@@ -478,8 +471,8 @@ __device__ __forceinline__ void pstamp(uint64_t *tl, int i) {
 // the value one lane up (lane 0: its own) - DPP wave_shr:1, no LDS round trip
 __device__ __forceinline__ int lane_up(int v) { return __builtin_amdgcn_update_dpp(v, v, 0x138, 0xF, 0xF, false); }
 
-// spk_val without branches around the load: clamped address, newv outside the image (all loads of a
-// thread issue back to back)
+// d16 of pixel (y, x) of the cropped map (newv outside the image) without branches around the load: a
+// clamped address, so all loads of a thread issue back to back
 __device__ __forceinline__ int spk_val_nb(const PostFullArgs &a, int Wc, int y, int x) {
     const bool in = y >= 0 && y < a.H && x >= 0 && x < Wc;
     const int yc = min(max(y, 0), a.H - 1), xc = a.crop + min(max(x, 0), Wc - 1);  // xc: uncropped column
