@@ -787,7 +787,8 @@ def dropin_figures(rk, dev, stream) -> dict:
             d0, _ = core.estimate_depth_device(pairs[0][2], pairs[0][3], stream=stream)
             torch.cuda.synchronize(dev)
             got = d0.cpu().numpy()
-            want = postprocess_disparity(CRef()(pairs[0][0], pairs[0][1], **matcher_kwargs(cfg))["disp"][:, D:],
+            th = max(1, min(16, cpu_threads_available() // rk.ws))  # the ranks share this host's CPUs
+            want = postprocess_disparity(CRef()(pairs[0][0], pairs[0][1], nthreads=th, **matcher_kwargs(cfg))["disp"][:, D:],
                                          max_speckle_size=100, max_diff=1.0, outlier_threshold=2.5,
                                          apply_outlier_removal=True, apply_hole_filling=False)
             mism = rk.allreduce(int(np.count_nonzero(got != want)), "sum")
