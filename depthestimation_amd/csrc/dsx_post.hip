@@ -923,6 +923,21 @@ __global__ __launch_bounds__(256, 8) void post_tail3(PostFullArgs a) {
         wide = bigs;
     }
     pstamp(a.tl_tail, 2);
+    if (a.out16) {
+        // cv2.StereoSGBM's own tail (launch_sgbm_post): the median ran before the speckles; write the
+        // speckle-filtered x16 map (and / 16) - int16 out16 / float out_disp, no crop
+        const int lx = tid & 31, ly = 2 * (tid >> 5);
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const int x = x0 + lx, y = y0 + ly + h;
+            if (x >= Wc || y >= H) continue;
+            const int v = iv[ly + h + 1 + R][lx + 1 + R];
+            const int64_t o = (int64_t)y * Wc + x;
+            a.out16[o] = (int16_t)v;
+            if (a.out_disp) a.out_disp[o] = (float)v * 0.0625f;
+        }
+        return;
+    }
     const bool outl = a.apply_outliers != 0;
     if (outl && !wide) {
         for (int q = tid; q < RH * W1; q += 256) {
@@ -1021,7 +1036,8 @@ size_t spk_pool_ints(int H, int Wc) {
 
 bool post_full_two_launch(const PostFullArgs &a) {
     const int Wc = a.W - a.crop;
-    return a.kernel / 2 <= kTailR && a.max_speckle <= kBfsMaxSpeckle && a.newv == 0 && a.H < 65536 && Wc < 65536 &&
+    return a.kernel / 2 <= kTailR && a.max_speckle <= kBfsMaxSpeckle && (a.newv == 0 || a.out16) && a.H < 65536 &&
+           Wc < 65536 &&
            spk_pool_ints(a.H, Wc) < (size_t)kPend && getenv("DSX_POST_LEGACY") == nullptr;
 }
 
@@ -1161,7 +1177,8 @@ hipError_t launch_post_full(PostFullArgs a, void *ws, hipStream_t st, LaunchHook
 size_t sgbm_post_workspace(int H, int W) {
     const size_t n = (size_t)H * W;
     const auto r = [](size_t b) { return (b + 255) & ~(size_t)255; };
-    return r(n * 2) + r(n * 4) * 4 + r(n * 2);  // median | parent, count, root, lsz | v16
+    // median | parent, count, root, lsz | v16 | code16 | code | pool
+    return r(n * 2) + r(n * 4) * 4 + r(n * 2) + r(n * 2) + r(n * 4) + r(spk_pool_ints(H, W) * 4);
 }
 
 hipError_t launch_sgbm_post(const int16_t *in, int H, int W, int newv, int max_speckle, int max_diff16, int16_t *out16,
@@ -1191,6 +1208,16 @@ hipError_t launch_sgbm_post(const int16_t *in, int H, int W, int newv, int max_s
     a.root = reinterpret_cast<int *>(w + r(n * 2) + 2 * r(n * 4));
     a.lsz = reinterpret_cast<int *>(w + r(n * 2) + 3 * r(n * 4));
     a.v16 = reinterpret_cast<int16_t *>(w + r(n * 2) + 4 * r(n * 4));
+    a.code16 = reinterpret_cast<int16_t *>(w + r(n * 2) + 4 * r(n * 4) + r(n * 2));
+    a.code = reinterpret_cast<int *>(w + r(n * 2) + 4 * r(n * 4) + 2 * r(n * 2));
+    a.pool = reinterpret_cast<int *>(w + r(n * 2) + 4 * r(n * 4) + 2 * r(n * 2) + r(n * 4));
+    a.kernel = 1;  // no outlier stage: post_tail3<0> writes the speckle-filtered map (out16 set)
+    if (post_full_two_launch(a)) {
+        hipLaunchKernelGGL(spk_tile, dim3((W + kSpTX - 1) / kSpTX, (H + kSpTY - 1) / kSpTY), dim3(256), 0, st, a);
+        hipLaunchKernelGGL(post_tail3<0>, dim3((W + kT3X - 1) / kT3X, (H + kT3Y - 1) / kT3Y), dim3(256),
+                           (size_t)4 * (max_speckle + 1) * sizeof(int), st, a);
+        return hipGetLastError();
+    }
     const int grid = (int)std::min<size_t>((n + 255) / 256, 4096);
     const int ntx = (W + kCcTX - 1) / kCcTX, nty = (H + kCcTY - 1) / kCcTY;
     hipLaunchKernelGGL(speckle_local, dim3(ntx, nty), dim3(256), 0, st, a);
