@@ -53,6 +53,12 @@
 #ifndef DSX_WPE_SSD
 #define DSX_WPE_SSD 4
 #endif
+#ifndef DSX_INIT_SB  // SSD segment init: scheduling barrier between column chunks
+#define DSX_INIT_SB 1
+#endif
+#ifndef DSX_SSD_LDSDIAG  // SSD LR pass (NW >= 2): right-view winners read from the finished tile
+#define DSX_SSD_LDSDIAG 1
+#endif
 
 #include <algorithm>
 #include <cstdio>
@@ -94,6 +100,32 @@ __device__ __forceinline__ uint32_t min_shr1(uint32_t src, uint32_t key) {
     return key;
 }
 __host__ __device__ constexpr int rnd16(int v) { return (v + 15) & ~15; }
+template <int N, typename F, int... I>
+__device__ __forceinline__ void static_for_impl(F &&f, std::integer_sequence<int, I...>) {
+    (f(std::integral_constant<int, I>{}), ...);
+}
+template <int N, typename F>
+__device__ __forceinline__ void static_for(F &&f) {
+    static_for_impl<N>(f, std::make_integer_sequence<int, N>{});
+}
+// A = min(A, ka) in the lanes of m, B = min(B, kb) in the others: the lane split as exec masks (a
+// constant SGPR pair), 2 VALU instead of 2 selects + 2 minima.  exec is restored before the asm ends.
+// The mask is built inside (lanes below 64 - K: ~0 >> K), so hipcc cannot hoist 32 of them out of
+// the row loop as 64 SGPRs.
+template <int K>
+__device__ __forceinline__ void min_split(uint32_t &A, uint32_t &B, uint32_t ka, uint32_t kb) {
+    uint64_t sv, m;
+    asm volatile(
+        "s_lshr_b64 %[m], -1, %[k]\n\t"
+        "s_and_saveexec_b64 %[sv], %[m]\n\t"
+        "v_min_u32 %[A], %[A], %[ka]\n\t"
+        "s_andn2_b64 exec, %[sv], %[m]\n\t"
+        "v_min_u32 %[B], %[B], %[kb]\n\t"
+        "s_mov_b64 exec, %[sv]"
+        : [A] "+v"(A), [B] "+v"(B), [sv] "=&s"(sv), [m] "=&s"(m)
+        : [k] "n"(K), [ka] "v"(ka), [kb] "v"(kb)
+        : "scc");
+}
 
 template <int R, bool SSD, int NW>
 struct Geo {
@@ -193,7 +225,7 @@ __device__ __forceinline__ Bm2Args kargs_row(const Bm2Args &a) {
 
 template <int R, bool SSD, int NW, int SIDE, bool FAST, bool ABS, bool LRFULL>
 __device__ __forceinline__ void bm2_segment(const Bm2Args &a_in, uint8_t *smem, int x0, int yb, int ye, long fin, long fout,
-                                            bool lr_on, int done0, const int (&pe)[3], int &qcur
+                                            bool lr_on, int done0, const int (&pe)[3], int &qcur, int wvu
 #ifdef DSX_STAMPS
                                             , uint64_t (&ph)[8], uint64_t &t_prev, uint64_t &nsteps
 #endif
@@ -203,7 +235,9 @@ __device__ __forceinline__ void bm2_segment(const Bm2Args &a_in, uint8_t *smem, 
                   PITCH = G::PITCH, NJ = G::NJ, SLOT = G::SLOT, NB = G::NB, NJ4 = (NJ + 3) / 4,
                   NCH = (NC + 7) / 8;
     constexpr int side = SIDE;
-    const Bm2Args &a = a_in;
+    // the LR pass reloads the launch arguments per segment too: values derived from them in the
+    // segment prologue would otherwise be hoisted out of the block's segment loop and spilled
+    const Bm2Args a = kargs_row<SIDE == 3 && DSX_KARG>(a_in);
     // FSS: SSD sums in f32.  Squared differences, column sums and (offset) box sums are integers
     // below 2^24, so v_sub_f32 / v_fma_f32 / v_add_f32 (full rate, ~2 cycles) are exact and
     // replace the quarter-rate v_mad_i32_i24.  Box sums carry a +2^23 offset: for box < 2^23
@@ -213,12 +247,19 @@ __device__ __forceinline__ void bm2_segment(const Bm2Args &a_in, uint8_t *smem, 
     // ABS (SAD1): SAD with the SSD layout (one disparity per lane, u32 column / box sums) for D <= 64,
     // where the packed pairs would leave half of the wave on padding disparities
     constexpr bool FSS = SSD && !ABS && R <= 5 && (SIDE == 0 || SIDE == 3);
+    // LDSD: the SSD LR pass takes the right-view winners from the finished tile in the epilogue
+    // (2 VALU per cost on most waves) instead of tracking the diagonals through the row loop (5)
+    constexpr bool LDSD = SIDE == 3 && SSD && !ABS && NW >= 2 && DSX_SSD_LDSDIAG;
     constexpr uint32_t OFF = FSS ? 0x4B000000u : 0u;
     typedef typename std::conditional<FSS, float, typename std::conditional<SSD, uint32_t, u16x2>::type>::type acc_t;
     uint8_t *tile = smem + 4 * SLOT;
 
-    const int tid = threadIdx.x;
-    const int wv = tid >> 6, ln = tid & 63;
+    // the lane index is rebuilt per segment from the wave index (an SGPR) and mbcnt: tid-derived
+    // values are then computed per segment instead of held (and spilled) across the whole kernel
+    int ln;  // mbcnt inside the asm: not hoisted out of the segment loop
+    asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(ln));
+    const int tid = (wvu << 6) + ln;
+    const int wv = wvu;
     const int H = a.H, W = a.W, m = a.m, D = a.D;
     const int64_t stride = a.stride;
     const int d0 = SSD ? (wv * 64 + ln) : (wv * 128 + 2 * ln);
@@ -530,6 +571,8 @@ __device__ __forceinline__ void bm2_segment(const Bm2Args &a_in, uint8_t *smem, 
                     }
                 }
             }
+            // SSD: one chunk's LDS words in flight at a time (hoisting them all spilled at 4 waves)
+            if constexpr (SSD && DSX_INIT_SB) __builtin_amdgcn_sched_barrier(0);
         }
     }
     }
@@ -649,7 +692,7 @@ __device__ __forceinline__ void bm2_segment(const Bm2Args &a_in, uint8_t *smem, 
                 if constexpr (SSD) acc += cs[c];
                 else acc = as2(as1(acc) + as1(cs[c]));
             }
-            if constexpr (side == 3) {
+            if constexpr (side == 3 && !LDSD) {
                 // Right-view winners along the tile's diagonals: C_R(xr, d) = C(xr + m + d, d), so
                 // right pixel xr collects keys (C << s | d) from (x, d) with x - m - d = xr.  Each
                 // lane keeps the running key minimum of the diagonal through its slot(s); moving to
@@ -984,6 +1027,58 @@ __device__ __forceinline__ void bm2_segment(const Bm2Args &a_in, uint8_t *smem, 
                 }
             }
         }
+        if constexpr (LDSD) {
+            // ---- right-view winners from the finished tile (SSD LR pass) ----
+            // Right pixel xr collects keys (C << s | d) from the tile entries (k, d) with
+            // x0 + k - m - d = xr, a diagonal of the tile.  Lane i follows the wrapped diagonal
+            // (k, (k + i) mod Dp), k = 0..TX-1 (consecutive lanes, consecutive banks): part A, d = k + i
+            // < Dp, belongs to xr = x0 - m - i; part B, the wrapped rest (k >= L = Dp - i, d = k - L),
+            // to xr = x0 - m + L.  Only the wave holding i > Dp - TX has B parts; it splits its lanes
+            // by exec masks, and the role rotates over the waves row by row.  Keys carry k in the low
+            // bits while minimising (same order as d along one diagonal) and d on the way out.
+            const int ks = a.kshift;
+            int wi = wv + (y % NW);
+            wi = wi >= NW ? wi - NW : wi;
+            const int i = wi * 64 + ln, L = Dp - i;
+            constexpr int DS = PITCH + 4;  // one pixel and one disparity further
+            const uint8_t *pa = tile + 4 * i, *pb = pa - 4 * Dp;
+            uint32_t A = 0xFFFFFFFFu, B = 0xFFFFFFFFu;
+            if constexpr (LRFULL) {
+                // 8 entries per group: bounded reads in flight (the row loop is at its VGPR budget)
+                if (__builtin_amdgcn_readfirstlane(wi) != NW - 1) {
+                    static_for<TX / 8>([&](auto g) __attribute__((always_inline)) {
+                        constexpr int k0 = 8 * decltype(g)::value;
+#pragma unroll
+                        for (int k = k0; k < k0 + 8; ++k)
+                            A = umin2(A, (*reinterpret_cast<const uint32_t *>(pa + k * DS) << ks) | (uint32_t)k);
+                        __builtin_amdgcn_sched_barrier(0);
+                    });
+                } else {
+                    // lanes ln < 64 - k are still on part A (L > k)
+                    static_for<TX>([&](auto kc) __attribute__((always_inline)) {
+                        constexpr int k = decltype(kc)::value;
+                        const uint32_t ca = *reinterpret_cast<const uint32_t *>(pa + k * DS);
+                        const uint32_t cb = *reinterpret_cast<const uint32_t *>(pb + k * DS);
+                        min_split<k>(A, B, (ca << ks) | (uint32_t)k, (cb << ks) | (uint32_t)k);
+                        if constexpr ((k & 7) == 7) __builtin_amdgcn_sched_barrier(0);
+                    });
+                }
+            } else {
+                // partial strip or D < Dp: per-entry bounds (x0 + k < W, d < D)
+                const int nA = min(min(L, D - i), W - x0);
+                const int bE = min(W - x0, D + L);
+                for (int k = 0; k < TX; ++k) {
+                    const uint32_t ca = *reinterpret_cast<const uint32_t *>(pa + k * DS);
+                    const uint32_t cb = *reinterpret_cast<const uint32_t *>(pb + k * DS);
+                    if (k < nA) A = umin2(A, (ca << ks) | (uint32_t)k);
+                    if (k >= L && k < bE) B = umin2(B, (cb << ks) | (uint32_t)k);
+                }
+            }
+            uint32_t *krow = a.lr_keys + fout + (long)y * W;
+            const int xa = x0 - m - i, xb = x0 - m + L;
+            if (A != 0xFFFFFFFFu && xa >= 0 && xa < W) atomicMin(krow + xa, A + (uint32_t)i);
+            if (B != 0xFFFFFFFFu && xb >= 0 && xb < W) atomicMin(krow + xb, B - (uint32_t)L);
+        }
         DSX_STAMP(5);
         if (more) {
             st(par ^ 2, pn0, pn1, pn2, pn3, pnr);
@@ -1002,9 +1097,10 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu((SSD &&
     constexpr int side = SIDE;
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const int tid = threadIdx.x;
+    const int wvu = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int H = a.H, W = a.W, m = a.m;
-    uint64_t t_start = 0;
-    if (a.timeline && tid == 0) t_start = __builtin_amdgcn_s_memrealtime();
+    // block timeline: the start stamp goes out at once (nothing held live across the segments)
+    if (a.timeline && wvu == 0 && __lane_id() == 0) a.timeline[4 * blockIdx.x] = __builtin_amdgcn_s_memrealtime();
 #ifdef DSX_STAMPS
     uint64_t ph[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     uint64_t t_prev = 0;
@@ -1070,9 +1166,9 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu((SSD &&
                           x0 - R >= 0 && x0 - R + 4 * ((NC + 3) / 4) - 1 <= W - 1;
 #ifdef DSX_STAMPS
 #define DSX_SEG(FASTV, FULLV) \
-    bm2_segment<R, SSD, NW, SIDE, FASTV, ABS, FULLV>(a, smem, x0, yb, ye, fin, fout, lr_on, done0, pe, qcur, ph, t_prev, nsteps)
+    bm2_segment<R, SSD, NW, SIDE, FASTV, ABS, FULLV>(a, smem, x0, yb, ye, fin, fout, lr_on, done0, pe, qcur, wvu, ph, t_prev, nsteps)
 #else
-#define DSX_SEG(FASTV, FULLV) bm2_segment<R, SSD, NW, SIDE, FASTV, ABS, FULLV>(a, smem, x0, yb, ye, fin, fout, lr_on, done0, pe, qcur)
+#define DSX_SEG(FASTV, FULLV) bm2_segment<R, SSD, NW, SIDE, FASTV, ABS, FULLV>(a, smem, x0, yb, ye, fin, fout, lr_on, done0, pe, qcur, wvu)
 #endif
         // LR pass: strips inside the image with D == Dp take the check-free diagonal loop
         const bool lrfull = side == 3 && x0 + TX <= W && a.D == G::Dp;
@@ -1085,10 +1181,9 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu((SSD &&
         }
 #undef DSX_SEG
     }
-    if (a.timeline && tid == 0) {
+    if (a.timeline && wvu == 0 && __lane_id() == 0) {
         const uint64_t t_end = __builtin_amdgcn_s_memrealtime();
         uint64_t *tl = a.timeline + 4 * blockIdx.x;
-        tl[0] = t_start;
         tl[1] = t_end;
         tl[2] = (uint64_t)__builtin_amdgcn_s_getreg((4 << 0) | (0 << 6) | (31 << 11));   // HW_REG_HW_ID
         tl[3] = (uint64_t)__builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (15 << 11));  // HW_REG_XCC_ID
@@ -1160,7 +1255,9 @@ static hipError_t bm2_partition_dev(const PartKey &k, int TX, const int **out) {
 template <int R, bool SSD, int NW, int SIDE, bool ABS = false>
 static hipError_t launch_bm2_side(const Bm2Args &a, hipStream_t st) {
     using G = Geo<R, SSD, NW>;
-    constexpr int SM = G::SMEM + ((SIDE == 3 && (SSD ? DSX_SSD_XB : DSX_XB4)) ? 128 * NW : 0);  // + the LR exit region
+    // + the LR exit region; the LDS-diagonal SSD LR pass reads up to TX * 4 - 24 B past the tile
+    constexpr bool LDSD = SIDE == 3 && SSD && !ABS && NW >= 2 && DSX_SSD_LDSDIAG;
+    constexpr int SM = G::SMEM + ((SIDE == 3 && (SSD ? DSX_SSD_XB : DSX_XB4)) ? 128 * NW : 0) + (LDSD ? 128 : 0);
     const void *fn = (const void *)bm2<R, SSD, NW, SIDE, ABS>;
     static int blocks_per_cu[64] = {};
     static int num_cu[64] = {};

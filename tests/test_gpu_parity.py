@@ -139,6 +139,26 @@ def test_large_vs_c_oracle(torch_dev):
             np.testing.assert_array_equal(fixed, ref["fixed"])
 
 
+@pytest.mark.parametrize("D,W,m,bs,u,lr", [
+    (128, 224, 0, 5, 10, 1),    # 2 waves, D == Dp, full strips only
+    (128, 250, 3, 7, 0, 0),     # 2 waves, partial last strip
+    (192, 400, -2, 9, 10, 1),   # 3 waves
+    (256, 480, 0, 11, 10, 1),   # C3's shape: 4 waves (the LR-diagonal role rotates over rows)
+    (256, 455, 1, 13, 5, 2),    # 4 waves, u32 sums (R = 6), partial strip
+    (100, 233, 1, 9, 10, 1),    # D < Dp (padding disparities)
+    (230, 420, -4, 5, 0, 1),    # 4 waves, D < Dp, negative min disparity
+])
+def test_ssd_lr_shapes(torch_dev, D, W, m, bs, u, lr):
+    """SSD LR pass (right-view winners read from the finished tile, csrc/dsx_bm.hip LDSD) over the
+    wave counts, full / partial strips and padded disparity ranges, bit-exact with the oracle."""
+    H = 23
+    L, R, _ = stereo_pair(H, W, max(m, 0), D, seed=D + W)
+    ref = stereo_bm(L, R, m, D, bs, "ssd", u, lr, True)
+    fixed, _ = _run(L, R, min_disp=m, num_disp=D, block_size=bs, cost="ssd", uniqueness_ratio=u,
+                    disp12_max_diff=lr)
+    np.testing.assert_array_equal(fixed, ref["fixed"])
+
+
 GOLDEN = sorted(glob.glob(os.path.join(os.path.dirname(__file__), "golden", "*.npz")))
 
 
