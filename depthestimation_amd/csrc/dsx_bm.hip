@@ -29,6 +29,8 @@
 //   side 2 (volume) : tile copied to the [H][W][Dp] cost volume (north-star "K1")
 //   side 3 (left+LR): side 0 plus right-view winners built along the tile's cost diagonals
 //                     (atomicMin across strips), checked afterwards by lr_fixup
+//   side 4 (left+CV): side 0 plus OpenCV's LR keys (each unique winner offers (cost, d) to its right
+//                     pixel), checked afterwards by lr_fixup_sgbm
 #include "dsx_internal.h"
 #include "dsx_partition.h"
 
@@ -53,11 +55,17 @@
 #ifndef DSX_WPE_SSD
 #define DSX_WPE_SSD 4
 #endif
+#ifndef DSX_LANE_REBUILD  // 4-wave SSD builds: lane index rebuilt per segment (wave index SGPR + mbcnt)
+#define DSX_LANE_REBUILD 1
+#endif
+#ifndef DSX_SEG_KARG  // LR pass: launch arguments reloaded per segment as well as per row
+#define DSX_SEG_KARG 1
+#endif
 #ifndef DSX_INIT_SB  // SSD segment init: scheduling barrier between column chunks
 #define DSX_INIT_SB 1
 #endif
 #ifndef DSX_SSD_LDSDIAG  // SSD LR pass (NW >= 2): right-view winners read from the finished tile
-#define DSX_SSD_LDSDIAG 1
+#define DSX_SSD_LDSDIAG 0  // measured slower (C3 325 -> 383 us): the reads wait in pairs at 128 VGPRs
 #endif
 
 #include <algorithm>
@@ -237,7 +245,7 @@ __device__ __forceinline__ void bm2_segment(const Bm2Args &a_in, uint8_t *smem, 
     constexpr int side = SIDE;
     // the LR pass reloads the launch arguments per segment too: values derived from them in the
     // segment prologue would otherwise be hoisted out of the block's segment loop and spilled
-    const Bm2Args a = kargs_row<SIDE == 3 && DSX_KARG>(a_in);
+    const Bm2Args a = kargs_row<SIDE == 3 && DSX_KARG && DSX_SEG_KARG>(a_in);
     // FSS: SSD sums in f32.  Squared differences, column sums and (offset) box sums are integers
     // below 2^24, so v_sub_f32 / v_fma_f32 / v_add_f32 (full rate, ~2 cycles) are exact and
     // replace the quarter-rate v_mad_i32_i24.  Box sums carry a +2^23 offset: for box < 2^23
@@ -246,7 +254,8 @@ __device__ __forceinline__ void bm2_segment(const Bm2Args &a_in, uint8_t *smem, 
     // lie above 23 + DB and leave the (C << DB | d) order intact); the epilogue subtracts OFF.
     // ABS (SAD1): SAD with the SSD layout (one disparity per lane, u32 column / box sums) for D <= 64,
     // where the packed pairs would leave half of the wave on padding disparities
-    constexpr bool FSS = SSD && !ABS && R <= 5 && (SIDE == 0 || SIDE == 3);
+    constexpr bool FSS = SSD && !ABS && R <= 5 && (SIDE == 0 || SIDE == 3 || SIDE == 4);
+    constexpr bool SGK = SIDE == 4;  // left pass + OpenCV-form LR keys (lr_form 'sgbm' on the fused path)
     // LDSD: the SSD LR pass takes the right-view winners from the finished tile in the epilogue
     // (2 VALU per cost on most waves) instead of tracking the diagonals through the row loop (5)
     constexpr bool LDSD = SIDE == 3 && SSD && !ABS && NW >= 2 && DSX_SSD_LDSDIAG;
@@ -254,12 +263,18 @@ __device__ __forceinline__ void bm2_segment(const Bm2Args &a_in, uint8_t *smem, 
     typedef typename std::conditional<FSS, float, typename std::conditional<SSD, uint32_t, u16x2>::type>::type acc_t;
     uint8_t *tile = smem + 4 * SLOT;
 
-    // the lane index is rebuilt per segment from the wave index (an SGPR) and mbcnt: tid-derived
-    // values are then computed per segment instead of held (and spilled) across the whole kernel
-    int ln;  // mbcnt inside the asm: not hoisted out of the segment loop
-    asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(ln));
-    const int tid = (wvu << 6) + ln;
-    const int wv = wvu;
+    // The 4-wave SSD build (128 VGPRs) rebuilds the lane index per segment from the wave index (an
+    // SGPR) and mbcnt, so tid-derived values are computed per segment instead of held (and spilled)
+    // across the kernel: 0 B of scratch.  The other builds keep threadIdx.x - the rebuild measured
+    // slower there (C2r +6 %, C1 +14 %: fewer VGPRs, different occupancy and schedule).
+    constexpr bool LANE_RB = DSX_LANE_REBUILD && SSD && !ABS && NW >= 4;
+    int ln = 0;
+    if constexpr (LANE_RB)  // mbcnt inside the asm: not hoisted out of the segment loop
+        asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(ln));
+    else
+        ln = (int)threadIdx.x & 63;
+    const int tid = LANE_RB ? (wvu << 6) + ln : (int)threadIdx.x;
+    const int wv = LANE_RB ? wvu : tid >> 6;
     const int H = a.H, W = a.W, m = a.m, D = a.D;
     const int64_t stride = a.stride;
     const int d0 = SSD ? (wv * 64 + ln) : (wv * 128 + 2 * ln);
@@ -953,7 +968,7 @@ __device__ __forceinline__ void bm2_segment(const Bm2Args &a_in, uint8_t *smem, 
                 if (h == 0 && x < W) a.out_dR[o] = cb == padv ? (int16_t)-1 : (int16_t)b;
             } else {
                 // valid band: A5' [m + D - 1, W - 1 + m]; OpenCV's form (sg_keys) [max(m + D, 0), W + min(m, 0))
-                bool valid = a.sg_keys ? (x < W && x >= max(m + D, 0) && x < W + min(m, 0))
+                bool valid = SGK ? (x < W && x >= max(m + D, 0) && x < W + min(m, 0))
                                        : (x < W && x >= m + D - 1 && x <= W - 1 + m);
                 if (a.uniq > 0) {
                     const int rel = b - h * DSL;
@@ -1014,7 +1029,7 @@ __device__ __forceinline__ void bm2_segment(const Bm2Args &a_in, uint8_t *smem, 
                 if (h == 0 && x < W) {
                     if (lr_on && !(DSX_EXP & 8)) a.dstar[o] = valid ? (int16_t)b : (int16_t)-1;  // LR check: lr_fixup
                     const int16_t fx = valid ? (int16_t)(m * 16 + f) : (int16_t)((m - 1) * 16);
-                    if (side == 0 && a.sg_keys) {
+                    if constexpr (SGK) {
                         // OpenCV's LR form: a unique winner offers (cost, d) to right pixel x - m - d
                         // (min cost, then max d); lr_fixup_sgbm tests against them afterwards
                         a.dstar[o] = fx;
@@ -1108,7 +1123,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu((SSD &&
 #endif
 
     // ---- left pass: columns of strips that lie entirely in the invalid band ----
-    if ((side == 0 || side == 3) && (a.out_fixed || a.out_float)) {
+    if ((side == 0 || side == 3 || side == 4) && (a.out_fixed || a.out_float)) {
         const int xa = a.strip_begin * TX, xb = min(W, (a.strip_begin + a.strip_count) * TX);
         const int nin = xa + (W - xb);
         const int total = nin * H * a.nframes;  // frames are H-row slabs of one tall output (< 2^31)
@@ -1120,12 +1135,12 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu((SSD &&
             const long o = (long)y * W + x;
             if (a.out_fixed) a.out_fixed[o] = fi;
             if (a.out_float) a.out_float[o] = (float)(m - 1);
-            if (side == 0 && a.sg_keys) a.dstar[o] = fi;  // lr_fixup_sgbm reads every pixel
+            if constexpr (side == 4) a.dstar[o] = fi;  // lr_fixup_sgbm reads every pixel
         }
     }
 
     // ---- LR pass: reset the other key half (the previous call's keys, already checked) ----
-    if ((side == 3 || side == 0) && a.lr_reset_n > 0) {
+    if ((side == 3 || side == 4) && a.lr_reset_n > 0) {
         uint32_t *kr = a.lr_reset;
         const int64_t n = a.lr_reset_n, stride = (int64_t)gridDim.x * NT;
         const int64_t t0 = (int64_t)blockIdx.x * NT + tid;
@@ -1337,7 +1352,9 @@ static hipError_t launch_bm2_side(const Bm2Args &a, hipStream_t st) {
 template <int R, bool SSD, int NW>
 static hipError_t launch_bm2_one(const Bm2Args &a, hipStream_t st) {
     switch (a.side) {
-        case 0: return launch_bm2_side<R, SSD, NW, 0>(a, st);
+        // the OpenCV-form keys are a separate build of the left pass: kept out of the plain one
+        // (their runtime branches cost the C2 pass 2 %, profiles/r04n_sg_side0_ab.txt)
+        case 0: return a.sg_keys ? launch_bm2_side<R, SSD, NW, 4>(a, st) : launch_bm2_side<R, SSD, NW, 0>(a, st);
         case 1: return launch_bm2_side<R, SSD, NW, 1>(a, st);
         case 3: return launch_bm2_side<R, SSD, NW, 3>(a, st);
         default: return launch_bm2_side<R, SSD, NW, 2>(a, st);
@@ -1348,7 +1365,7 @@ static hipError_t launch_bm2_one(const Bm2Args &a, hipStream_t st) {
 template <int R>
 static hipError_t launch_bm2_sad1(const Bm2Args &a, hipStream_t st) {
     switch (a.side) {
-        case 0: return launch_bm2_side<R, true, 1, 0, true>(a, st);
+        case 0: return a.sg_keys ? launch_bm2_side<R, true, 1, 4, true>(a, st) : launch_bm2_side<R, true, 1, 0, true>(a, st);
         case 1: return launch_bm2_side<R, true, 1, 1, true>(a, st);
         case 3: return launch_bm2_side<R, true, 1, 3, true>(a, st);
         default: return hipErrorInvalidValue;

@@ -28,7 +28,7 @@ struct Bm2Args {
     int H, W;
     int m;               // min_disp
     int D;               // num_disp (padded internally to the kernel's Dp)
-    int side;            // 0 left (full epilogue), 1 right (dR map), 2 volume (K1 store), 3 left + LR keys
+    int side;            // 0 left (full epilogue; with sg_keys the launcher runs the side-4 build), 1 right (dR map), 2 volume (K1 store), 3 left + LR keys
     int uniq, lr, subpix, float_mode;
     uint32_t padv;       // cost stored for disparities outside [0, D) / outside the image
     int strip_begin, strip_count;  // 32-column strips forming the work space

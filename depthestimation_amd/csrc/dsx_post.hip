@@ -770,9 +770,6 @@ __device__ bool spk_small(const PostFullArgs &a, int k0, int *vis, int lane, int
 //    of the three sorted columns (v_min3 / v_med3 / v_max3).
 constexpr int kT3X = 32, kT3Y = 16;
 constexpr int kSqMax = 8191;
-#ifndef DSX_POST_NT  // experiment: non-temporal loads of the codes (the K1 -> K2 hand-off effect)
-#define DSX_POST_NT 0
-#endif
 
 template <int R>
 struct T3 {
@@ -837,8 +834,7 @@ __global__ __launch_bounds__(256, 8) void post_tail3(PostFullArgs a) {
     for (int j = 0; j < NQ; ++j) {  // every load of the thread in flight at once
         const int q = min(tid + 256 * j, RH * RW - 1);
         const int ty = q / RW, tx = q - ty * RW;
-        if constexpr (DSX_POST_NT) cv[j] = __builtin_nontemporal_load(a.code16 + (int64_t)ry(ty) * Wc + rx(tx));
-        else cv[j] = a.code16[(int64_t)ry(ty) * Wc + rx(tx)];
+        cv[j] = a.code16[(int64_t)ry(ty) * Wc + rx(tx)];
     }
 #pragma unroll
     for (int j = 0; j < NQ; ++j) {

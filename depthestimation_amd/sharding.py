@@ -39,39 +39,29 @@ class DistEnv:
                    int(os.environ.get("WORLD_SIZE", 1)))
 
 
-def _free_port() -> int:
-    import socket
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    p = s.getsockname()[1]
-    s.close()
-    return p
-
-
 def init_distributed(backend: Optional[str] = None, single_rank_group: bool = False) -> DistEnv:
     """Initialise the default process group when WORLD_SIZE > 1 (RCCL when a GPU is
     present, gloo otherwise). With ``single_rank_group`` a one-rank group is created as well
     (outside torch.distributed.run too: a local rendezvous on 127.0.0.1), so the job's
     collectives run through the same backend at N = 1 (bench.py). Idempotent."""
     env = DistEnv.from_env()
-    if single_rank_group and env.world_size == 1:
-        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        os.environ.setdefault("MASTER_PORT", str(_free_port()))
-        os.environ.setdefault("RANK", "0")
-        os.environ.setdefault("LOCAL_RANK", "0")
-        os.environ.setdefault("WORLD_SIZE", "1")
+    # a one-rank group started outside a launcher rendezvouses through an in-process store: no TCP
+    # port to pick (a free port probed here could be taken again before the store binds it)
+    local_store = single_rank_group and env.world_size == 1 and "MASTER_PORT" not in os.environ
     if env.world_size > 1 or single_rank_group:
         import torch
         import torch.distributed as dist
         if not dist.is_initialized():
             if backend is None:
                 backend = "nccl" if torch.cuda.is_available() else "gloo"
-            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            kw = dict(store=dist.HashStore(), rank=0, world_size=1) if local_store else {}
+            if not local_store:
+                os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
             if backend == "nccl":
                 torch.cuda.set_device(env.local_rank)
-                dist.init_process_group(backend, device_id=torch.device("cuda", env.local_rank))
+                dist.init_process_group(backend, device_id=torch.device("cuda", env.local_rank), **kw)
             else:
-                dist.init_process_group(backend)
+                dist.init_process_group(backend, **kw)
     return env
 
 

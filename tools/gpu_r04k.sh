@@ -8,8 +8,3 @@ rc=$?; tail -3 gpurun_out/r04k_tests.txt; [ $rc -eq 0 ] || { grep -E "FAIL|Error
 CONFIGS="c3 c2 c2r c4 c1 c5" REPS=2 STEPS=500 bash tools/lib_ab.sh r04k_ab tools/explib/libdsx_base.so || exit 1
 timeout -k 10 300 python3 tools/dropin_bench.py --configs c2r c4 > gpurun_out/r04k_dropin.json 2> gpurun_out/r04k_dropin.err || { tail -20 gpurun_out/r04k_dropin.err; exit 1; }
 cut -c1-400 gpurun_out/r04k_dropin.json
-for v in new postnt; do
-  if [ $v = new ]; then L=$PWD/depthestimation_amd/libdsx.so; else L=$PWD/tools/explib/libdsx_$v.so; fi
-  DSX_LIB=$L timeout -k 10 300 python3 tools/dropin_bench.py --configs c2r c4 --frames 400 > gpurun_out/r04k_dropin_$v.json 2>> gpurun_out/r04k_dropin.err || { tail -20 gpurun_out/r04k_dropin.err; exit 1; }
-  echo "$v $(python3 -c "import json;[print(d['config'],d['gpu_ms_per_frame'],d['kernels_ms']) for d in map(json.loads,open('gpurun_out/r04k_dropin_$v.json'))]")"
-done
