@@ -19,7 +19,7 @@ import sys
 from collections import defaultdict
 
 # kernel names: vol_wta / lr_fixup by name, bm2<R, SSD, NW, SIDE[, ABS]> by its SIDE argument
-SIDES = {"0": "bm_pass_left", "3": "bm_pass_left", "1": "bm_pass_right", "2": "cost_volume"}
+SIDES = {"0": "bm_pass_left", "3": "bm_pass_left", "4": "bm_pass_left", "1": "bm_pass_right", "2": "cost_volume"}
 
 
 def short(k):
