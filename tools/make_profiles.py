@@ -55,7 +55,7 @@ def main(src, tag, config, path):
     vp = os.path.join(prof, "valu_counts.json")
     valu = json.load(open(vp)) if os.path.exists(vp) else {}
     for k, cs in acc.items():
-        if "rocclr" in k:
+        if "rocclr" in k or "dsx::" not in k:  # torch fill kernels of the bench harness
             continue
         lines.append(f"{k}  [{short(k)}]  avg_ns={avg_ns.get(k)}")
         for c, v in sorted(cs.items()):
