@@ -411,12 +411,14 @@ def main():
     if args.steps > 0:
         torch.cuda.synchronize(dev)
         rk.barrier()
+        torch.cuda.synchronize(dev)
         tu = time.perf_counter()
         for i in range(args.steps):
             step(i)
         torch.cuda.synchronize(dev)
+        tu = time.perf_counter() - tu
         rk.barrier()
-        tu = rk.allreduce(float(time.perf_counter() - tu), "max")
+        tu = rk.allreduce(float(tu), "max")
         unsettled = {"value": round(H * W * B * args.steps * ws / tu / 1e6, 1), "unit": "Mpix/s",
                      "ms_per_step": round(tu / args.steps * 1e3, 5),
                      "note": "the K timed steps run once right after the secondary figures, before --settle and the "
@@ -441,8 +443,10 @@ def main():
         step(i)
     ev1.record(stream)
     torch.cuda.synchronize(dev)
-    rk.barrier()
+    # each rank's clock stops at its own synchronize, then the closing barrier; the job time is the
+    # max over ranks (an RCCL barrier inside the window added 1-3 us per step of noise at 20 steps)
     elapsed = time.perf_counter() - t0
+    rk.barrier()
     region_ms = ev0.elapsed_time(ev1) / args.steps  # GPU time per step over the timed region
     elapsed = rk.allreduce(float(elapsed), "max")
 
