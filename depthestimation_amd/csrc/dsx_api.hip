@@ -316,8 +316,11 @@ int begin_timed(dsx_handle *h, const char *name, hipStream_t st, TimedLaunch &t)
         t.b = h->free_events.back().second;
         h->free_events.pop_back();
     } else {
-        DSX_HIP(hipEventCreate(&t.a));
-        DSX_HIP(hipEventCreate(&t.b));
+        // timing-only events: no system-scope fence (cache writeback + invalidate) at each record,
+        // which made every timed kernel start on cold caches (C3's left pass read 331 us against 298 us
+        // under rocprofv3, profiles/r04_final_bench_c3.json)
+        DSX_HIP(hipEventCreateWithFlags(&t.a, hipEventDisableSystemFence));
+        DSX_HIP(hipEventCreateWithFlags(&t.b, hipEventDisableSystemFence));
     }
     DSX_HIP(hipEventRecord(t.a, st));
     return DSX_OK;
