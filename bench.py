@@ -495,7 +495,10 @@ def main():
             ksrc = f"per-launch HIP events, breakdown pass of {nbd} steps after the timed region"
         traffic = load_traffic()
         tr = traffic.get(f"{args.config}:{args.path}:{dom_name}")
-        per_launch_bytes = ab["frame"] * (B if dom_name == "bm_pass_left" else 1)  # one launch covers B frames
+        # one launch covers B frames; a volume-path kernel moves only its own half (K1 writes the volume,
+        # K2 reads it: SURVEY 8(d) per kernel)
+        kbytes = {"cost_volume": ab["k1"], "volume_wta": ab["k2"]}.get(dom_name, ab["frame"])
+        per_launch_bytes = kbytes * (B if dom_name == "bm_pass_left" else 1)
         equiv = per_launch_bytes / (dom_ms * 1e-3) / 1e9
         roofline = None
         if args.path == "fused" and dom_name == "bm_pass_left":
