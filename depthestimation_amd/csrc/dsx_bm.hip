@@ -61,6 +61,9 @@
 #ifndef DSX_SEG_KARG  // LR pass: launch arguments reloaded per segment as well as per row
 #define DSX_SEG_KARG 1
 #endif
+#ifndef DSX_SADINIT_ABS  // SAD1 builds: transposed v_sad_u8 segment init (see SADINIT)
+#define DSX_SADINIT_ABS 1
+#endif
 #ifndef DSX_INIT_SB  // SSD segment init: scheduling barrier between column chunks
 #define DSX_INIT_SB 1
 #endif
@@ -427,8 +430,10 @@ __device__ __forceinline__ void bm2_segment(const Bm2Args &a_in, uint8_t *smem, 
     // 57.3 -> 56.3 us, C5 (R=7) 610 -> 581 us; but the R=4 instantiation (C2) runs 72.9 -> 79.0 us
     // with it - its row loop is scheduled worse (more full vmcnt drains), not its init - so R=4 keeps
     // the row-by-row init.
-    constexpr bool SADINIT = DSX_SADINIT && R != 4;
-    if constexpr (!SSD && side != 1 && SADINIT) {
+    // SAD1 (ABS, one disparity per lane) takes the same transposed init with one v_sad_u8 per column
+    // and row group (the pair's first entry only)
+    constexpr bool SADINIT = DSX_SADINIT && (ABS ? DSX_SADINIT_ABS : R != 4);
+    if constexpr ((!SSD || ABS) && side != 1 && SADINIT) {
         // SAD (left / volume passes): rows in groups of 4, bytes transposed so that one v_sad_u8
         // sums a column's 4 row terms for one disparity: TP_g[j] = {P(j), P(j+1)} with P(j) the
         // group's 4 search bytes at position pos(j) (one per row), R_g[c] the 4 reference bytes
@@ -526,15 +531,23 @@ __device__ __forceinline__ void bm2_segment(const Bm2Args &a_in, uint8_t *smem, 
 #pragma unroll
                 for (int c = 0; c < 4; ++c) {
                     if (c0 + c < NC) {
-                        const uint2 pr = *reinterpret_cast<const uint2 *>(tb + g * TPG + (NC - 1 - c0 - c) * 8);
-                        ae[c0 + c] = __builtin_amdgcn_sad_u8(rv[c], pr.x, ae[c0 + c]);
-                        ao[c0 + c] = __builtin_amdgcn_sad_u8(rv[c], pr.y, ao[c0 + c]);
+                        if constexpr (ABS) {
+                            const uint32_t p0 = *reinterpret_cast<const uint32_t *>(tb + g * TPG + (NC - 1 - c0 - c) * 8);
+                            ae[c0 + c] = __builtin_amdgcn_sad_u8(rv[c], p0, ae[c0 + c]);
+                        } else {
+                            const uint2 pr = *reinterpret_cast<const uint2 *>(tb + g * TPG + (NC - 1 - c0 - c) * 8);
+                            ae[c0 + c] = __builtin_amdgcn_sad_u8(rv[c], pr.x, ae[c0 + c]);
+                            ao[c0 + c] = __builtin_amdgcn_sad_u8(rv[c], pr.y, ao[c0 + c]);
+                        }
                     }
                 }
             }
         }
 #pragma unroll
-        for (int c = 0; c < NC; ++c) cs[c] = as2(ae[c] | (ao[c] << 16));  // <= 255 (2R+1) < 2^16
+        for (int c = 0; c < NC; ++c) {
+            if constexpr (ABS) cs[c] = ae[c];
+            else cs[c] = as2(ae[c] | (ao[c] << 16));  // <= 255 (2R+1) < 2^16
+        }
         }
 
     } else {
