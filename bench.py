@@ -263,6 +263,10 @@ def main():
     ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
     ap.add_argument("--path", default="fused", choices=["fused", "volume"])
     ap.add_argument("--frames", type=int, default=4, help="distinct resident frame pairs per GPU")
+    ap.add_argument("--streams", type=int, default=3,
+                    help="frames in flight per GPU in the timed region: step i runs on HIP stream i mod S with its "
+                         "own handle and outputs, so frame i+1's blocks take the slots frame i's finished blocks "
+                         "free (1: one frame at a time)")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="nccl: one rank per GPU over RCCL (the measured mode); gloo: oversubscribed rehearsal, "
                          "ranks share the visible GPUs (labelled in the JSON line, not a scaling figure)")
@@ -368,13 +372,29 @@ def main():
                                aggregation=args.sgm, **kw)
     stream = torch.cuda.current_stream(dev)
 
-    def step(i, m=matcher):
+    def step(i, m=matcher, st=None, of=None, ff=None):
+        st = stream if st is None else st
+        of = out_fixed if of is None else of
+        ff = out_float if ff is None else ff
         if B == 1:
             fl, fr = frames[i % len(frames)]
-            m.compute_device(fl, fr, out_fixed=out_fixed[0], out_float=out_float[0], stream=stream)
+            m.compute_device(fl, fr, out_fixed=of[0], out_float=ff[0], stream=st)
         else:
             gl, gr = groups[i % len(groups)]
-            m.compute_batch_device(gl, gr, out_fixed=out_fixed, out_float=out_float, stream=stream)
+            m.compute_batch_device(gl, gr, out_fixed=of, out_float=ff, stream=st)
+
+    # frames in flight (the timed region, its warmup and settling): S handles (a handle's LR / volume
+    # scratch is its own), S streams, S output sets; lane 0 is the parity-checked matcher on `stream`
+    S = max(1, args.streams)
+    lanes = [(matcher, stream, out_fixed, out_float)]
+    for _ in range(S - 1):
+        lanes.append((HipBlockMatcher(device=local, path=args.path, timing=False, grid_blocks=args.grid_blocks,
+                                      aggregation=args.sgm, **kw), torch.cuda.Stream(dev),
+                      torch.empty_like(out_fixed), torch.empty_like(out_float)))
+
+    def tstep(i):
+        m, st, of, ff = lanes[i % S]
+        step(i, m, st, of, ff)
 
     # parity of the timed matcher: every rank's frame 0 against the C restatement of the contract
     # (oracle/bm_ref.c, the checker; never on the measured path), before the timed region; after it
@@ -414,7 +434,7 @@ def main():
         torch.cuda.synchronize(dev)
         tu = time.perf_counter()
         for i in range(args.steps):
-            step(i)
+            tstep(i)
         torch.cuda.synchronize(dev)
         tu = time.perf_counter() - tu
         rk.barrier()
@@ -428,11 +448,11 @@ def main():
     t_settle = time.perf_counter()
     while time.perf_counter() - t_settle < args.settle:
         for _ in range(64):
-            step(settle_steps)
+            tstep(settle_steps)
             settle_steps += 1
         torch.cuda.synchronize(dev)
     for i in range(args.warmup):
-        step(i)
+        tstep(i)
     torch.cuda.synchronize(dev)
     rk.barrier()
     torch.cuda.synchronize(dev)
@@ -440,7 +460,9 @@ def main():
     t0 = time.perf_counter()
     ev0.record(stream)
     for i in range(args.steps):
-        step(i)
+        tstep(i)
+    for _, st, _, _ in lanes[1:]:  # the region's end event waits for every lane
+        stream.wait_stream(st)
     ev1.record(stream)
     torch.cuda.synchronize(dev)
     # each rank's clock stops at its own synchronize, then the closing barrier; the job time is the
@@ -465,7 +487,25 @@ def main():
     # 298 us under rocprofv3; tools/timing_probe.py, profiles/r04v_timing_probe.json)
     nbd = 100
     if args.path == "fused" and cfg["disp12_max_diff"] < 0:
-        ktimes = {"bm_pass_left": (region_ms, args.steps)}
+        if S == 1:
+            ktimes = {"bm_pass_left": (region_ms, args.steps)}
+        else:
+            # frames overlapped in the region, so a launch's own duration comes from one stream: the
+            # timed handle back to back (settled) for 100 launches, stream events around them
+            t_bd = time.perf_counter()
+            i = 0
+            while i < 3 or time.perf_counter() - t_bd < args.settle:
+                for _ in range(8):
+                    step(i)
+                    i += 1
+                torch.cuda.synchronize(dev)
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+            for i in range(nbd):
+                step(i)
+            e1.record(stream)
+            torch.cuda.synchronize(dev)
+            ktimes = {"bm_pass_left": (e0.elapsed_time(e1) / nbd, nbd)}
     else:
         t_bd = time.perf_counter()
         i = 0
@@ -488,9 +528,10 @@ def main():
         dom = max(ktimes.items(), key=lambda kv: kv[1][0] * kv[1][1])
         dom_name, (dom_ms, dom_n) = dom
         if len(ktimes) == 1:
-            # one kernel per step: its average launch duration over the timed region itself (stream
-            # events around the K back-to-back launches; includes the inter-launch dispatch gaps)
-            dom_ms, dom_n, ksrc = region_ms, args.steps, "stream events over the timed region / steps"
+            # one kernel per step: its average launch duration from stream events around back-to-back
+            # launches on one stream (the timed region itself at --streams 1; includes the dispatch gaps)
+            ksrc = ("stream events over the timed region / steps" if S == 1 else
+                    f"stream events over {nbd} back-to-back launches on one stream after the timed region")
         else:
             ksrc = f"per-launch HIP events, breakdown pass of {nbd} steps after the timed region"
         traffic = load_traffic()
@@ -513,6 +554,9 @@ def main():
             "kernels_ms": {k: round(v[0], 5) for k, v in ktimes.items()},
             "region_ms_per_step": round(region_ms, 5),
         })
+        if S > 1:
+            roofline["region_note"] = (f"region_ms_per_step: {S} frames in flight, so a step's GPU time is below a "
+                                       "launch's own duration (kernel_ms)")
         if roofline.get("traffic"):
             hbm = roofline["traffic"] / (dom_ms * 1e-3) / 1e9
             roofline["hbm_achieved_GBs"] = round(hbm, 1)
@@ -539,13 +583,17 @@ def main():
                        "block_size": cfg["block_size"], "cost": cfg["cost"],
                        "uniqueness_ratio": cfg["uniqueness_ratio"], "disp12_max_diff": cfg["disp12_max_diff"],
                        "subpixel": True, "path": args.path, "aggregation": args.sgm or "none",
-                       "frames_per_step_per_gpu": B, "parallelism": par},
+                       "frames_per_step_per_gpu": B, "frames_in_flight_per_gpu": S, "parallelism": par},
             "roofline": roofline,
             "parity": parity,
             "sharding": sharding_info,
             "order": "parity check -> secondary measurements -> the K steps unsettled -> clock settling -> warmup "
                      "-> timed region -> breakdown pass -> CPU baseline",
             "settle": {"seconds": args.settle, "steps": settle_steps, "timed": False},
+            "streams": {"frames_in_flight": S,
+                        "note": "step i runs on HIP stream i mod S with its own handle and output buffers (a frame's "
+                                "work is unchanged; consecutive frames overlap the persistent pass's tail); "
+                                "--streams 1 is one frame at a time"},
             "unsettled": unsettled,
         }
         if args.dist_backend == "gloo":

@@ -229,8 +229,11 @@ class HostPipeline:
         self.copy = bool(copy)
         kw = dict(matcher_kw)
         kw.pop("device", None)
-        self.m = HipBlockMatcher(device=int(device), **kw)
         self.streams = [torch.cuda.Stream(device=self.dev) for _ in range(max(1, int(streams)))]
+        # one handle per stream: a handle's scratch (LR keys, cost volume) orders its calls across
+        # streams, so with one handle the LR / volume configs would run one frame at a time
+        self.ms = [HipBlockMatcher(device=int(device), **kw) for _ in self.streams]
+        self.m = self.ms[0]
         self.shape = None
         self.pending: List[Optional[Tuple[int, object]]] = [None] * self.depth  # slot -> (frame index, event)
 
@@ -291,10 +294,11 @@ class HostPipeline:
             np.copyto(hv[0], L)
             np.copyto(hv[1], R)
             src = self.hin[slot]
-        st = self.streams[i % len(self.streams)]
+        k = i % len(self.streams)
+        st = self.streams[k]
         with torch.cuda.stream(st):
             self.din[slot].copy_(src, non_blocking=True)
-            self.m.compute_device(self.din[slot][0], self.din[slot][1], out_fixed=self.dfx[slot], stream=st)
+            self.ms[k].compute_device(self.din[slot][0], self.din[slot][1], out_fixed=self.dfx[slot], stream=st)
             self.hfx[i % (2 * self.depth)].copy_(self.dfx[slot], non_blocking=True)
             ev = torch.cuda.Event()
             ev.record(st)
@@ -317,7 +321,8 @@ class HostPipeline:
 
     def close(self) -> None:
         self.drain_all()
-        self.m.close()
+        for m in self.ms:
+            m.close()
 
 
 class DepthPipeline:

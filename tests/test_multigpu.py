@@ -184,8 +184,9 @@ def test_multi_device_stereo_matches_oracle():
 @pytest.mark.gpu
 @pytest.mark.parametrize("depth,streams,lr", [(3, 2, 1), (2, 1, -1), (4, 3, 1)])
 def test_host_pipeline_in_flight_matches_oracle(depth, streams, lr):
-    """HostPipeline: frames in flight over several streams (LR buffers shared by one handle),
-    numpy and pinned-tensor inputs, a shape change mid-stream, views vs copies."""
+    """HostPipeline: frames in flight over several streams (one handle per stream; one handle shared
+    across streams is test_gpu_configs.py::test_lr_handle_on_alternating_streams), numpy and pinned-tensor
+    inputs, a shape change mid-stream, views vs copies."""
     import torch
     from depthestimation_amd.multigpu import HostPipeline
     from depthestimation_amd.synthetic import stereo_pair
