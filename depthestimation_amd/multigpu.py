@@ -126,6 +126,8 @@ def sharded_map(frames: Iterable, slots: Sequence[int], make_fn: Callable[[int],
                 if item is _STOP:
                     if pipelined:
                         publish(fn.drain_all())
+                        if hasattr(fn, "close"):
+                            fn.close()  # the stage's own handles
                     return
                 i, payload = item
                 if pipelined:
@@ -335,6 +337,7 @@ class DepthPipeline:
     generator yields, StereoDepthEstimatorVideo.py:101-103)."""
 
     def __init__(self, core, device: int, depth: int = 3, streams: int = 2):
+        import copy
         import torch
         self.torch = torch
         self.core = core
@@ -342,6 +345,18 @@ class DepthPipeline:
         torch.cuda.set_device(self.dev)
         self.depth = max(2, int(depth))
         self.streams = [torch.cuda.Stream(device=self.dev) for _ in range(max(1, int(streams)))]
+        # one matcher handle per stream: a handle's scratch (the drop-in call's maps and workspace, LR
+        # keys) orders its calls across streams, so a shared handle would run one frame at a time.  The
+        # other streams use shallow copies of ``core`` (same parameters and rectification cache) with
+        # a handle of their own.
+        self.cores = [core]
+        self._own = []
+        for _ in self.streams[1:]:
+            c = copy.copy(core)
+            if getattr(core, "sgbm", None) is not None and hasattr(core.sgbm, "params"):
+                c.sgbm = HipBlockMatcher(**dict(core.sgbm.params))
+                self._own.append(c.sgbm)
+            self.cores.append(c)
         self.shape = None
         self.pending: List[Optional[Tuple[int, object, object]]] = [None] * self.depth
 
@@ -373,11 +388,12 @@ class DepthPipeline:
         hl, hr = self.hin[slot]
         np.copyto(hl.numpy(), L)
         np.copyto(hr.numpy(), R)
-        st = self.streams[i % len(self.streams)]
+        k = i % len(self.streams)
+        st = self.streams[k]
         with torch.cuda.stream(st):
             dl = hl.to(self.dev, non_blocking=True)
             dr = hr.to(self.dev, non_blocking=True)
-            _, z = self.core.estimate_depth_device(dl, dr, stream=st)
+            _, z = self.cores[k].estimate_depth_device(dl, dr, stream=st)
             zshape = None
             if z is not None:
                 if self.hout[slot] is None or self.hout[slot].shape != z.shape:
@@ -403,6 +419,13 @@ class DepthPipeline:
     def drain_all(self) -> List[Tuple[int, Optional[np.ndarray]]]:
         live = sorted((p[0], s) for s, p in enumerate(self.pending) if p is not None)
         return [self._finish(s) for _, s in live]
+
+    def close(self) -> None:
+        """Finish the frames in flight and release the per-stream handles this pipeline created."""
+        self.drain_all()
+        for m in self._own:
+            m.close()
+        self._own = []
 
 
 class MultiDeviceStereo:

@@ -3,7 +3,7 @@
 # command, then every config at --streams 3 and --streams 1
 set -o pipefail
 mkdir -p gpurun_out
-timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_bench_multirank.py > gpurun_out/r04aa_tests.txt 2>&1
+timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_bench_multirank.py tests/test_multigpu.py tests/test_gpu_reference_plumbing.py > gpurun_out/r04aa_tests.txt 2>&1
 rc=$?; tail -3 gpurun_out/r04aa_tests.txt; [ $rc -eq 0 ] || exit $rc
 SKIP_TESTS=1 TAG=r04aa bash tools/gpu_full.sh || exit 1
 for c in c1 c2 c2r c3 c4 c5; do
