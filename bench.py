@@ -396,6 +396,10 @@ def main():
         m, st, of, ff = lanes[i % S]
         step(i, m, st, of, ff)
 
+    for i in range(S):  # each lane's first call sets its handle up (partition tables, scratch): untimed
+        tstep(i)
+    torch.cuda.synchronize(dev)
+
     # parity of the timed matcher: every rank's frame 0 against the C restatement of the contract
     # (oracle/bm_ref.c, the checker; never on the measured path), before the timed region; after it
     # the same handle's frame-0 map is compared with this one again on the device
