@@ -878,6 +878,24 @@ def dropin_figures(rk, dev, stream) -> dict:
             torch.cuda.synchronize(dev)
             dt = rk.allreduce(float(time.perf_counter() - t0), "max")
             gpu_ms = e0.elapsed_time(e1) / n
+            # the video path's form (multigpu.DepthPipeline): 3 frames in flight, a StereoCore copy with
+            # its own handle per stream, frames resident
+            import copy
+            pcores = [core] + [copy.copy(core) for _ in range(2)]
+            for c in pcores[1:]:
+                c.sgbm = HipBlockMatcher(**dict(core.sgbm.params))
+            pst = [stream, torch.cuda.Stream(dev), torch.cuda.Stream(dev)]
+            for i in range(30):
+                pcores[i % 3].estimate_depth_device(pairs[i % 2][2], pairs[i % 2][3], stream=pst[i % 3])
+            torch.cuda.synchronize(dev)
+            rk.barrier()
+            t0 = time.perf_counter()
+            for i in range(n):
+                pcores[i % 3].estimate_depth_device(pairs[i % 2][2], pairs[i % 2][3], stream=pst[i % 3])
+            torch.cuda.synchronize(dev)
+            pdt = rk.allreduce(float(time.perf_counter() - t0), "max")
+            for c in pcores[1:]:
+                c.sgbm.close()
             core.sgbm = HipBlockMatcher(**dict(core.sgbm.params, timing=True))
             t_bd = time.perf_counter()  # back to back for 0.2 s first: settled clocks, as the loop above
             i = 0
@@ -896,6 +914,10 @@ def dropin_figures(rk, dev, stream) -> dict:
         res[name] = {"value": round(H * W * n * rk.ws / dt / 1e6, 1), "unit": "Mpix/s",
                      "ms_per_frame": round(dt / n * 1e3, 5), "gpu_ms_per_frame": round(gpu_ms, 5),
                      "kernels_ms": kt, "post_processing_ms": post,
+                     "frames_in_flight_3": {"value": round(H * W * n * rk.ws / pdt / 1e6, 1), "unit": "Mpix/s",
+                                            "ms_per_frame": round(pdt / n * 1e3, 5),
+                                            "note": "the same calls with 3 frames in flight (one StereoCore copy and "
+                                                    "handle per HIP stream: multigpu.DepthPipeline's form)"},
                      "config": {"H": H, "W": W, "num_disp": D, "block_size": cfg["block_size"], "uniqueness_ratio": 10,
                                 "disp12_max_diff": 1, "fast_mode": False, "depth": True},
                      "parity": {"mismatches": mism, "frames_checked": rk.ws,
