@@ -3,5 +3,5 @@
 # (tools/gpu_configs_bench.sh) - files gpurun_out/<tag>_*
 set -o pipefail
 T=${TAG:-final}
-SKIP_TESTS=1 TAG=$T bash tools/gpu_full.sh || exit 1
+TAG=$T bash tools/gpu_full.sh || exit 1
 bash tools/gpu_configs_bench.sh $T || exit 1
