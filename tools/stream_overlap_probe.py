@@ -20,9 +20,15 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--configs", nargs="+", default=["c2"])
     ap.add_argument("--steps", type=int, default=1000)
+    ap.add_argument("--streams", type=int, nargs="+", default=[1, 2, 3])
     args = ap.parse_args()
+    global NS
+    NS = tuple(args.streams)
     for c in args.configs:
         run(c, args.steps)
+
+
+NS = (1, 2, 3)
 
 
 def run(config, steps):
@@ -35,10 +41,10 @@ def run(config, steps):
         frames.append((torch.from_numpy(L).to(dev), torch.from_numpy(R).to(dev)))
     kw = dict(device=0, num_disp=D, block_size=cfg["block_size"], cost=cfg["cost"],
               uniqueness_ratio=cfg["uniqueness_ratio"], disp12_max_diff=cfg["disp12_max_diff"])
-    ms = [HipBlockMatcher(**kw) for _ in range(3)]  # one handle per stream: LR scratch is per handle
+    ms = [HipBlockMatcher(**kw) for _ in range(max(NS))]  # one handle per stream: LR scratch is per handle
     res = {"config": config}
     for rep in range(2):
-        for ns in (1, 2, 3):
+        for ns in NS:
             streams = [torch.cuda.Stream(dev) for _ in range(ns)]
             outs = [(torch.empty((H, W), dtype=torch.int16, device=dev), torch.empty((H, W), dtype=torch.float32, device=dev))
                     for _ in range(ns)]
