@@ -12,6 +12,8 @@
 #include "../../include/dsx.h"
 #include "dsx_internal.h"
 
+extern char **environ;  // the DSX_* tuning variables: dsx_env()
+
 #ifndef DSX_RESET_LEFT  // 1: the LR pass resets the other key half; 0: lr_fixup does
 #define DSX_RESET_LEFT 1
 #endif
@@ -371,7 +373,33 @@ struct ScratchRecord {
     }
 };
 
-dsx::Bm2Args base_args(dsx_handle *h, int H, int W, int64_t stride) {
+// The DSX_* tuning variables a fused launch reads, in one pass over the environment (seven getenv
+// scans cost ~2 us of host time per call; tests and tools change them at run time, so no caching)
+struct DsxEnv {
+    const char *prio = nullptr, *prio_t = nullptr, *slow_w8 = nullptr, *agew = nullptr, *variant = nullptr,
+               *timeline = nullptr;
+};
+DsxEnv dsx_env() {
+    DsxEnv e;
+    for (char **p = environ; p && *p; ++p) {
+        const char *s = *p;
+        if (s[0] != 'D' || s[1] != 'S' || s[2] != 'X' || s[3] != '_') continue;
+        s += 4;
+        const auto take = [s](const char *key, const char *&dst) {
+            const size_t n = strlen(key);
+            if (strncmp(s, key, n) == 0 && s[n] == '=') dst = s + n + 1;
+        };
+        take("PRIO", e.prio);
+        take("PRIO_T", e.prio_t);
+        take("SLOW_W8", e.slow_w8);
+        take("AGEW", e.agew);
+        take("VARIANT", e.variant);
+        take("TIMELINE", e.timeline);
+    }
+    return e;
+}
+
+dsx::Bm2Args base_args(dsx_handle *h, int H, int W, int64_t stride, const DsxEnv &env = dsx_env()) {
     dsx::Bm2Args a{};
     a.stride = stride;
     a.H = H;
@@ -390,20 +418,15 @@ dsx::Bm2Args base_args(dsx_handle *h, int H, int W, int64_t stride) {
         // Balance (measured on C2-C5, profiles/README.md r01d): co-resident waves drop their issue
         // priority as they pass 50 / 80 / 95 % of their rows, and strips on the clamped-load
         // path count 11/8 of a fast strip.  DSX_PRIO=0 / DSX_PRIO_T / DSX_SLOW_W8 override.
-        const char *pe = getenv("DSX_PRIO");
-        a.prio = pe ? atoi(pe) : 1;
+        a.prio = env.prio ? atoi(env.prio) : 1;
         a.pt1 = 128, a.pt2 = 205, a.pt3 = 243;
-        const char *pt = getenv("DSX_PRIO_T");
-        if (pt) sscanf(pt, "%d,%d,%d", &a.pt1, &a.pt2, &a.pt3);
-        const char *sw = getenv("DSX_SLOW_W8");
-        a.slow_w8 = sw ? atoi(sw) : 11;
+        if (env.prio_t) sscanf(env.prio_t, "%d,%d,%d", &a.pt1, &a.pt2, &a.pt3);
+        a.slow_w8 = env.slow_w8 ? atoi(env.slow_w8) : 11;
         // age-level work weights (single frames; r01f A/B: C2 83.6 -> 81.7 us, C4 61.4 -> 59.9 us)
         a.agew[0] = 78, a.agew[1] = 70, a.agew[2] = a.agew[3] = 64;
-        const char *aw = getenv("DSX_AGEW");
-        if (aw) sscanf(aw, "%d,%d,%d,%d", &a.agew[0], &a.agew[1], &a.agew[2], &a.agew[3]);
+        if (env.agew) sscanf(env.agew, "%d,%d,%d,%d", &a.agew[0], &a.agew[1], &a.agew[2], &a.agew[3]);
         a.nlev = 0;  // set by the launcher from the residency it computes
-        const char *va = getenv("DSX_VARIANT");
-        a.variant = va ? atoi(va) : 0;
+        a.variant = env.variant ? atoi(env.variant) : 0;
     }
     a.nframes = 1;
     a.frame_stride = 0;
@@ -484,7 +507,8 @@ int run(dsx_handle *h, const void *dL, const void *dR, int H, int W, int64_t str
     }
     if (fused) {
         const bool lr = h->p.disp12_max_diff >= 0 && !lr_sg;
-        dsx::Bm2Args a = base_args(h, H, W, stride);
+        const DsxEnv env = dsx_env();
+        dsx::Bm2Args a = base_args(h, H, W, stride, env);
         a.side = dsx::SIDE_LEFT;
         a.ref = static_cast<const uint8_t *>(dL);
         a.src = static_cast<const uint8_t *>(dR);
@@ -527,7 +551,7 @@ int run(dsx_handle *h, const void *dL, const void *dR, int H, int W, int64_t str
             }
         }
         uint64_t *tl = nullptr;
-        const char *tlpath = getenv("DSX_TIMELINE");
+        const char *tlpath = env.timeline;
         if (tlpath && *tlpath) DSX_HIP(hipMalloc(&tl, 12 * 8 * 65536));
         if (tl) DSX_HIP(hipMemsetAsync(tl, 0, 12 * 8 * 65536, st));
         a.timeline = tl;

@@ -1329,7 +1329,8 @@ static hipError_t launch_bm2_side(const Bm2Args &a, hipStream_t st) {
     if (a.grid_override > 0) grid = a.grid_override;
     if (grid > T) grid = T;
     if (grid < 1) grid = 1;
-    if (getenv("DSX_VERBOSE"))
+    static const bool verbose = getenv("DSX_VERBOSE") != nullptr;  // diagnostics: read once
+    if (verbose)
         fprintf(stderr, "[dsx] bm2<R=%d,SSD=%d,NW=%d,SIDE=%d> grid %ld (%d/CU) smem %d\n", R, (int)SSD, NW, SIDE, grid,
                 blocks_per_cu[dev], SM);
     // age levels: with one block per resident slot, block b is the (b / num_cu)-th block its CU

@@ -29,8 +29,20 @@ def _ptr(t):
 
 
 def _device_index(t):
-    d = t.device
-    return d.index if d.index is not None else 0
+    i = t.get_device()  # one call (the per-frame checks below run on every launch)
+    return i if i >= 0 else 0
+
+
+_DTYPES = {}
+
+
+def _dt(name):
+    """torch dtype object for "torch.<name>" (cached: identity tests instead of str() per call)."""
+    d = _DTYPES.get(name)
+    if d is None:
+        import torch
+        d = _DTYPES[name] = getattr(torch, name.split(".")[-1])
+    return d
 
 
 def _check_inputs_on(dev, *ts):
@@ -50,9 +62,9 @@ def _check_out(t, shape, dtype_name, dev, name):
         return
     if not hasattr(t, "data_ptr") or not getattr(t, "is_cuda", False):
         raise ValueError(f"{name} must be a device tensor (or a raw device pointer)")
-    if str(t.dtype) != dtype_name:
+    if t.dtype is not _dt(dtype_name):
         raise ValueError(f"{name} must be {dtype_name.split('.')[-1]}, got {str(t.dtype).split('.')[-1]}")
-    if tuple(t.shape) != tuple(shape):
+    if t.shape != tuple(shape):
         raise ValueError(f"{name} must have shape {tuple(shape)}, got {tuple(t.shape)}")
     if not t.is_contiguous():
         raise ValueError(f"{name} must be contiguous")
@@ -165,12 +177,12 @@ class HipBlockMatcher:
         else:
             if left.dtype != right.dtype or left.shape != right.shape or left.dim() != 2:
                 raise ValueError("left and right must be uint8 H x W tensors of the same shape")
-            if str(left.dtype) != "torch.uint8" or left.stride(1) != 1 or right.stride(1) != 1 or \
-                    left.stride(0) != right.stride(0):
+            ls, rs = left.stride(), right.stride()
+            if left.dtype is not _dt("torch.uint8") or ls[1] != 1 or rs[1] != 1 or ls[0] != rs[0]:
                 raise ValueError("inputs must be uint8 with unit column stride and equal row strides")
             _check_inputs_on(self.device, left, right)
             H, W = left.shape
-            lp, rp, st = left.data_ptr(), right.data_ptr(), left.stride(0)
+            lp, rp, st = left.data_ptr(), right.data_ptr(), ls[0]
         if out_fixed is None and out_float is None:
             raise ValueError("at least one of out_fixed / out_float is required")
         _check_out(out_fixed, (H, W), "torch.int16", self.device, "out_fixed")
