@@ -59,7 +59,9 @@ extern "C" {
  *                      sub-pixel disparity's floor and ceiling are tested and the pixel is dropped
  *                      only if both have a disp2 entry and both differ by more than disp12MaxDiff
  *                      (which is max(disp12_max_diff, 1): always on); valid band
- *                      x in [max(m + D, 0), W + min(m, 0)).  Runs on the volume path (K1 + K2). */
+ *                      x in [max(m + D, 0), W + min(m, 0)).  Runs on both paths: the volume path
+ *                      in K2, the fused path as a separate left-pass build (each unique winner
+ *                      offers its key by one atomicMin) + lr_fixup_sgbm. */
 #define DSX_LR_FORM_BM 0
 #define DSX_LR_FORM_SGBM 1
 
