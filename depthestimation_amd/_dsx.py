@@ -62,7 +62,8 @@ class DsxParams(ctypes.Structure):
         ("speckle_window_size", ctypes.c_int32),
         ("speckle_range", ctypes.c_int32),
         ("lr_form", ctypes.c_int32),
-        ("reserved", ctypes.c_int32 * 3),
+        ("in_flight", ctypes.c_int32),
+        ("reserved", ctypes.c_int32 * 2),
     ]
 
 
@@ -188,7 +189,8 @@ def default_params() -> DsxParams:
 def make_params(min_disp=0, num_disp=128, block_size=5, cost="sad", uniqueness_ratio=10,
                 disp12_max_diff=1, subpixel=True, float_mode="fixed", path="fused",
                 timing=False, grid_blocks=0, aggregation=None, p1=0, p2=0, prefilter_cap=31,
-                sgbm_post=False, speckle_window_size=50, speckle_range=2, lr_form="bm") -> DsxParams:
+                sgbm_post=False, speckle_window_size=50, speckle_range=2, lr_form="bm",
+                in_flight=False) -> DsxParams:
     p = default_params()
     p.min_disp = int(min_disp)
     p.num_disp = int(num_disp)
@@ -219,6 +221,7 @@ def make_params(min_disp=0, num_disp=128, block_size=5, cost="sad", uniqueness_r
     if lr_form not in LR_FORM:
         raise ValueError(f"lr_form must be one of {list(LR_FORM)}")
     p.lr_form = LR_FORM[lr_form]
+    p.in_flight = int(bool(in_flight))
     return p
 
 

@@ -111,6 +111,7 @@ int check(const dsx_params *p) {
     if (p->path != DSX_PATH_FUSED && p->path != DSX_PATH_VOLUME) return fail(DSX_EINVAL, "path must be 0 or 1");
     if (p->lr_form != DSX_LR_FORM_BM && p->lr_form != DSX_LR_FORM_SGBM)
         return fail(DSX_EINVAL, "lr_form must be 0 (bm) or 1 (sgbm)");
+    if (p->in_flight != 0 && p->in_flight != 1) return fail(DSX_EINVAL, "in_flight must be 0 or 1");
     if (p->grid_blocks < 0) return fail(DSX_EINVAL, "grid_blocks must be >= 0");
     if (p->min_disp < -2047 || p->min_disp + p->num_disp > 2047)
         return fail(DSX_EINVAL, "min_disp/num_disp out of the int16 x16 fixed-point range");
@@ -418,12 +419,15 @@ dsx::Bm2Args base_args(dsx_handle *h, int H, int W, int64_t stride, const DsxEnv
         // Balance (measured on C2-C5, profiles/README.md r01d): co-resident waves drop their issue
         // priority as they pass 50 / 80 / 95 % of their rows, and strips on the clamped-load
         // path count 11/8 of a fast strip.  DSX_PRIO=0 / DSX_PRIO_T / DSX_SLOW_W8 override.
-        a.prio = env.prio ? atoi(env.prio) : 1;
+        // in_flight handles: no priority bands and equal age weights (profiles/r04af_balance_in_flight.txt:
+        // C4 19.5k -> 20.8k Mpix/s with 3 frames in flight; a lone launch needs the balance)
+        const bool fl = h->p.in_flight != 0;
+        a.prio = env.prio ? atoi(env.prio) : (fl ? 0 : 1);
         a.pt1 = 128, a.pt2 = 205, a.pt3 = 243;
         if (env.prio_t) sscanf(env.prio_t, "%d,%d,%d", &a.pt1, &a.pt2, &a.pt3);
         a.slow_w8 = env.slow_w8 ? atoi(env.slow_w8) : 11;
         // age-level work weights (single frames; r01f A/B: C2 83.6 -> 81.7 us, C4 61.4 -> 59.9 us)
-        a.agew[0] = 78, a.agew[1] = 70, a.agew[2] = a.agew[3] = 64;
+        a.agew[0] = fl ? 64 : 78, a.agew[1] = fl ? 64 : 70, a.agew[2] = a.agew[3] = 64;
         if (env.agew) sscanf(env.agew, "%d,%d,%d,%d", &a.agew[0], &a.agew[1], &a.agew[2], &a.agew[3]);
         a.nlev = 0;  // set by the launcher from the residency it computes
         a.variant = env.variant ? atoi(env.variant) : 0;

@@ -78,12 +78,12 @@ class HipBlockMatcher:
     def __init__(self, min_disp=0, num_disp=128, block_size=5, cost="sad", uniqueness_ratio=10,
                  disp12_max_diff=1, subpixel=True, float_mode="fixed", path="fused", device=0,
                  timing=False, grid_blocks=0, aggregation=None, p1=0, p2=0, prefilter_cap=31,
-                 sgbm_post=False, speckle_window_size=50, speckle_range=2, lr_form="bm"):
+                 sgbm_post=False, speckle_window_size=50, speckle_range=2, lr_form="bm", in_flight=False):
         self.device = int(device)
         self._params = _dsx.make_params(min_disp, num_disp, block_size, cost, uniqueness_ratio,
                                         disp12_max_diff, subpixel, float_mode, path, timing,
                                         grid_blocks, aggregation, p1, p2, prefilter_cap, sgbm_post,
-                                        speckle_window_size, speckle_range, lr_form)
+                                        speckle_window_size, speckle_range, lr_form, in_flight)
         _dsx.check_params(self._params)  # validates on the host, no device needed
         self._h = None
         self._cfg = dict(min_disp=min_disp, num_disp=num_disp, block_size=block_size, cost=cost,
@@ -91,7 +91,8 @@ class HipBlockMatcher:
                          subpixel=subpixel, float_mode=float_mode, path=path, timing=timing,
                          grid_blocks=grid_blocks, aggregation=aggregation, p1=p1, p2=p2,
                          prefilter_cap=prefilter_cap, sgbm_post=sgbm_post,
-                         speckle_window_size=speckle_window_size, speckle_range=speckle_range, lr_form=lr_form)
+                         speckle_window_size=speckle_window_size, speckle_range=speckle_range, lr_form=lr_form,
+                         in_flight=in_flight)
 
     # -- lifetime ---------------------------------------------------------------------------
     def _handle(self):

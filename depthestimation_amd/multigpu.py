@@ -233,7 +233,9 @@ class HostPipeline:
         kw.pop("device", None)
         self.streams = [torch.cuda.Stream(device=self.dev) for _ in range(max(1, int(streams)))]
         # one handle per stream: a handle's scratch (LR keys, cost volume) orders its calls across
-        # streams, so with one handle the LR / volume configs would run one frame at a time
+        # streams, so with one handle the LR / volume configs would run one frame at a time; with
+        # several streams the handles know frames overlap (dsx_params.in_flight)
+        kw.setdefault("in_flight", len(self.streams) > 1)
         self.ms = [HipBlockMatcher(device=int(device), **kw) for _ in self.streams]
         self.m = self.ms[0]
         self.shape = None
@@ -349,14 +351,17 @@ class DepthPipeline:
         # keys) orders its calls across streams, so a shared handle would run one frame at a time.  The
         # other streams use shallow copies of ``core`` (same parameters and rectification cache) with
         # a handle of their own.
+        # With several streams every stream gets a copy with its own in-flight handle (dsx_params.in_flight:
+        # the balance for a lone frame is dropped); the caller's core keeps its own handle untouched.
         self.cores = [core]
         self._own = []
-        for _ in self.streams[1:]:
-            c = copy.copy(core)
-            if getattr(core, "sgbm", None) is not None and hasattr(core.sgbm, "params"):
-                c.sgbm = HipBlockMatcher(**dict(core.sgbm.params))
+        if len(self.streams) > 1 and getattr(core, "sgbm", None) is not None and hasattr(core.sgbm, "params"):
+            self.cores = []
+            for _ in self.streams:
+                c = copy.copy(core)
+                c.sgbm = HipBlockMatcher(**dict(core.sgbm.params, in_flight=True))
                 self._own.append(c.sgbm)
-            self.cores.append(c)
+                self.cores.append(c)
         self.shape = None
         self.pending: List[Optional[Tuple[int, object, object]]] = [None] * self.depth
 

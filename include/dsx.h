@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define DSX_VERSION 103 /* 1.0.3: dsx_process_pair_device (the per-frame _process_pair in one call), dsx_fill_holes_status */
+#define DSX_VERSION 104 /* 1.0.4: dsx_params.in_flight; 1.0.3: dsx_process_pair_device, dsx_fill_holes_status */
 
 #define DSX_OK 0
 #define DSX_EINVAL (-1) /* bad argument (mirrors ValueError / cv2.error on bad input) */
@@ -102,7 +102,11 @@ typedef struct dsx_params {
     int32_t speckle_window_size; /* 'speckle_window_size' (stereo_core.py:23), >= 0              */
     int32_t speckle_range;    /* 'speckle_range'     (stereo_core.py:24), maxDiff = 16 * range   */
     int32_t lr_form;          /* DSX_LR_FORM_BM (default) | DSX_LR_FORM_SGBM                     */
-    int32_t reserved[3];
+    int32_t in_flight;        /* 1: the caller keeps other frames in flight on other handles and  */
+                              /* streams (multigpu.DepthPipeline / HostPipeline): the fused pass  */
+                              /* drops the balance that makes one frame's blocks finish together */
+                              /* (priority bands, age weights) - the next frame fills the tail     */
+    int32_t reserved[2];
 } dsx_params;
 
 typedef struct dsx_handle dsx_handle;

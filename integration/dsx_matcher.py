@@ -16,7 +16,7 @@ class _Params(ctypes.Structure):
     _fields_ = [(n, ctypes.c_int32) for n in (
         "min_disp", "num_disp", "block_size", "cost", "uniqueness_ratio", "disp12_max_diff",
         "subpixel", "float_mode", "path", "timing", "grid_blocks", "aggregation", "p1", "p2",
-        "prefilter_cap", "sgbm_post", "speckle_window_size", "speckle_range", "lr_form")] + [("reserved", ctypes.c_int32 * 3)]
+        "prefilter_cap", "sgbm_post", "speckle_window_size", "speckle_range", "lr_form", "in_flight")] + [("reserved", ctypes.c_int32 * 2)]
 
 
 # sgbm_mode names (stereo_core.py:55-61) -> DSX_AGG_* (semi-global aggregation over SAD costs)
