@@ -67,6 +67,9 @@
 #ifndef DSX_INIT_SB  // SSD segment init: scheduling barrier between column chunks
 #define DSX_INIT_SB 1
 #endif
+#ifndef DSX_LRCOAL  // SAD LR pass: the row's partial keys staged per wave in LDS, atomics on contiguous words
+#define DSX_LRCOAL 0  // WRITE_SIZE C4 -29 %, but C4 +6 %, C2r +9 % in time (r04ah): the LDS round trip sits in the row step
+#endif
 #ifndef DSX_SSD_LDSDIAG  // SSD LR pass (NW >= 2): right-view winners read from the finished tile
 #define DSX_SSD_LDSDIAG 0  // measured slower (C3 325 -> 383 us): the reads wait in pairs at 128 VGPRs
 #endif
@@ -161,6 +164,8 @@ struct Geo {
     static constexpr int SLOT = SROW + REFB;
     static constexpr int SMEM0 = 4 * SLOT + TX * PITCH;
     static constexpr int SMEM = SMEM0 > (2 * R + 1) * SLOT ? SMEM0 : (2 * R + 1) * SLOT;
+    // LR pass, per-wave region after SMEM: the 31 exits (+ with DSX_LRCOAL the 128 end-of-row keys)
+    static constexpr int XRB = (!SSD && DSX_LRCOAL) ? 640 : 128;
 };
 
 // Diagnostic build (-DDSX_STAMPS, libdsx_diag.so): per-phase s_memtime sums per block.
@@ -313,9 +318,13 @@ __device__ __forceinline__ void bm2_segment(const Bm2Args &a_in, uint8_t *smem, 
             w1 = side == 1 ? p[4] : p[-1];
         } else {
             uint32_t v[4];
+            // the SAD LR build (DSX_LRCOAL) recomputes 4 * tid here: hoisted, the 4 clamped indices
+            // below were held across the kernel and spilled (16 B of scratch)
+            int t4 = 4 * tid;
+            if constexpr (SIDE == 3 && !SSD && DSX_LRCOAL) asm volatile("" : "+v"(t4));
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
-                const int j = min(4 * tid + q, NJ - 1);
+                const int j = min(t4 + q, NJ - 1);
                 const int pp = PB + sgn * j;
                 uint32_t t = srow[clampi2(pp, 0, W - 1)];
                 if constexpr (!SSD) t |= (uint32_t)srow[clampi2(pp + sgn, 0, W - 1)] << 16;
@@ -749,7 +758,7 @@ __device__ __forceinline__ void bm2_segment(const Bm2Args &a_in, uint8_t *smem, 
                 // single-lane b128 store; r03: 31 exec-masked b32 stores per row cost ~6 % at C2r),
                 // else this wave's slot in each tile row's padding
                 constexpr bool XREG = SSD ? DSX_SSD_XB : DSX_XB4;  // exits in the per-wave region
-                uint8_t *xq = XREG ? smem + G::SMEM + 128 * wv : tile + Dp * CB + 4 * wv;
+                uint8_t *xq = XREG ? smem + G::SMEM + G::XRB * wv : tile + Dp * CB + 4 * wv;
                 constexpr int XST = XREG ? 4 : PITCH;
                 uint32_t X[4] = {0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu};
                 uint32_t Ae = 0xFFFFFFFFu, Ao = 0xFFFFFFFFu, E = 0xFFFFFFFFu;
@@ -836,6 +845,25 @@ __device__ __forceinline__ void bm2_segment(const Bm2Args &a_in, uint8_t *smem, 
                 uint32_t *krow = a.lr_keys + fout + (long)y * W;
                 const int dtop = (wv + 1) * G::LDW - 1;  // disparity of the wave's top slot
                 if constexpr (DSX_EXP & 2) {
+                } else if constexpr (!SSD && XREG && DSX_LRCOAL) {
+                    // The row's 159 partial keys name the right pixels base .. base + 158 in order:
+                    // exit k at base + k, lane l's Ao / Ae at base + 157 - 2l / 158 - 2l.  Staged at word
+                    // j of the wave's region, they leave as three atomics on consecutive words: 10-11
+                    // 64-B requests a row step instead of 18-19 for the two stride-8-B pair atomics +
+                    // the exits
+                    uint32_t *xw = reinterpret_cast<uint32_t *>(xq);
+                    xw[157 - 2 * ln] = Ao;
+                    xw[158 - 2 * ln] = Ae;
+                    const int base = x0 - m - dtop;
+#pragma unroll
+                    for (int i = 0; i < 3; ++i) {
+                        const int j = 64 * i + ln;
+                        if (i < 2 || ln < 31) {
+                            const uint32_t K = xw[j];
+                            const int xk = base + j;
+                            if (K != 0xFFFFFFFFu && xk >= 0 && xk < W) atomicMin(krow + xk, K);
+                        }
+                    }
                 } else if constexpr (SSD && !DSX_SSD_XB) {
                     const int xe = x0 + (TX - 2 - ln) - m - dtop;  // E lane j: exit of pixel TX-2-j
                     if (ln < TX - 1 && E != 0xFFFFFFFFu && xe >= 0 && xe < W) atomicMin(krow + xe, E);
@@ -845,8 +873,9 @@ __device__ __forceinline__ void bm2_segment(const Bm2Args &a_in, uint8_t *smem, 
                     if (E != 0xFFFFFFFFu && xe >= 0 && xe < W) atomicMin(krow + xe, E);
                 }
                 const int xa = x0 + TX - 1 - m - d0;
-                if (!(DSX_EXP & 2) && Ae != 0xFFFFFFFFu && xa >= 0 && xa < W) atomicMin(krow + xa, Ae);
-                if constexpr (!SSD && !(DSX_EXP & 2)) {
+                if constexpr (!SSD && XREG && DSX_LRCOAL) {
+                } else if (!(DSX_EXP & 2) && Ae != 0xFFFFFFFFu && xa >= 0 && xa < W) atomicMin(krow + xa, Ae);
+                if constexpr (!SSD && !(DSX_EXP & 2) && !(XREG && DSX_LRCOAL)) {
                     if (Ao != 0xFFFFFFFFu && xa - 1 >= 0 && xa - 1 < W) atomicMin(krow + xa - 1, Ao);
                 }
             } else if (lane_writes) {
@@ -1285,7 +1314,7 @@ static hipError_t launch_bm2_side(const Bm2Args &a, hipStream_t st) {
     using G = Geo<R, SSD, NW>;
     // + the LR exit region; the LDS-diagonal SSD LR pass reads up to TX * 4 - 24 B past the tile
     constexpr bool LDSD = SIDE == 3 && SSD && !ABS && NW >= 2 && DSX_SSD_LDSDIAG;
-    constexpr int SM = G::SMEM + ((SIDE == 3 && (SSD ? DSX_SSD_XB : DSX_XB4)) ? 128 * NW : 0) + (LDSD ? 128 : 0);
+    constexpr int SM = G::SMEM + ((SIDE == 3 && (SSD ? DSX_SSD_XB : DSX_XB4)) ? G::XRB * NW : 0) + (LDSD ? 128 : 0);
     const void *fn = (const void *)bm2<R, SSD, NW, SIDE, ABS>;
     static int blocks_per_cu[64] = {};
     static int num_cu[64] = {};
