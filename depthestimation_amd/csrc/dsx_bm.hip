@@ -318,10 +318,12 @@ __device__ __forceinline__ void bm2_segment(const Bm2Args &a_in, uint8_t *smem, 
             w1 = side == 1 ? p[4] : p[-1];
         } else {
             uint32_t v[4];
-            // the SAD LR build (DSX_LRCOAL) recomputes 4 * tid here: hoisted, the 4 clamped indices
-            // below were held across the kernel and spilled (16 B of scratch)
+            // The one-wave SAD LR builds recompute 4 * tid per load: hoisted, the 4 clamped indices
+            // below are held across the kernel (with DSX_LRCOAL they spilled).  C4 19.5k -> 21.5k
+            // Mpix/s with 3 frames in flight, C2r +1.5 %; the R >= 6 and two-wave builds measured
+            // slower with it (C5 -0.5 %, C1 at D = 140 with the checks +2.5 %: profiles/r04ai_*)
             int t4 = 4 * tid;
-            if constexpr (SIDE == 3 && !SSD && DSX_LRCOAL) asm volatile("" : "+v"(t4));
+            if constexpr (!SSD && SIDE == 3 && NW == 1) asm volatile("" : "+v"(t4));
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
                 const int j = min(t4 + q, NJ - 1);
