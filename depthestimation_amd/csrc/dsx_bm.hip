@@ -70,6 +70,9 @@
 #ifndef DSX_LRCOAL  // SAD LR pass: the row's partial keys staged per wave in LDS, atomics on contiguous words
 #define DSX_LRCOAL 0  // WRITE_SIZE C4 -29 %, but C4 +6 %, C2r +9 % in time (r04ah): the LDS round trip sits in the row step
 #endif
+#ifndef DSX_T4B  // one-wave SAD builds whose slow-path staging indices are recomputed per load: 1 LR, 2 others
+#define DSX_T4B 1
+#endif
 #ifndef DSX_SSD_LDSDIAG  // SSD LR pass (NW >= 2): right-view winners read from the finished tile
 #define DSX_SSD_LDSDIAG 0  // measured slower (C3 325 -> 383 us): the reads wait in pairs at 128 VGPRs
 #endif
@@ -323,7 +326,8 @@ __device__ __forceinline__ void bm2_segment(const Bm2Args &a_in, uint8_t *smem, 
             // Mpix/s with 3 frames in flight, C2r +1.5 %; the R >= 6 and two-wave builds measured
             // slower with it (C5 -0.5 %, C1 at D = 140 with the checks +2.5 %: profiles/r04ai_*)
             int t4 = 4 * tid;
-            if constexpr (!SSD && SIDE == 3 && NW == 1) asm volatile("" : "+v"(t4));
+            if constexpr (!SSD && NW == 1 && (((DSX_T4B & 1) && SIDE == 3) || ((DSX_T4B & 2) && SIDE != 3)))
+                asm volatile("" : "+v"(t4));
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
                 const int j = min(t4 + q, NJ - 1);
