@@ -285,6 +285,7 @@ def main():
                     help="SGM aggregation mode (SURVEY 8f F4; volume path + path passes); not the headline")
     ap.add_argument("--no-process-group", action="store_true",
                     help="at N = 1, skip the one-rank process group (collectives become local no-ops)")
+    ap.add_argument("--breakdown-steps", type=int, default=500, help="launches of the one-stream kernel timing pass")
     ap.add_argument("--no-dropin", action="store_true",
                     help="skip the drop-in pipeline secondary (StereoCore defaults, one call per frame)")
     ap.add_argument("--selftest-launch", action="store_true", help=argparse.SUPPRESS)
@@ -486,10 +487,11 @@ def main():
     # breakdown pass: per-kernel HIP events on the same stream (outside the timed region), only for
     # paths with several kernels per step; the fused pass without the LR check is one kernel, whose
     # launch duration is the timed region's per-step GPU time
-    # 100 steps after the handle ran back to back for the settle time: a 20-step breakdown right after
-    # the parity re-check started on lowered clocks and read the C3 LR pass 13 % slow (337 against
-    # 298 us under rocprofv3; tools/timing_probe.py, profiles/r04v_timing_probe.json)
-    nbd = 100
+    # --breakdown-steps (500) steps after the handle ran back to back for the settle time: a 20-step
+    # breakdown right after the parity re-check started on lowered clocks and read the C3 LR pass 13 %
+    # slow (337 against 298 us under rocprofv3; profiles/r04v_timing_probe.json), and 100 steps read
+    # C4's pass 49.1-51.9 us against 48.6-48.9 at 500 (profiles/r04am_breakdown_steps.txt)
+    nbd = args.breakdown_steps
     if args.path == "fused" and cfg["disp12_max_diff"] < 0:
         if S == 1:
             ktimes = {"bm_pass_left": (region_ms, args.steps)}
