@@ -285,6 +285,8 @@ def main():
                     help="SGM aggregation mode (SURVEY 8f F4; volume path + path passes); not the headline")
     ap.add_argument("--no-process-group", action="store_true",
                     help="at N = 1, skip the one-rank process group (collectives become local no-ops)")
+    ap.add_argument("--in-flight", default="0", choices=["auto", "0", "1"],
+                    help="the timed lanes' handles carry dsx_params.in_flight (auto: when --streams > 1)")
     ap.add_argument("--breakdown-steps", type=int, default=500, help="launches of the one-stream kernel timing pass")
     ap.add_argument("--no-dropin", action="store_true",
                     help="skip the drop-in pipeline secondary (StereoCore defaults, one call per frame)")
@@ -387,11 +389,19 @@ def main():
     # frames in flight (the timed region, its warmup and settling): S handles (a handle's LR / volume
     # scratch is its own), S streams, S output sets; lane 0 is the parity-checked matcher on `stream`
     S = max(1, args.streams)
-    lanes = [(matcher, stream, out_fixed, out_float)]
+    # --in-flight: the lanes' handles carry dsx_params.in_flight (the fused pass drops the balance a lone
+    # frame needs, as DepthPipeline's handles do); `matcher` itself stays a lone-frame handle for the
+    # parity checks and the one-stream kernel timing pass
+    lane_ifl = args.in_flight == "1" or (args.in_flight == "auto" and S > 1)
+    lane_kw = dict(kw, in_flight=True) if lane_ifl else kw
+
+    def lane_matcher():
+        return HipBlockMatcher(device=local, path=args.path, timing=False, grid_blocks=args.grid_blocks,
+                               aggregation=args.sgm, **lane_kw)
+
+    lanes = [(lane_matcher() if lane_ifl else matcher, stream, out_fixed, out_float)]
     for _ in range(S - 1):
-        lanes.append((HipBlockMatcher(device=local, path=args.path, timing=False, grid_blocks=args.grid_blocks,
-                                      aggregation=args.sgm, **kw), torch.cuda.Stream(dev),
-                      torch.empty_like(out_fixed), torch.empty_like(out_float)))
+        lanes.append((lane_matcher(), torch.cuda.Stream(dev), torch.empty_like(out_fixed), torch.empty_like(out_float)))
 
     def tstep(i):
         m, st, of, ff = lanes[i % S]
@@ -596,7 +606,7 @@ def main():
             "order": "parity check -> secondary measurements -> the K steps unsettled -> clock settling -> warmup "
                      "-> timed region -> breakdown pass -> CPU baseline",
             "settle": {"seconds": args.settle, "steps": settle_steps, "timed": False},
-            "streams": {"frames_in_flight": S,
+            "streams": {"frames_in_flight": S, "in_flight_handles": lane_ifl,
                         "note": "step i runs on HIP stream i mod S with its own handle and output buffers (a frame's "
                                 "work is unchanged; consecutive frames overlap the persistent pass's tail); "
                                 "--streams 1 is one frame at a time"},
