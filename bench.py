@@ -285,7 +285,7 @@ def main():
                     help="SGM aggregation mode (SURVEY 8f F4; volume path + path passes); not the headline")
     ap.add_argument("--no-process-group", action="store_true",
                     help="at N = 1, skip the one-rank process group (collectives become local no-ops)")
-    ap.add_argument("--in-flight", default="0", choices=["auto", "0", "1"],
+    ap.add_argument("--in-flight", default="auto", choices=["auto", "0", "1"],
                     help="the timed lanes' handles carry dsx_params.in_flight (auto: when --streams > 1)")
     ap.add_argument("--breakdown-steps", type=int, default=500, help="launches of the one-stream kernel timing pass")
     ap.add_argument("--no-dropin", action="store_true",
