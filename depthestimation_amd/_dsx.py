@@ -32,7 +32,8 @@ EXPORTS = (
     "dsx_set_params", "dsx_compute_host", "dsx_compute_device", "dsx_compute_batch_device", "dsx_right_map_device",
     "dsx_postprocess_fast_device", "dsx_postprocess_workspace_bytes", "dsx_postprocess_full_device",
     "dsx_postprocess_full_ex_device", "dsx_fill_holes_workspace_bytes", "dsx_fill_holes_device",
-    "dsx_rectify_device", "dsx_fill_holes_status", "dsx_process_pair_device",
+    "dsx_rectify_device", "dsx_fill_holes_status", "dsx_process_pair_device", "dsx_fill_holes_ex_device",
+    "dsx_fill_holes_status_ws", "dsx_fill_holes_status_handle",
     "dsx_kernel_times", "dsx_reset_times", "dsx_workspace_bytes", "dsx_destroy", "dsx_last_error",
     "dsx_comm_init_all", "dsx_comm_size", "dsx_bcast", "dsx_comm_destroy",
 )
@@ -87,7 +88,18 @@ class DsxPostParams(ctypes.Structure):
         ("fill_radius", ctypes.c_int32),
         ("has_depth", ctypes.c_int32),
         ("has_max_depth", ctypes.c_int32),
-        ("reserved", ctypes.c_int32 * 5),
+        ("fill_spin_limit", ctypes.c_uint32),
+        ("fill_steps", ctypes.c_int32),
+        ("reserved", ctypes.c_int32 * 3),
+    ]
+
+
+class DsxFillOpts(ctypes.Structure):
+    """dsx_fill_opts (include/dsx.h): launch shape of the hole-filling march (tests, experiments)."""
+    _fields_ = [
+        ("spin_limit", ctypes.c_uint32),
+        ("steps", ctypes.c_int32),
+        ("reserved", ctypes.c_int32 * 6),
     ]
 
 
@@ -125,6 +137,10 @@ def _bind(lib):
                                                         ctypes.c_double, ctypes.c_double, ctypes.c_double,
                                                         ctypes.c_double, i32, vp]),
         "dsx_fill_holes_status": (ctypes.c_int, []),
+        "dsx_fill_holes_status_ws": (ctypes.c_int, [vp]),
+        "dsx_fill_holes_status_handle": (ctypes.c_int, [vp]),
+        "dsx_fill_holes_ex_device": (ctypes.c_int, [vp, i32, i32, i64, i32, vp, vp, ctypes.c_size_t,
+                                                     ctypes.POINTER(DsxFillOpts), vp]),
         "dsx_process_pair_device": (ctypes.c_int, [vp, vp, vp, i32, i32, i64, ctypes.POINTER(DsxPostParams), vp, vp,
                                                     vp]),
         "dsx_kernel_times": (ctypes.c_int, [vp, ctypes.c_char_p, ctypes.c_int, ctypes.POINTER(ctypes.c_float),

@@ -469,10 +469,17 @@ struct TimingHook : dsx::LaunchHook {
     }
 };
 
-int sticky_inpaint_timeout() {
-    if (dsx::inpaint_take_timeout())
-        return fail(DSX_EHIP, "hole filling: a grid barrier of the persistent march timed out; the holes of that "
-                              "call were left unfilled (its results are invalid)");
+// key: the caller's workspace (dsx_fill_holes_device, dsx_postprocess_full_ex_device) or the handle
+// (dsx_process_pair_device); nullptr: any
+int sticky_inpaint_timeout(const void *key) {
+    if (key ? dsx::inpaint_take_timeout(key) : dsx::inpaint_take_timeout_any())
+        return fail(DSX_EHIP, "hole filling: the persistent march timed out; the holes of that call were left "
+                              "unfilled (its results are invalid)");
+    return DSX_OK;
+}
+
+int check_fill_shape(int64_t H, int64_t W) {
+    if (H * W >= dsx::kInpaintMaxPixels) return fail(DSX_EINVAL, "image too large for hole filling (H * W >= 2^30)");
     return DSX_OK;
 }
 
@@ -874,10 +881,9 @@ int dsx_postprocess_full_ex_device(const void *d_disp, int32_t H, int32_t W, int
     if (!d_workspace || workspace_bytes < dsx::post_full_workspace(H, W, crop))
         return fail(DSX_EINVAL, "workspace too small (dsx_postprocess_workspace_bytes)");
     if ((int64_t)H * (W - crop) > 0x7FFFFFFF) return fail(DSX_EINVAL, "image too large for int32 labels");
-    if (fill_radius > 0 && W - crop > dsx::kInpaintMaxW)
-        return fail(DSX_EINVAL, "image too wide for hole filling (W > 19200)");
     if (fill_radius > 0) {
-        const int rc = sticky_inpaint_timeout();
+        int rc = check_fill_shape(H, W - crop);
+        if (!rc) rc = sticky_inpaint_timeout(d_workspace);
         if (rc) return rc;
     }
     dsx::PostFullArgs a{};
@@ -908,21 +914,32 @@ size_t dsx_fill_holes_workspace_bytes(int32_t H, int32_t W) {
     return dsx::inpaint_workspace(H, W);
 }
 
-int dsx_fill_holes_device(const void *d_disp, int32_t H, int32_t W, int64_t in_pitch, int32_t radius, void *d_out,
-                          void *d_workspace, size_t workspace_bytes, void *hip_stream) {
+int dsx_fill_holes_ex_device(const void *d_disp, int32_t H, int32_t W, int64_t in_pitch, int32_t radius, void *d_out,
+                             void *d_workspace, size_t workspace_bytes, const dsx_fill_opts *opts, void *hip_stream) {
     g_err.clear();
     if (!d_disp || !d_out) return fail(DSX_EINVAL, "NULL input or output");
     if (H <= 0 || W <= 0 || in_pitch < W) return fail(DSX_EINVAL, "bad shape / pitch");
     if (radius < 0) return fail(DSX_EINVAL, "radius must be >= 0");
-    if ((int64_t)H * W > 0x7FFFFFFF) return fail(DSX_EINVAL, "image too large");
-    if (W > dsx::kInpaintMaxW) return fail(DSX_EINVAL, "image too wide for hole filling (W > 19200)");
+    int rc = check_fill_shape(H, W);
+    if (rc) return rc;
     if (!d_workspace || workspace_bytes < dsx::inpaint_workspace(H, W))
         return fail(DSX_EINVAL, "workspace too small (dsx_fill_holes_workspace_bytes)");
-    const int rc = sticky_inpaint_timeout();
+    rc = sticky_inpaint_timeout(d_workspace);
     if (rc) return rc;
+    dsx::InpaintOpts o;
+    if (opts) {
+        o.spin_limit = opts->spin_limit;
+        o.steps = opts->steps == 0 ? -1 : std::max(0, (int)opts->steps);
+    }
     DSX_HIP(dsx::launch_inpaint(static_cast<const float *>(d_disp), in_pitch, H, W, radius, static_cast<float *>(d_out),
-                                d_workspace, static_cast<hipStream_t>(hip_stream)));
+                                d_workspace, static_cast<hipStream_t>(hip_stream), o));
     return DSX_OK;
+}
+
+int dsx_fill_holes_device(const void *d_disp, int32_t H, int32_t W, int64_t in_pitch, int32_t radius, void *d_out,
+                          void *d_workspace, size_t workspace_bytes, void *hip_stream) {
+    return dsx_fill_holes_ex_device(d_disp, H, W, in_pitch, radius, d_out, d_workspace, workspace_bytes, nullptr,
+                                    hip_stream);
 }
 
 int dsx_rectify_device(const void *d_img, int32_t Hs, int32_t Ws, int64_t stride_bytes, int32_t channels,
@@ -1007,7 +1024,19 @@ int dsx_compute_host(dsx_handle *h, const uint8_t *L, const uint8_t *R, int32_t 
 
 int dsx_fill_holes_status(void) {
     g_err.clear();
-    return sticky_inpaint_timeout();
+    return sticky_inpaint_timeout(nullptr);
+}
+
+int dsx_fill_holes_status_ws(const void *d_workspace) {
+    g_err.clear();
+    if (!d_workspace) return fail(DSX_EINVAL, "workspace is NULL");
+    return sticky_inpaint_timeout(d_workspace);
+}
+
+int dsx_fill_holes_status_handle(dsx_handle *h) {
+    g_err.clear();
+    if (!h) return fail(DSX_EINVAL, "handle is NULL");
+    return sticky_inpaint_timeout(h);
 }
 
 int dsx_process_pair_device(dsx_handle *h, const void *dL, const void *dR, int32_t H, int32_t W, int64_t stride_bytes,
@@ -1030,8 +1059,8 @@ int dsx_process_pair_device(dsx_handle *h, const void *dL, const void *dR, int32
     const bool depth = pp->has_depth != 0;
     if (Wc <= 0 || (!d_out_disp && !(depth && d_out_depth))) return DSX_OK;  // disp[:, num_disp:] is empty
     if (pp->mode == DSX_POST_FULL && pp->fill_radius > 0) {
-        if (Wc > dsx::kInpaintMaxW) return fail(DSX_EINVAL, "image too wide for hole filling (W > 19200)");
-        rc = sticky_inpaint_timeout();
+        rc = check_fill_shape(H, Wc);
+        if (!rc) rc = sticky_inpaint_timeout(h);
         if (rc) return rc;
     }
     DSX_HIP(hipSetDevice(h->device));
@@ -1096,6 +1125,9 @@ int dsx_process_pair_device(dsx_handle *h, const void *dL, const void *dR, int32
         a.max_depth = (float)pp->max_depth;
         a.has_max = pp->has_max_depth ? 1 : 0;
         a.fill_radius = pp->fill_radius;
+        a.fill_opts.status_key = h;  // the handle's own timeout flag and step history
+        a.fill_opts.spin_limit = pp->fill_spin_limit;
+        a.fill_opts.steps = pp->fill_steps == 0 ? -1 : std::max(0, (int)pp->fill_steps);
         TimingHook hook(h);
         hipError_t e = dsx::launch_post_full(a, h->ppWs, st, h->p.timing ? &hook : nullptr);
         if (e != hipSuccess) return fail(DSX_EHIP, std::string("post-processing launch: ") + hipGetErrorString(e));
@@ -1172,6 +1204,7 @@ int dsx_destroy(dsx_handle *h) {
     (void)hipSetDevice(h->device);
     (void)hipStreamSynchronize(h->stream);
     collect_times(h);
+    dsx::inpaint_forget(h);
     for (auto &e : h->free_events) {
         (void)hipEventDestroy(e.first);
         (void)hipEventDestroy(e.second);

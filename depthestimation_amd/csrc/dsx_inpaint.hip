@@ -2,37 +2,38 @@
 // from postprocess_disparity :160-166 when StereoCore's hole_filling is set, stereo_core.py:175-184),
 // i.e. cv2.inpaint(..., INPAINT_TELEA) on the pixels with d <= 0.
 //
-// Telea's fast-marching inpainting, marched in 4-connected distance layers so each layer is one
-// parallel step (the host restatement depthestimation_amd/postprocess.py:_telea_inpaint defines the
-// arithmetic; this file follows it operation for operation, float64 throughout, no contraction):
-//   layer k = hole pixels not yet filled with a 4-neighbour in layer k-1 (known pixels: layer 0);
-//   T(p)   = min over the 4 quadrants of Telea's upwind solve from earlier-layer neighbours' T;
-//   value  = sum w v / sum w over earlier-layer pixels q with 0 < |p-q|^2 <= r^2 (window rows
-//            summed left to right, then the row sums top to bottom),
-//            w = max(|(p-q).gradT| / |p-q| / |p-q|^2 / (1 + |T(q) - T(p)|), 1e-6).
-//
-// The layers are known before the march: a hole pixel's layer is its 4-connected (BFS) distance
-// through holes to the nearest known pixel, and that equals its plain L1 distance to the nearest
-// known pixel (the known pixel q nearest in L1 is joined to p by a monotone lattice path whose inner
-// pixels are all holes, else one of them would be nearer).  So the layers come from a separable L1
-// distance transform (row scans, then column scans), the hole pixels are bucketed by layer with a
-// counting sort, and the march visits list k at step k.  Nothing is read back to the host:
-//   inp_rows     copy, distance to the nearest known pixel of the row (block scans)
-//   inp_cols     column pass of the L1 transform (segment summaries + scans) -> layer map, with the
-//                per-layer counts and the deepest layer K (LDS histograms); its last block to finish
-//                turns the counts into per-layer list offsets
-//   inp_scatter  hole pixels into their layer's list
-//   inp_layer    one launch per layer k = 1..L0, enqueued without waiting; a launch past K exits
-//   inp_rest     layers L0+1..K, if any, in ONE persistent launch with a grid barrier per layer
-// L0 follows the deepest layer of the previous call (written by the device into mapped host memory),
-// so a video stream normally finishes in the per-layer launches and the persistent kernel exits at
-// once.  A layer only reads pixels of earlier layers and writes its own, so the kernel boundary (or
-// the barrier) is the only ordering the march needs.
+// Telea's fast march in cv2.inpaint's own order: by arrival time T.  The heap pops the narrow band
+// by (T, push order); popping p fills each still-INSIDE 4-neighbour q from what is filled so far:
+// T(q) by the upwind solve over its filled 4-neighbours, value(q) = sum w v / sum w over the filled
+// pixels of its radius disc.  A child's T exceeds its parent's by at least sqrt(2)/2, so with
+// T-buckets of width 0.7 the pops of a bucket are exactly the band pixels in it when the bucket starts
+// (host restatement and proof: depthestimation_amd/postprocess.py _telea_inpaint; sequential heap
+// oracle: oracle/telea_heap.py).  Per bucket:
+//   POP      band pixels with T below the bucket bound are popped; each marks its INSIDE 4-neighbours
+//            (atomic CAS on the fill-bucket word: the first one appends the child to the list);
+//   SWEEP 0  each child picks its parent (the pop neighbour with the least pop key (T, T_parent, root
+//            seed, direction, raster)), stores its fill key (the parent's pop key + its direction) and
+//            computes T / value from the pixels filled before the bucket;
+//   SWEEP i  each child recomputes from the pre-bucket pixels and the bucket's children with a
+//            smaller fill key - a DAG, so the fixed point is unique: sweeps repeat until one changes no
+//            bit.  A child recomputes only when a child it reads changed in the previous sweep (the
+//            per-pixel stamp of its last change), so late sweeps touch few pixels.  Updates are in
+//            place (a child may read a neighbour's value of this sweep or the last): the fixed point
+//            is the same, and a sweep without a change proves it.
+// The steps are launches of one kernel, `tl_step`, that reads a small state machine the previous step
+// left in the workspace (triple-buffered by step index: step s reads slot s%3, accumulates into
+// (s+1)%3 and clears (s+2)%3) and does the next POP or sweep; the host enqueues the step count the
+// previous call on this workspace needed (+3, written by the device into mapped host memory) and one
+// persistent cooperative launch, `tl_tail`, runs whatever is left with a grid barrier per step.
+// Arithmetic: float64 throughout, no contraction, window rows summed left to right, row sums top to
+// bottom - the host restatement's order, so the device equals it bit for bit.
 #include "dsx_internal.h"
 
 #include <algorithm>
+#include <cmath>
 #include <cstdlib>
 #include <mutex>
+#include <unordered_map>
 
 namespace dsx {
 
@@ -40,12 +41,41 @@ namespace dsx {
 
 namespace {
 
-constexpr int kFar = 1 << 28;             // "no known pixel" in the distance transform
-constexpr int kUnreached = 0x7FFFFFFF;    // layer of a hole no known pixel reaches
-constexpr int kCtlK = 0, kCtlBar = 1, kCtlTmo = 2, kCtlDone = 3, kCtlGen = 32;  // Gen: own cache line
-constexpr int kCtlWords = 64;
-constexpr int kHistBins = 2048;           // LDS histogram bins of inp_cols / inp_scatter
-constexpr int kChunk = 4096;              // pixels per block of inp_scatter
+constexpr int kInside = 0x7FFFFFFF;  // fill-bucket word of an unfilled hole (known pixels: -1)
+constexpr double kDelta = 0.7;       // T-bucket width (postprocess._TELEA_DELTA)
+constexpr int kStepBlocks = 512;     // grid of the step launches (an empty step costs ~1.5 us at 512)
+constexpr unsigned kMaxSteps = 1u << 24;
+
+enum Phase : int { kPhInit = 0, kPhPop = 1, kPhSweep = 2, kPhDone = 3 };
+
+// One state slot (written by step s-1, read by step s).  Counters and minima are accumulated by the
+// blocks of the writing step; the rest is carried by block 0.
+struct alignas(128) State {
+    int phase, k, b, sweep, lsel, nF, nC, changed;
+    double bound;
+    unsigned long long minF, minC;  // bit patterns of non-negative doubles (monotone as integers)
+};
+struct Ctl {
+    State st[3];
+    unsigned bar, pad0[31];  // grid-barrier arrival counter (own line)
+    unsigned gen, pad1[31];  // barrier generation (own line)
+    int tmo, pad2[31];       // barrier timed out: every block leaves
+};
+
+struct Args {
+    float *out;
+    int *fb;               // fill bucket: -1 known, kInside unfilled, b filled in bucket b
+    double *T, *Tpar, *Tgp;
+    unsigned long long *lowkey;  // root << 34 | dir(parent) << 32 | parent << 2 | dir(self)
+    int *stamp;            // sweep of the pixel's last change
+    int *F[2], *C[2];      // frontier (unpopped band) and children lists, ping-pong
+    Ctl *ctl;
+    int *host;             // mapped host words of this workspace (nullable)
+    int H, W, radius;
+    unsigned spin_limit;
+};
+
+constexpr int kHostSteps = 0, kHostTmo = 16;
 
 __device__ __forceinline__ double telea_solve(double t1, double t2) {
     if (t1 < 1e6 && t2 < 1e6) {
@@ -59,426 +89,450 @@ __device__ __forceinline__ double telea_solve(double t1, double t2) {
     return 1.0 + (t1 < t2 ? t1 : t2);
 }
 
-// ---- L1 distance transform -------------------------------------------------------------------
+__device__ __forceinline__ unsigned long long dbits(double v) { return (unsigned long long)__double_as_longlong(v); }
+__device__ __forceinline__ double bitsd(unsigned long long v) { return __longlong_as_double((long long)v); }
 
-// Block-wide inclusive scan over 256 values into buf[0..255]: MAXOP: prefix max (t' <= t), else
-// suffix min (t' >= t).  Shuffles inside each wave, then the 4 wave totals through LDS.
-template <bool MAXOP>
-__device__ __forceinline__ void block_scan(int v, int *buf) {
-    __shared__ int wtot[4];
-    const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        if constexpr (MAXOP) {
-            const int u = __shfl_up(v, o);
-            v = lane >= o && u > v ? u : v;
-        } else {
-            const int u = __shfl_down(v, o);
-            v = lane + o < 64 && u < v ? u : v;
-        }
-    }
-    if (lane == (MAXOP ? 63 : 0)) wtot[wv] = v;
-    __syncthreads();
-#pragma unroll
-    for (int w = 0; w < 4; ++w) {
-        const int u = wtot[w];
-        if (MAXOP ? w < wv : w > wv) v = MAXOP ? (u > v ? u : v) : (u < v ? u : v);
-    }
-    buf[t] = v;
-    __syncthreads();
+// Fill key of a child of the current bucket: (T_parent, T_grandparent, lowkey).  Lexicographic.
+struct Key {
+    double tp, tg;
+    unsigned long long lo;
+};
+__device__ __forceinline__ bool key_less(const Key &a, const Key &b) {
+    return a.tp < b.tp || (a.tp == b.tp && (a.tg < b.tg || (a.tg == b.tg && a.lo < b.lo)));
+}
+__device__ __forceinline__ Key load_key(const Args &a, int64_t q) { return Key{a.Tpar[q], a.Tgp[q], a.lowkey[q]}; }
+
+// Is pixel q (fill bucket f) filled before child `me` of bucket b?  Pre-bucket pixels always; the
+// bucket's own children when their fill key is smaller (and only after sweep 0 stored the keys).
+__device__ __forceinline__ bool filled_before(const Args &a, int64_t q, int f, int b, bool keys, const Key &me) {
+    if (f < b) return true;
+    if (f != b || !keys) return false;
+    return key_less(load_key(a, q), me);
 }
 
-// One block per row: out = in, g = distance to the nearest known pixel of the row (kFar if none).
-// The row is staged in LDS with coalesced loads, each thread scans a contiguous chunk of it, and two
-// block scans carry the last / first known pixel across chunks.  T is not initialised: it is only
-// read at pixels of earlier layers, i.e. known pixels (T = 0, substituted by layer) or pixels the
-// march has filled.  Block 0..: also zeroes the per-layer counters and the control words.
-__global__ __launch_bounds__(256) void inp_rows(const float *in, int64_t pitch, int H, int W, float *out, int *g,
-                                                int *cnt, int ncnt, int *ctl) {
-    extern __shared__ __attribute__((aligned(16))) uint8_t rsm[];
-    float *sv = reinterpret_cast<float *>(rsm);
-    int *sg = reinterpret_cast<int *>(rsm + (size_t)W * 4);
-    __shared__ int buf[256];
-    const int y = blockIdx.x, t = threadIdx.x;
-    for (int i = y * 256 + t; i < ncnt; i += H * 256) cnt[i] = 0;
-    if (y == 0 && t < kCtlWords) ctl[t] = 0;
-    const float *row = in + (int64_t)y * pitch;
-    float *orow = out + (int64_t)y * W;
-    for (int x = t; x < W; x += 256) {
-        const float v = row[x];
-        sv[x] = v;
-        orow[x] = v;
-    }
-    __syncthreads();
-    const int chunk = (W + 255) / 256;
-    const int x0 = min(W, t * chunk), x1 = min(W, x0 + chunk);
-    int last = -kFar, first = kFar;
-    for (int x = x0; x < x1; ++x) {
-        if (sv[x] > 0.0f) {  // fill_holes' mask = disparity <= 0 (postprocess.py:96-97)
-            first = first == kFar ? x : first;
-            last = x;
-        }
-    }
-    // last known left of this chunk, first known right of it
-    block_scan<true>(last, buf);
-    const int prev_last = t > 0 ? buf[t - 1] : -kFar;
-    __syncthreads();
-    block_scan<false>(first, buf);
-    const int next_first = t < 255 ? buf[t + 1] : kFar;
-    int p = prev_last;
-    for (int x = x0; x < x1; ++x) {
-        if (sv[x] > 0.0f) p = x;
-        sg[x] = p == -kFar ? kFar : x - p;
-    }
-    int q = next_first;
-    for (int x = x1 - 1; x >= x0; --x) {
-        if (sv[x] > 0.0f) q = x;
-        if (q != kFar) sg[x] = min(sg[x], q - x);
-    }
-    __syncthreads();
-    int *grow = g + (int64_t)y * W;
-    for (int x = t; x < W; x += 256) grow[x] = sg[x];
-}
+// ---- setup -----------------------------------------------------------------------------------
 
-// Column pass: layer = min over y' of g(x, y') + |y - y'| (exact L1 distance), 0 on known pixels,
-// kUnreached where no known pixel exists.  Block = 16 columns x 64 row segments; each thread loads
-// its segment of g into registers at once (SLM rows at most; SLM = 0: a row loop for very tall maps),
-// summarises it for both directions, takes the other segments' summaries from LDS, then scans its
-// segment forwards and backwards.  The per-layer counts go through an LDS histogram; the block that
-// finishes last (a done counter, no waiting) turns the counts into list offsets: off[k] = first list
-// slot of layer k (k = 1..K+1), cur[k] = off[k] (the scatter cursors, in place of the counts), and
-// writes the deepest layer K to the host word.
-constexpr int kColW = 16, kColS = 64;
-template <int SLM>
-__global__ __launch_bounds__(1024) void inp_cols(const int *g, int H, int W, int *layer, int *cnt_cur, int *off,
-                                                 int *ctl, int *host_k) {
-    __shared__ int sf[kColS][kColW], sb[kColS][kColW];
-    __shared__ int hist[kHistBins];
-    __shared__ int kmax, last;
-    for (int i = threadIdx.x; i < kHistBins; i += 1024) hist[i] = 0;
-    if (threadIdx.x == 0) kmax = 0;
-    const int cx = threadIdx.x % kColW, sj = threadIdx.x / kColW;
-    const int x = blockIdx.x * kColW + cx;
-    const int SL = (H + kColS - 1) / kColS;  // <= SLM (host) unless SLM == 0
-    const int y0 = min(H, sj * SL), y1 = min(H, y0 + SL);
-    const bool live = x < W;
-    constexpr int NR = SLM > 0 ? SLM : 1;
-    int gv[NR];
-    int cf = kFar, cb = kFar;  // min_y g(y) + (y1 - 1 - y) and min_y g(y) + (y - y0)
-    if constexpr (SLM > 0) {
-#pragma unroll
-        for (int i = 0; i < SLM; ++i) gv[i] = (live && y0 + i < y1) ? g[(int64_t)(y0 + i) * W + x] : kFar;
-#pragma unroll
-        for (int i = 0; i < SLM; ++i) {
-            // rows past the segment must not count: kFar - offset would read as a (huge) layer
-            if (y0 + i < y1) {
-                cf = min(cf, gv[i] + (y1 - 1 - (y0 + i)));
-                cb = min(cb, gv[i] + i);
-            }
-        }
-    } else if (live) {
-        for (int y = y0; y < y1; ++y) {
-            const int v = g[(int64_t)y * W + x];
-            cf = min(cf, v + (y1 - 1 - y));
-            cb = min(cb, v + (y - y0));
-        }
+// out = in; fill-bucket words; the seeds (known pixels with a hole 4-neighbour) into F[0] with their
+// count in slot 0; slots 1 and 2 get empty minima.  The control block was zeroed before (memset).
+__global__ __launch_bounds__(256) void tl_init(const float *in, int64_t pitch, Args a) {
+    const int H = a.H, W = a.W;
+    const int64_t n = (int64_t)H * W;
+    State &s0 = a.ctl->st[0];
+    if (blockIdx.x == 0 && threadIdx.x < 2) {
+        State &s = a.ctl->st[1 + threadIdx.x];
+        s.minF = ~0ull;
+        s.minC = ~0ull;
     }
-    sf[sj][cx] = cf;
-    sb[sj][cx] = cb;
-    __syncthreads();
-    // distance from the segments above (at row y0 - 1) / below (at row y1)
-    int hf = kFar, hb = kFar;
-#pragma unroll 16
-    for (int j = 0; j < kColS; ++j) {
-        const int ys = min(H, j * SL), ye = min(H, (j + 1) * SL);  // segment j: rows ys..ye-1
-        const int vf = sf[j][cx] + (y0 - ye), vb = sb[j][cx] + (ys - y1);
-        hf = j < sj ? min(hf, vf) : hf;
-        hb = (j > sj && ys < H) ? min(hb, vb) : hb;
-    }
-    int km = 0;
-    auto emit = [&](int y, int d) {
-        // a reached hole lies at most H + W - 2 from a known pixel; anything past H + W is a
-        // kFar-derived "no known pixel" (and never indexes the per-layer counts)
-        const bool reached = d <= H + W;
-        layer[(int64_t)y * W + x] = reached ? d : kUnreached;  // known pixels: g = 0
-        if (d > 0 && reached) {
-            km = d > km ? d : km;
-            if (d < kHistBins) atomicAdd(&hist[d], 1);
-            else atomicAdd(&cnt_cur[d], 1);
-        }
-    };
-    if constexpr (SLM > 0) {
-        int fw[SLM];
-#pragma unroll
-        for (int i = 0; i < SLM; ++i) {
-            hf = min(gv[i], hf + 1);
-            fw[i] = hf;
-        }
-#pragma unroll
-        for (int i = SLM - 1; i >= 0; --i) {
-            if (live && y0 + i < y1) {
-                hb = min(gv[i], hb + 1);
-                emit(y0 + i, min(fw[i], hb));
-            }
-        }
-    } else if (live) {
-        for (int y = y0; y < y1; ++y) {
-            hf = min(g[(int64_t)y * W + x], hf + 1);
-            layer[(int64_t)y * W + x] = hf;
-        }
-        for (int y = y1 - 1; y >= y0; --y) {
-            const int64_t o = (int64_t)y * W + x;
-            hb = min(g[o], hb + 1);
-            emit(y, min(layer[o], hb));
-        }
-    }
-    atomicMax(&kmax, km);
-    __syncthreads();
-    const int kb = min(kmax + 1, kHistBins);
-    for (int i = threadIdx.x; i < kb; i += 1024)
-        if (hist[i]) atomicAdd(&cnt_cur[i], hist[i]);
-    if (threadIdx.x == 0 && kmax) atomicMax(&ctl[kCtlK], kmax);
-
-    // ---- the last block to finish: per-layer list offsets ----
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        const unsigned done = __hip_atomic_fetch_add(reinterpret_cast<unsigned *>(ctl + kCtlDone), 1u,
-                                                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        last = done == gridDim.x - 1;
-        if (last) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    }
-    __syncthreads();
-    if (!last) return;  // block-uniform
-    int *part = &sf[0][0];  // 1024 ints of LDS, free now
-    const int K = __hip_atomic_load(&ctl[kCtlK], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const int t = threadIdx.x;
-    const int chunk = (K + 1024) / 1024;  // layers 1..K
-    const int k0 = 1 + t * chunk, k1 = min(K + 1, k0 + chunk);
-    int sum = 0;
-    for (int k = k0; k < k1; ++k) sum += __hip_atomic_load(&cnt_cur[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    part[t] = sum;
-    __syncthreads();
-    for (int o = 1; o < 1024; o <<= 1) {
-        const int v = t >= o ? part[t - o] : 0;
-        __syncthreads();
-        part[t] += v;
-        __syncthreads();
-    }
-    int base = t > 0 ? part[t - 1] : 0;
-    for (int k = k0; k < k1; ++k) {
-        const int c = __hip_atomic_load(&cnt_cur[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        off[k] = base;
-        cnt_cur[k] = base;
-        base += c;
-    }
-    if (t == 1023) off[K + 1] = part[1023];
-    if (t == 0 && host_k) __hip_atomic_store(host_k, K, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-}
-
-// Hole pixels into their layer's list (order inside a layer is free: its pixels are independent).
-__global__ __launch_bounds__(256) void inp_scatter(const int *layer, int n, int *cur, int *list, const int *ctl) {
-    __shared__ int h[kHistBins], base[kHistBins];
-    constexpr int PER = kChunk / 256;
-    const int nb = min(ctl[kCtlK] + 1, kHistBins);  // bins 0..K
-    for (int i = threadIdx.x; i < nb; i += 256) h[i] = 0;
-    __syncthreads();
-    const int p0 = blockIdx.x * kChunk;
-    int rank[PER];
-#pragma unroll
-    for (int j = 0; j < PER; ++j) {
-        const int p = p0 + j * 256 + (int)threadIdx.x;
-        rank[j] = -1;
+    for (int64_t p0 = (int64_t)blockIdx.x * 256; p0 < n; p0 += (int64_t)gridDim.x * 256) {  // block-uniform
+        const int64_t p = p0 + threadIdx.x;
+        bool seed = false;
         if (p < n) {
-            const int k = layer[p];
-            if (k > 0 && k != kUnreached) {
-                if (k < kHistBins) rank[j] = atomicAdd(&h[k], 1);
-                else list[atomicAdd(&cur[k], 1)] = p;
+            const int y = (int)(p / W), x = (int)(p - (int64_t)y * W);
+            const float *row = in + (int64_t)y * pitch;
+            const float v = row[x];
+            a.out[p] = v;
+            const bool known = !(v <= 0.0f);  // fill_holes' mask = disparity <= 0 (postprocess.py:96-97)
+            a.fb[p] = known ? -1 : kInside;
+            if (known) {
+                const bool hu = y > 0 && row[x - pitch] <= 0.0f, hd = y < H - 1 && row[x + pitch] <= 0.0f;
+                const bool hl = x > 0 && row[x - 1] <= 0.0f, hr = x < W - 1 && row[x + 1] <= 0.0f;
+                seed = hu || hd || hl || hr;
             }
         }
-    }
-    __syncthreads();
-    for (int i = threadIdx.x; i < nb; i += 256)
-        if (h[i]) base[i] = atomicAdd(&cur[i], h[i]);
-    __syncthreads();
-#pragma unroll
-    for (int j = 0; j < PER; ++j) {
-        const int p = p0 + j * 256 + (int)threadIdx.x;
-        if (rank[j] >= 0) list[base[layer[p]] + rank[j]] = p;
+        // wave-aggregated append
+        const unsigned long long m = __ballot(seed);
+        if (m) {
+            const int lane = threadIdx.x & 63;
+            int base = 0;
+            if (lane == __builtin_ctzll(m)) base = atomicAdd(&s0.nF, __popcll(m));
+            base = __shfl(base, __builtin_ctzll(m));
+            if (seed) a.F[0][base + __popcll(m & ((1ull << lane) - 1))] = (int)p;
+        }
     }
 }
 
-// ---- the march ------------------------------------------------------------------------------
+// ---- one step ----------------------------------------------------------------------------------
 
-struct Front {
-    double tp, gx, gy;
+struct Mode {
+    int what;  // kPhPop, kPhSweep, kPhDone
+    int k, b, sweep, lsel, nIn, nPrev;
+    double bound;
 };
 
-// T and grad T of a pixel p of layer k from its earlier-layer 4-neighbours (T 1e6 when absent).
-// The 8 loads are unconditional (clamped to p at the border, then discarded) so they issue together.
-__device__ __forceinline__ Front front_of(const int *layer, const double *T, int p, int y, int x, int H, int W, int k) {
-    Front f;
-    const bool iu = y > 0, id = y < H - 1, il = x > 0, ir = x < W - 1;
-    const int pu = iu ? p - W : p, pd = id ? p + W : p, pl = il ? p - 1 : p, pr = ir ? p + 1 : p;
-    const int lu0 = layer[pu], ld0 = layer[pd], ll0 = layer[pl], lr0 = layer[pr];
-    const double Tu = T[pu], Td = T[pd], Tl = T[pl], Tr = T[pr];
-    const int lu = iu ? lu0 : kUnreached, ld = id ? ld0 : kUnreached;
-    const int ll = il ? ll0 : kUnreached, lr = ir ? lr0 : kUnreached;
-    const bool ou = lu < k, od = ld < k, ol = ll < k, orr = lr < k;
-    // T is never initialised: known pixels (layer 0) have T = 0, holes of earlier layers their march value
-    const double tu = ou ? (lu == 0 ? 0.0 : Tu) : 1e6, td = od ? (ld == 0 ? 0.0 : Td) : 1e6;
-    const double tl = ol ? (ll == 0 ? 0.0 : Tl) : 1e6, tr = orr ? (lr == 0 ? 0.0 : Tr) : 1e6;
-    const double a0 = telea_solve(tu, tl), a1 = telea_solve(td, tl);
-    const double a2 = telea_solve(tu, tr), a3 = telea_solve(td, tr);
-    const double m01 = a0 < a1 ? a0 : a1, m23 = a2 < a3 ? a2 : a3;
-    f.tp = m01 < m23 ? m01 : m23;
-    f.gx = (orr && ol) ? (tr - tl) * 0.5 : (orr ? tr - f.tp : (ol ? f.tp - tl : 0.0));
-    f.gy = (od && ou) ? (td - tu) * 0.5 : (od ? td - f.tp : (ou ? f.tp - tu : 0.0));
-    return f;
+// The step's mode from the slot the previous step wrote (every block computes the same).
+__device__ __forceinline__ Mode decide(const State &S) {
+    Mode m{};
+    m.k = S.k;
+    m.b = S.b;
+    m.lsel = S.lsel;
+    m.bound = S.bound;
+    if (S.phase == kPhDone) {
+        m.what = kPhDone;
+        return m;
+    }
+    if (S.phase == kPhSweep && (S.sweep == 0 || S.changed > 0)) {
+        m.what = kPhSweep;
+        m.sweep = S.sweep + 1;
+        m.nIn = S.nC;
+        return m;
+    }
+    if (S.phase == kPhPop && S.nC > 0) {
+        m.what = kPhSweep;
+        m.sweep = 0;
+        m.nIn = S.nC;
+        return m;
+    }
+    // a POP: over the survivors F[lsel] and the last bucket's children C[lsel] (none after a POP
+    // without children or at the start)
+    const bool after_sweep = S.phase == kPhSweep;
+    m.nIn = S.nF;
+    m.nPrev = after_sweep ? S.nC : 0;
+    if (m.nIn + m.nPrev == 0) {
+        m.what = kPhDone;
+        return m;
+    }
+    unsigned long long mn = S.minF;
+    if (after_sweep && S.minC < mn) mn = S.minC;
+    const int kf = (int)floor(bitsd(mn) / kDelta);
+    const int kn = S.k > kf ? S.k : kf;
+    m.what = kPhPop;
+    m.bound = (double)(kn + 1) * kDelta;
+    m.k = kn + 1;
+    m.b = kn + 1;
+    return m;
 }
 
-// Telea's weight of the window cell (oy, ox) with layer lq, stored T Tq and value vq (known pixels,
-// layer 0, have T = 0, not stored).
-__device__ __forceinline__ void cell_weight(int oy, int ox, int lq, double Tq, float vq, const Front &f, double &w,
-                                            double &wv) {
-    const int d2 = oy * oy + ox * ox;
-    const double tq = lq == 0 ? 0.0 : Tq;
-    const double ry = (double)(-oy), rx = (double)(-ox);
-    const double w_dir = __builtin_fabs(ry * f.gy + rx * f.gx) / __builtin_sqrt((double)d2);
-    const double w_dst = 1.0 / (double)d2;
-    const double w_lev = 1.0 / (1.0 + __builtin_fabs(tq - f.tp));
-    w = w_dir * w_dst * w_lev;
-    w = w > 1e-6 ? w : 1e-6;
-    wv = w * (double)vq;
+__device__ __forceinline__ void wave_append(bool take, int *list, int *count, int item) {
+    const unsigned long long m = __ballot(take);
+    if (!m) return;
+    const int lane = threadIdx.x & 63;
+    const int lead = __builtin_ctzll(m);
+    int base = 0;
+    if (lane == lead) base = atomicAdd(count, __popcll(m));
+    base = __shfl(base, lead);
+    if (take) list[base + __popcll(m & ((1ull << lane) - 1))] = item;
 }
 
-// Weight of the window cell (oy, ox) for the pixel (y, x); false when the cell is outside the disc,
-// the image or the earlier layers.
-__device__ __forceinline__ bool cell_term(const float *out, const int *layer, const double *T, int y, int x, int oy,
-                                          int ox, int H, int W, int r2, int k, const Front &f, double &w, double &wv) {
-    const int d2 = oy * oy + ox * ox;
-    const int qy = y + oy, qx = x + ox;
-    if (d2 == 0 || d2 > r2 || qy < 0 || qy >= H || qx < 0 || qx >= W) return false;
-    const int64_t q = (int64_t)qy * W + qx;
-    const int lq = layer[q];
-    const double Tq = T[q];
-    const float vq = out[q];
-    if (lq >= k) return false;
-    cell_weight(oy, ox, lq, Tq, vq, f, w, wv);
-    return true;
+__device__ __forceinline__ unsigned long long wave_min_u64(unsigned long long v) {
+    for (int o = 32; o > 0; o >>= 1) {
+        const unsigned long long u = __shfl_xor(v, o);
+        v = u < v ? u : v;
+    }
+    return v;
 }
 
-// Layer k's pixels list[beg..end), one pixel per group of G lanes (G = 8 for radius <= 3, 16 for
-// radius <= 7): lane j of the group sums window row j - radius, cell by cell from 0.0 (the divisions,
-// square roots and neighbour loads of the rows in parallel), then the row sums are added top to
-// bottom through shuffles - the order of the host restatement, so the result keeps its bits.
-template <int G>
-__device__ __forceinline__ void march_layer_grp(float *out, const int *layer, double *T, int H, int W, int radius,
-                                                int k, const int *list, int beg, int end, int g0, int gstride) {
-    constexpr int RM = (G - 2) / 2;  // widest radius of the group form: 3 (G 8), 7 (G 16)
-    constexpr int NCELL = 2 * RM + 1;
-    const int j = threadIdx.x & (G - 1);
-    const int r2 = radius * radius;
-    for (int i = beg + g0; i < end; i += gstride) {  // group-uniform
-        const int p = list[i];
-        const int y = p / W, x = p - y * W;
-        const Front f = front_of(layer, T, p, y, x, H, W, k);
-        double rn = 0.0, rd = 0.0;
-        if (j <= 2 * radius) {
-            // the whole window row loads at once (clamped addresses, unused cells discarded), then
-            // the cells are summed left to right, skipping the ones outside the disc / image / layers
-            const int oy = j - radius;
-            const int qy = y + oy;
-            const bool rowin = qy >= 0 && qy < H;
-            const int64_t rowq = (int64_t)(rowin ? qy : y) * W;
-            int lq[NCELL];
-            double tq[NCELL];
-            float vq[NCELL];
+// POP: entries of F[lsel] (nIn) then C[lsel] (nPrev); T < bound pops (marks children), the rest
+// survives into F[lsel^1].  T of a known seed is 0.
+__device__ void do_pop(const Args &a, const Mode &m, State &N, int blk, int nblk) {
+    const int *Fi = a.F[m.lsel], *Ci = a.C[m.lsel];
+    int *Fo = a.F[m.lsel ^ 1], *Co = a.C[m.lsel ^ 1];
+    const int tot = m.nIn + m.nPrev;
+    const int W = a.W, H = a.H;
+    unsigned long long mn = ~0ull;
+    for (int base = blk * 256; base < tot; base += nblk * 256) {  // block-uniform trip count
+        const int i = base + (int)threadIdx.x;
+        bool keep = false;
+        int p = 0;
+        bool marks[4] = {false, false, false, false};
+        int kids[4] = {0, 0, 0, 0};
+        if (i < tot) {
+            p = i < m.nIn ? Fi[i] : Ci[i - m.nIn];
+            const double t = a.fb[p] < 0 ? 0.0 : a.T[p];
+            if (t < m.bound) {
+                const int y = p / W, x = p - y * W;
+                const int nb[4] = {y > 0 ? p - W : -1, x > 0 ? p - 1 : -1, y < H - 1 ? p + W : -1, x < W - 1 ? p + 1 : -1};
 #pragma unroll
-            for (int c = 0; c < NCELL; ++c) {
-                const int qx = x + c - RM;
-                const int64_t q = rowq + (qx < 0 ? 0 : (qx >= W ? W - 1 : qx));
-                lq[c] = layer[q];
-                tq[c] = T[q];
-                vq[c] = out[q];
-            }
-#pragma unroll
-            for (int c = 0; c < NCELL; ++c) {
-                const int ox = c - RM;
-                const int qx = x + ox;
-                const int d2 = oy * oy + ox * ox;
-                const bool use = rowin && qx >= 0 && qx < W && d2 > 0 && d2 <= r2 && lq[c] < k;
-                double w, wv;
-                cell_weight(oy, ox, lq[c], tq[c], vq[c], f, w, wv);
-                rn = use ? rn + wv : rn;
-                rd = use ? rd + w : rd;
+                for (int d = 0; d < 4; ++d) {
+                    if (nb[d] >= 0 && a.fb[nb[d]] == kInside) {
+                        marks[d] = atomicCAS(&a.fb[nb[d]], kInside, m.b) == kInside;
+                        kids[d] = nb[d];
+                    }
+                }
+            } else {
+                keep = true;
+                mn = dbits(t);
             }
         }
-        double num = 0.0, den = 0.0;
+        wave_append(keep, Fo, &N.nF, p);
+#pragma unroll
+        for (int d = 0; d < 4; ++d) wave_append(marks[d], Co, &N.nC, kids[d]);
+    }
+    mn = wave_min_u64(mn);
+    if ((threadIdx.x & 63) == 0 && mn != ~0ull) atomicMin(&N.minF, mn);
+}
+
+// Pop key of a band pixel p (known seed or filled): (T, T_parent, root << 32 | dir << 30 | p).
+struct PopKey {
+    double t, tp;
+    unsigned long long lo;
+};
+__device__ __forceinline__ bool pop_less(const PopKey &a, const PopKey &b) {
+    return a.t < b.t || (a.t == b.t && (a.tp < b.tp || (a.tp == b.tp && a.lo < b.lo)));
+}
+
+// One child (group of G lanes, lane j = window row j - radius; G = 0: one thread does every row).
+// Returns (via lane 0 / the thread) whether T or the value changed, and the child's T.
+template <int G>
+__device__ __forceinline__ void sweep_child(const Args &a, const Mode &m, int c, bool &changed, double &tc) {
+    constexpr int RM = G > 0 ? (G - 2) / 2 : 0;  // widest radius of the group form: 3 (G 8), 7 (G 16)
+    const int j = G > 0 ? (int)(threadIdx.x & (G - 1)) : 0;
+    const int H = a.H, W = a.W, radius = a.radius, r2 = radius * radius;
+    const int y = c / W, x = c - y * W;
+    const int b = m.b;
+    const bool first = m.sweep == 0;
+    const int nbp[4] = {y > 0 ? c - W : -1, x > 0 ? c - 1 : -1, y < H - 1 ? c + W : -1, x < W - 1 ? c + 1 : -1};
+    Key me;
+    if (first) {
+        // the parent: the pop neighbour with the least pop key (any band neighbour below the bound is
+        // a pop of this bucket: one popped earlier would have filled c then)
+        PopKey best{0, 0, 0};
+        int bp = -1, bd = 0;
+#pragma unroll
+        for (int d = 0; d < 4; ++d) {
+            const int p = nbp[d];
+            if (p < 0) continue;
+            const int f = a.fb[p];
+            if (f >= b) continue;
+            PopKey k;
+            int pdir;
+            unsigned long long proot;
+            if (f < 0) {
+                k.t = 0.0;
+                k.tp = -1.0;
+                proot = (unsigned long long)p;
+                pdir = 0;
+            } else {
+                k.t = a.T[p];
+                k.tp = a.Tpar[p];
+                const unsigned long long lk = a.lowkey[p];
+                proot = lk >> 34;
+                pdir = (int)(lk & 3);
+            }
+            if (!(k.t < m.bound)) continue;
+            k.lo = proot << 32 | (unsigned long long)pdir << 30 | (unsigned long long)p;
+            if (bp < 0 || pop_less(k, best)) {
+                best = k;
+                bp = p;
+                bd = d;
+            }
+        }
+        // direction from the parent to the child (up, left, down, right): parent above -> down, ...
+        const int dirc = bd ^ 2;
+        me.tp = best.t;
+        me.tg = best.tp;
+        const unsigned long long root = best.lo >> 32, pdir = (best.lo >> 30) & 3;
+        me.lo = root << 34 | pdir << 32 | (unsigned long long)bp << 2 | (unsigned long long)dirc;
+        if (j == 0) {
+            a.Tpar[c] = me.tp;
+            a.Tgp[c] = me.tg;
+            a.lowkey[c] = me.lo;
+        }
+    } else {
+        me = load_key(a, c);
+    }
+
+    // ---- does anything this child reads change? (sweeps >= 1; a child of no intra-bucket pixel is
+    // settled after sweep 0) ----
+    const double Told = a.T[c];
+    const float vold = a.out[c];
+    tc = Told;
+    changed = false;
+
+    // ---- T and grad T from the 4-neighbours filled before this child ----
+    double tn[4];
+    bool on[4];
+    bool need = first;
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+        const int p = nbp[d];
+        on[d] = false;
+        tn[d] = 1e6;
+        if (p < 0) continue;
+        const int f = a.fb[p];
+        if (filled_before(a, p, f, b, !first, me)) {
+            on[d] = true;
+            tn[d] = f < 0 ? 0.0 : a.T[p];
+            if (f == b && a.stamp[p] >= m.sweep - 1) need = true;
+        }
+    }
+
+    // ---- the disc rows ----
+    constexpr int NCELL = 2 * RM + 1;
+    const int row0 = G > 0 ? j - radius : -radius, row1 = G > 0 ? j - radius : radius;
+    // group form: one row per lane, its cells in registers; G = 0: rows looped below
+    int fq[G > 0 ? NCELL : 1];
+    if constexpr (G > 0) {
+        const int oy = row0;
+        const int qy = y + oy;
+        const bool rowin = j <= 2 * radius && qy >= 0 && qy < H;
+#pragma unroll
+        for (int cc = 0; cc < NCELL; ++cc) {
+            const int ox = cc - RM, qx = x + ox;
+            const int d2 = oy * oy + ox * ox;
+            fq[cc] = kInside;
+            if (rowin && qx >= 0 && qx < W && d2 > 0 && d2 <= r2) {
+                const int64_t q = (int64_t)qy * W + qx;
+                const int f = a.fb[q];
+                if (filled_before(a, q, f, b, !first, me)) {
+                    fq[cc] = f;
+                    if (f == b && a.stamp[q] >= m.sweep - 1) need = true;
+                }
+            }
+        }
+    } else {
+        for (int oy = -radius; oy <= radius && !need; ++oy)
+            for (int ox = -radius; ox <= radius; ++ox) {
+                const int qy = y + oy, qx = x + ox, d2 = oy * oy + ox * ox;
+                if (d2 == 0 || d2 > r2 || qy < 0 || qy >= H || qx < 0 || qx >= W) continue;
+                const int64_t q = (int64_t)qy * W + qx;
+                const int f = a.fb[q];
+                if (f == b && filled_before(a, q, f, b, !first, me) && a.stamp[q] >= m.sweep - 1) need = true;
+            }
+    }
+    if constexpr (G > 0) {
+        // group-uniform decision
+#pragma unroll
+        for (int o = 1; o < G; o <<= 1) {
+            const int other = __shfl_xor((int)need, o, G);  // every lane must take part: no short circuit
+            need = need || other != 0;
+        }
+    }
+    if (!need) return;
+
+    const double ta = telea_solve(tn[0], tn[1]), tb = telea_solve(tn[2], tn[1]);
+    const double tc2 = telea_solve(tn[0], tn[3]), td = telea_solve(tn[2], tn[3]);
+    const double m01 = ta < tb ? ta : tb, m23 = tc2 < td ? tc2 : td;
+    const double tp = m01 < m23 ? m01 : m23;
+    const bool ou = on[0], ol = on[1], od = on[2], orr = on[3];
+    const double tu = tn[0], tl = tn[1], tdn = tn[2], tr = tn[3];
+    const double gx = (orr && ol) ? (tr - tl) * 0.5 : (orr ? tr - tp : (ol ? tp - tl : 0.0));
+    const double gy = (od && ou) ? (tdn - tu) * 0.5 : (od ? tdn - tp : (ou ? tp - tu : 0.0));
+
+    auto weight = [&](int oy, int ox, double Tq) {
+        const int d2 = oy * oy + ox * ox;
+        const double ry = (double)(-oy), rx = (double)(-ox);
+        const double w_dir = __builtin_fabs(ry * gy + rx * gx) / __builtin_sqrt((double)d2);
+        const double w_dst = 1.0 / (double)d2;
+        const double w_lev = 1.0 / (1.0 + __builtin_fabs(Tq - tp));
+        double w = w_dir * w_dst * w_lev;
+        return w > 1e-6 ? w : 1e-6;
+    };
+    double num = 0.0, den = 0.0;
+    if constexpr (G > 0) {
+        double rn = 0.0, rd = 0.0;
+        const int oy = row0;
+        const int64_t rowq = (int64_t)(y + oy) * W;
+#pragma unroll
+        for (int cc = 0; cc < NCELL; ++cc) {
+            if (fq[cc] == kInside) continue;
+            const int64_t q = rowq + x + cc - RM;
+            const double Tq = fq[cc] < 0 ? 0.0 : a.T[q];
+            const double w = weight(oy, cc - RM, Tq);
+            rn = rn + w * (double)a.out[q];
+            rd = rd + w;
+        }
+        (void)row1;
 #pragma unroll
         for (int q = 0; q < G; ++q) {  // rows past 2 radius add +0.0: exact
             num = num + __shfl(rn, q, G);
             den = den + __shfl(rd, q, G);
         }
-        if (j == 0) {
-            if (den > 0) out[p] = (float)(num / den);
-            T[p] = f.tp;
-        }
-    }
-}
-
-// Larger windows: one pixel per thread, the same row-by-row order.
-__device__ __forceinline__ void march_layer_px(float *out, const int *layer, double *T, int H, int W, int radius, int k,
-                                               const int *list, int beg, int end, int t0, int tstride) {
-    const int r2 = radius * radius;
-    for (int i = beg + t0; i < end; i += tstride) {
-        const int p = list[i];
-        const int y = p / W, x = p - y * W;
-        const Front f = front_of(layer, T, p, y, x, H, W, k);
-        double num = 0.0, den = 0.0;
+    } else {
         for (int oy = -radius; oy <= radius; ++oy) {
             double rn = 0.0, rd = 0.0;
             for (int ox = -radius; ox <= radius; ++ox) {
-                double w, wv;
-                if (cell_term(out, layer, T, y, x, oy, ox, H, W, r2, k, f, w, wv)) {
-                    rn = rn + wv;
-                    rd = rd + w;
-                }
+                const int qy = y + oy, qx = x + ox, d2 = oy * oy + ox * ox;
+                if (d2 == 0 || d2 > r2 || qy < 0 || qy >= H || qx < 0 || qx >= W) continue;
+                const int64_t q = (int64_t)qy * W + qx;
+                const int f = a.fb[q];
+                if (!filled_before(a, q, f, b, !first, me)) continue;
+                const double w = weight(oy, ox, f < 0 ? 0.0 : a.T[q]);
+                rn = rn + w * (double)a.out[q];
+                rd = rd + w;
             }
             num = num + rn;
             den = den + rd;
         }
-        if (den > 0) out[p] = (float)(num / den);
-        T[p] = f.tp;
+    }
+    const float v = den > 0 ? (float)(num / den) : vold;
+    tc = tp;
+    changed = first || __double_as_longlong(tp) != __double_as_longlong(Told) || __float_as_int(v) != __float_as_int(vold);
+    if (changed && j == 0) {
+        a.T[c] = tp;
+        a.out[c] = v;
+        a.stamp[c] = m.sweep;
     }
 }
 
-// G > 0: groups of G lanes per pixel; G = 0: one pixel per thread.
 template <int G>
-__device__ __forceinline__ void march_layer(float *out, const int *layer, double *T, int H, int W, int radius, int k,
-                                            const int *list, int beg, int end, int blk, int nblk) {
-    if constexpr (G > 0)
-        march_layer_grp<G>(out, layer, T, H, W, radius, k, list, beg, end, blk * (256 / G) + (int)(threadIdx.x / G),
-                           nblk * (256 / G));
-    else
-        march_layer_px(out, layer, T, H, W, radius, k, list, beg, end, blk * 256 + (int)threadIdx.x, nblk * 256);
+__device__ void do_sweep(const Args &a, const Mode &m, State &N, int blk, int nblk) {
+    const int *Cl = a.C[m.lsel];
+    constexpr int per = G > 0 ? 256 / G : 256;
+    const int g = G > 0 ? (int)threadIdx.x / G : (int)threadIdx.x;
+    bool any = false;
+    unsigned long long mn = ~0ull;
+    for (int base = blk * per; base < m.nIn; base += nblk * per) {  // group-uniform
+        const int i = base + g;
+        if (i >= m.nIn) continue;
+        bool ch;
+        double t;
+        sweep_child<G>(a, m, Cl[i], ch, t);
+        any = any || ch;
+        const unsigned long long tb = dbits(t);
+        mn = tb < mn ? tb : mn;
+    }
+    if (__syncthreads_or(any) && threadIdx.x == 0) atomicAdd(&N.changed, 1);
+    mn = wave_min_u64(mn);
+    if ((threadIdx.x & 63) == 0 && mn != ~0ull) atomicMin(&N.minC, mn);
 }
 
-// Step k of the march (a launch past the deepest layer does nothing).
+// Step s: returns the mode it ran (kPhDone: the march had finished).
 template <int G>
-__global__ __launch_bounds__(256) void inp_layer(float *out, const int *layer, double *T, int H, int W, int radius,
-                                                 int k, const int *list, const int *off, const int *ctl) {
-    const int K = ctl[kCtlK], beg = off[k], end = off[k + 1];  // independent loads, one round trip
-    if (k > K) return;
-    march_layer<G>(out, layer, T, H, W, radius, k, list, beg, end, blockIdx.x, gridDim.x);
+__device__ int step(const Args &a, unsigned s, int blk, int nblk) {
+    Ctl *ctl = a.ctl;
+    const State S = ctl->st[s % 3];
+    State &N = ctl->st[(s + 1) % 3];
+    const Mode m = decide(S);
+    if (blk == 0 && threadIdx.x == 0) {
+        State &Z = ctl->st[(s + 2) % 3];
+        Z.nF = 0;
+        Z.nC = 0;
+        Z.changed = 0;
+        Z.minF = ~0ull;
+        Z.minC = ~0ull;
+        N.phase = m.what;
+        N.k = m.k;
+        N.b = m.b;
+        N.sweep = m.sweep;
+        N.bound = m.bound;
+        if (m.what == kPhSweep) {  // carried: the POP's outputs
+            N.lsel = m.lsel;
+            N.nF = S.nF;
+            N.nC = S.nC;
+            N.minF = S.minF;
+        } else if (m.what == kPhPop) {
+            N.lsel = m.lsel ^ 1;
+        } else {
+            N.lsel = m.lsel;
+            if (S.phase != kPhDone && a.host)
+                __hip_atomic_store(a.host + kHostSteps, (int)s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+    }
+    if (m.what == kPhPop) do_pop(a, m, N, blk, nblk);
+    else if (m.what == kPhSweep) do_sweep<G>(a, m, N, blk, nblk);
+    return m.what;
+}
+
+template <int G>
+__global__ __launch_bounds__(256) void tl_step(Args a, unsigned s) {
+    step<G>(a, s, blockIdx.x, gridDim.x);
 }
 
 // Grid barrier: every wave drains its stores, lane 0 of the block releases them to the device
 // (agent scope) and arrives on a monotonic counter; the block that arrives last publishes the epoch
-// in a generation word on its own cache line, which the others poll (relaxed, with s_sleep) - so the
-// pollers never contend with the arrivals.  Then an acquire (invalidates this CU's caches) before any
-// wave reads pixels other blocks wrote.  Spins are bounded: on a timeout the block sets the timeout
-// word and every block leaves the march.
+// in a generation word on its own cache line, which the others poll (relaxed, with s_sleep).  Then an
+// acquire before any wave reads what other blocks wrote.  Spins are bounded: on a timeout the block
+// sets the timeout word and every block leaves.
 __device__ __forceinline__ bool grid_barrier(unsigned *ctr, unsigned *gen, unsigned epoch, unsigned nblk, int *tmo,
                                              unsigned spin_limit) {
     __shared__ int ok;
@@ -511,25 +565,23 @@ __device__ __forceinline__ bool grid_barrier(unsigned *ctr, unsigned *gen, unsig
     return ok;
 }
 
-// Layers k0..K in one persistent launch (a cooperative launch of one block per CU: the runtime
-// refuses it unless every block is co-resident), a grid barrier between layers.  Exits at once
-// when the per-layer launches already reached K.  A barrier that times out (spin_limit) leaves the
-// remaining layers unfilled; the block that saw it raises the sticky flag in mapped host memory
-// (htmo), which the next hole-filling call and dsx_fill_holes_status() report as an error.
+// The steps from s0 on, in ONE persistent launch (cooperative: the runtime refuses it unless every
+// block is co-resident), a grid barrier per step.  Exits at once when the step launches finished the
+// march.  A barrier timeout (or the step cap) leaves holes unfilled and raises the workspace's sticky
+// flag in mapped host memory, which the next hole-filling call on it and the status queries report.
 template <int G>
-__global__ __launch_bounds__(256) void inp_rest(float *out, const int *layer, double *T, int H, int W, int radius,
-                                                int k0, const int *list, const int *off, int *ctl, int *htmo,
-                                                unsigned spin_limit) {
-    const int K = ctl[kCtlK];
-    if (k0 > K) return;  // grid-uniform
+__global__ __launch_bounds__(256) void tl_tail(Args a, unsigned s0) {
     unsigned epoch = 0;
-    for (int k = k0; k <= K; ++k) {
-        march_layer<G>(out, layer, T, H, W, radius, k, list, off[k], off[k + 1], blockIdx.x, gridDim.x);
-        if (k == K) break;
+    for (unsigned s = s0;; ++s) {
+        if (s - s0 > kMaxSteps) {
+            if (blockIdx.x == 0 && threadIdx.x == 0 && a.host)
+                __hip_atomic_store(a.host + kHostTmo, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            return;
+        }
+        if (step<G>(a, s, blockIdx.x, gridDim.x) == kPhDone) return;  // grid-uniform
         ++epoch;
-        if (!grid_barrier(reinterpret_cast<unsigned *>(ctl + kCtlBar), reinterpret_cast<unsigned *>(ctl + kCtlGen), epoch,
-                          gridDim.x, ctl + kCtlTmo, spin_limit)) {
-            if (threadIdx.x == 0 && htmo) __hip_atomic_store(htmo, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        if (!grid_barrier(&a.ctl->bar, &a.ctl->gen, epoch, gridDim.x, &a.ctl->tmo, a.spin_limit)) {
+            if (threadIdx.x == 0 && a.host) __hip_atomic_store(a.host + kHostTmo, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             return;
         }
     }
@@ -546,47 +598,53 @@ hipError_t dbg_sync(const char *what, hipStream_t st) {
     return e;
 }
 
-struct Views {
-    int *layer, *g, *list, *cnt, *off, *ctl;
-    double *T;
-    int ncnt;
-};
-
-Views views(void *ws, int H, int W) {
+Args views(void *ws, int H, int W) {
     const size_t n = (size_t)H * W;
-    const int ncnt = H + W + 3;  // layers 0..H+W (+1 end slot)
     uint8_t *w = static_cast<uint8_t *>(ws);
-    Views v;
-    v.ncnt = ncnt;
-    v.layer = reinterpret_cast<int *>(w);
+    Args a{};
+    a.ctl = reinterpret_cast<Ctl *>(w);
+    w += align256(sizeof(Ctl));
+    a.fb = reinterpret_cast<int *>(w);
     w += align256(n * 4);
-    v.T = reinterpret_cast<double *>(w);
+    a.T = reinterpret_cast<double *>(w);
     w += align256(n * 8);
-    v.g = reinterpret_cast<int *>(w);
+    a.Tpar = reinterpret_cast<double *>(w);
+    w += align256(n * 8);
+    a.Tgp = reinterpret_cast<double *>(w);
+    w += align256(n * 8);
+    a.lowkey = reinterpret_cast<unsigned long long *>(w);
+    w += align256(n * 8);
+    a.stamp = reinterpret_cast<int *>(w);
     w += align256(n * 4);
-    v.list = reinterpret_cast<int *>(w);
-    w += align256(n * 4);
-    v.cnt = reinterpret_cast<int *>(w);
-    w += align256((size_t)ncnt * 4);
-    v.off = reinterpret_cast<int *>(w);
-    w += align256((size_t)ncnt * 4);
-    v.ctl = reinterpret_cast<int *>(w);
-    return v;
+    for (int i = 0; i < 2; ++i) {
+        a.F[i] = reinterpret_cast<int *>(w);
+        w += align256(n * 4);
+        a.C[i] = reinterpret_cast<int *>(w);
+        w += align256(n * 4);
+    }
+    a.H = H;
+    a.W = W;
+    return a;
 }
 
-// Mapped host words shared by every device / stream: [0] the deepest layer of the previous call
-// (written by the device; it only sizes the next call's run of per-layer launches), [16] the sticky
-// grid-barrier timeout flag of inp_rest (own cache line).
-constexpr int kHostLastK = 0, kHostTmo = 16;
-int *host_words() {
-    static int *p = [] {
-        int *h = nullptr;
-        if (hipHostMalloc(&h, 128, hipHostMallocMapped | hipHostMallocPortable) != hipSuccess) return (int *)nullptr;
-        h[kHostLastK] = -1;
-        h[kHostTmo] = 0;
-        return h;
-    }();
-    return p;
+// Mapped host words per workspace: [kHostSteps] the step count of the previous call (written by the
+// device; it only sizes the next call's run of step launches), [kHostTmo] the sticky timeout flag.
+std::mutex g_words_mu;
+std::unordered_map<const void *, int *> &words_map() {
+    static std::unordered_map<const void *, int *> m;
+    return m;
+}
+int *host_words(const void *ws) {
+    std::lock_guard<std::mutex> lk(g_words_mu);
+    auto &m = words_map();
+    auto it = m.find(ws);
+    if (it != m.end()) return it->second;
+    int *h = nullptr;
+    if (hipHostMalloc(&h, 128, hipHostMallocMapped | hipHostMallocPortable) != hipSuccess) return nullptr;
+    h[kHostSteps] = -1;
+    h[kHostTmo] = 0;
+    m.emplace(ws, h);
+    return h;
 }
 
 // per-device constants, set once (thread-per-GPU callers may race here)
@@ -601,90 +659,95 @@ DeviceInfo &device_info(int dev) {
         DeviceInfo &d = info[dev];
         int c = 0;
         d.err = hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev);
-        if (d.err == hipSuccess)
-            d.err = hipFuncSetAttribute((const void *)inp_rows, hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024);
         d.ncu = c > 0 ? c : 1;
     });
     return info[dev];
+}
+
+template <int G>
+hipError_t run_march(const float *in, int64_t pitch, Args a, int ncu, int *hw, const InpaintOpts &o, hipStream_t st) {
+    hipError_t e;
+    const size_t n = (size_t)a.H * a.W;
+    if ((e = hipMemsetAsync(a.ctl, 0, sizeof(Ctl), st)) != hipSuccess) return e;
+    const int ib = (int)std::min<size_t>((n + 255) / 256, 2048);
+    hipLaunchKernelGGL(tl_init, dim3(ib), dim3(256), 0, st, in, pitch, a);
+    if ((e = dbg_sync("tl_init", st)) != hipSuccess) return e;
+    if (a.radius < 1) return hipSuccess;  // no neighbourhood: nothing changes (cv2 uses radius >= 1)
+    // step launches: as many as the previous call on this workspace needed (+3); the persistent
+    // kernel takes whatever is left
+    const int prev = hw ? __atomic_load_n(hw + kHostSteps, __ATOMIC_RELAXED) : -1;
+    int nsteps = prev < 0 ? 48 : prev + 3;
+    if (o.steps >= 0) nsteps = o.steps;
+    static const bool trace = getenv("DSX_INPAINT_TRACE") != nullptr;  // debugging: the state after each step
+    for (int s = 0; s < nsteps; ++s) {
+        hipLaunchKernelGGL(tl_step<G>, dim3(kStepBlocks), dim3(256), 0, st, a, (unsigned)s);
+        if ((e = dbg_sync("tl_step", st)) != hipSuccess) return e;
+        if (trace) {
+            State S;
+            if ((e = hipMemcpyAsync(&S, &a.ctl->st[(s + 1) % 3], sizeof(State), hipMemcpyDeviceToHost, st)) != hipSuccess ||
+                (e = hipStreamSynchronize(st)) != hipSuccess)
+                return e;
+            fprintf(stderr, "step %d: phase %d k %d b %d sweep %d lsel %d nF %d nC %d changed %d bound %.3f\n", s, S.phase, S.k,
+                    S.b, S.sweep, S.lsel, S.nF, S.nC, S.changed, S.bound);
+            if (S.phase == kPhDone) break;
+        }
+    }
+    unsigned s0 = (unsigned)nsteps;
+    void *args[] = {&a, &s0};
+    if ((e = hipLaunchCooperativeKernel(reinterpret_cast<const void *>(tl_tail<G>), dim3(ncu), dim3(256), args, 0, st)) !=
+        hipSuccess)
+        return e;
+    return dbg_sync("tl_tail", st);
 }
 
 }  // namespace
 
 size_t inpaint_workspace(int H, int W) {
     const size_t n = (size_t)H * W;
-    const size_t ncnt = (size_t)H + W + 3;
-    return align256(n * 4) + align256(n * 8) + 2 * align256(n * 4) + 2 * align256(ncnt * 4) + align256(kCtlWords * 4);
+    return align256(sizeof(Ctl)) + align256(n * 4) + 4 * align256(n * 8) + align256(n * 4) + 4 * align256(n * 4);
 }
 
-hipError_t launch_inpaint(const float *in, int64_t pitch, int H, int W, int radius, float *out, void *ws, hipStream_t st) {
-    const int n = H * W;  // < 2^31 (host check)
-    const Views v = views(ws, H, W);
-    hipError_t e;
-    if (W > kInpaintMaxW) return hipErrorInvalidValue;  // the row kernel stages a row in LDS
+hipError_t launch_inpaint(const float *in, int64_t pitch, int H, int W, int radius, float *out, void *ws, hipStream_t st,
+                          const InpaintOpts &o) {
+    if ((int64_t)H * W >= kInpaintMaxPixels) return hipErrorInvalidValue;  // 30-bit pixel indices in the keys
     int dev = 0;
+    hipError_t e;
     if ((e = hipGetDevice(&dev)) != hipSuccess) return e;
     if (dev < 0 || dev >= 64) return hipErrorInvalidDevice;
     const DeviceInfo &di = device_info(dev);
     if (di.err != hipSuccess) return di.err;
-    hipLaunchKernelGGL(inp_rows, dim3(H), dim3(256), (size_t)W * 8, st, in, pitch, H, W, out, v.g, v.cnt, v.ncnt, v.ctl);
-    if ((e = dbg_sync("inp_rows", st)) != hipSuccess) return e;
-    if (radius < 1) return hipSuccess;  // no neighbourhood: nothing changes (cv2 uses radius >= 1)
-    int *hk = host_words();
-    int *hk_dev = nullptr;
-    if (hk && hipHostGetDevicePointer(reinterpret_cast<void **>(&hk_dev), hk, 0) != hipSuccess) hk_dev = nullptr;
-    const int SL = (H + kColS - 1) / kColS;
-    auto cols = SL <= 16 ? inp_cols<16> : SL <= 32 ? inp_cols<32> : SL <= 48 ? inp_cols<48> : inp_cols<0>;
-    hipLaunchKernelGGL(cols, dim3((W + kColW - 1) / kColW), dim3(1024), 0, st, v.g, H, W, v.layer, v.cnt, v.off, v.ctl,
-                       hk_dev);
-    if ((e = dbg_sync("inp_cols", st)) != hipSuccess) return e;
-    const int nch = (n + kChunk - 1) / kChunk;
-    hipLaunchKernelGGL(inp_scatter, dim3(nch), dim3(256), 0, st, v.layer, n, v.cnt, v.list, v.ctl);
-    if ((e = dbg_sync("inp_scatter", st)) != hipSuccess) return e;
-
-    // per-layer launches, enqueued without waiting: as many as the previous call needed (+1), at
-    // least 8; the persistent kernel takes whatever is left
-    const int maxk = H + W;
-    const int prev = hk ? __atomic_load_n(hk, __ATOMIC_RELAXED) : -1;
-    int L0 = std::min(maxk, prev < 0 ? 64 : std::max(8, prev + 1));
-    if (const char *fl = getenv("DSX_INPAINT_L0")) L0 = std::min(maxk, std::max(0, atoi(fl)));  // tests: force the split
-    // lanes per pixel: one per window row (8 up to radius 3, 16 up to 7); larger windows one pixel
-    // per thread.  512 blocks: an empty launch (a layer past K) costs ~1.5 us where 2048 cost ~4.6 us
-    const int np = radius <= 3 ? 8 : radius <= 7 ? 16 : 0;
-    const int lgrid = (int)std::min<size_t>(((size_t)n * (np ? np : 1) + 255) / 256, 512);
-    auto lay = np == 8 ? inp_layer<8> : np == 16 ? inp_layer<16> : inp_layer<0>;
-    for (int k = 1; k <= L0; ++k) {
-        hipLaunchKernelGGL(lay, dim3(lgrid), dim3(256), 0, st, out, v.layer, v.T, H, W, radius, k, v.list, v.off, v.ctl);
-        if ((e = dbg_sync("inp_layer", st)) != hipSuccess) return e;
-    }
-    if (L0 < maxk) {
-        auto rest = np == 8 ? inp_rest<8> : np == 16 ? inp_rest<16> : inp_rest<0>;
-        int rb = di.ncu;
-        if (const char *fb = getenv("DSX_INPAINT_RB")) rb = std::max(1, std::min(di.ncu, atoi(fb)));  // experiments
-        // barrier spin bound (polls with s_sleep 1); DSX_INPAINT_SPINS lowers it for the timeout test
-        const char *sp = getenv("DSX_INPAINT_SPINS");
-        const unsigned spins = sp ? (unsigned)strtoul(sp, nullptr, 10) : (1u << 23);
-        int *htmo = nullptr;
-        if (hk && hipHostGetDevicePointer(reinterpret_cast<void **>(&htmo), hk, 0) == hipSuccess) htmo += kHostTmo;
-        int k0 = L0 + 1;
-        float *o = out;
-        const int *lyr = v.layer, *lst = v.list, *of = v.off;
-        double *Tp = v.T;
-        int Hh = H, Ww = W, rad = radius;
-        int *ctl = v.ctl;
-        unsigned sl = spins;
-        void *args[] = {&o, &lyr, &Tp, &Hh, &Ww, &rad, &k0, &lst, &of, &ctl, &htmo, &sl};
-        if ((e = hipLaunchCooperativeKernel(reinterpret_cast<const void *>(rest), dim3(rb), dim3(256), args, 0, st)) !=
-            hipSuccess)
-            return e;
-        if ((e = dbg_sync("inp_rest", st)) != hipSuccess) return e;
-    }
-    return hipSuccess;
+    Args a = views(ws, H, W);
+    a.out = out;
+    a.radius = radius;
+    int *hw = host_words(o.status_key ? o.status_key : ws);
+    a.host = nullptr;
+    if (hw && hipHostGetDevicePointer(reinterpret_cast<void **>(&a.host), hw, 0) != hipSuccess) a.host = nullptr;
+    a.spin_limit = o.spin_limit ? o.spin_limit : (1u << 23);
+    int rb = di.ncu;
+    if (radius <= 3) return run_march<8>(in, pitch, a, rb, hw, o, st);
+    if (radius <= 7) return run_march<16>(in, pitch, a, rb, hw, o, st);
+    return run_march<0>(in, pitch, a, rb, hw, o, st);
 }
 
-// 1 if a persistent march timed out since the last call (and clears the flag), else 0
-int inpaint_take_timeout() {
-    int *h = host_words();
+int inpaint_take_timeout(const void *key) {
+    int *h = host_words(key);
     return h ? __atomic_exchange_n(h + kHostTmo, 0, __ATOMIC_ACQ_REL) : 0;
+}
+
+int inpaint_take_timeout_any() {
+    std::lock_guard<std::mutex> lk(g_words_mu);
+    int any = 0;
+    for (auto &kv : words_map()) any |= __atomic_exchange_n(kv.second + kHostTmo, 0, __ATOMIC_ACQ_REL);
+    return any;
+}
+
+void inpaint_forget(const void *key) {
+    std::lock_guard<std::mutex> lk(g_words_mu);
+    auto &m = words_map();
+    auto it = m.find(key);
+    if (it == m.end()) return;
+    (void)hipHostFree(it->second);
+    m.erase(it);
 }
 
 }  // namespace dsx

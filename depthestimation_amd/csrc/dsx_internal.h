@@ -141,6 +141,13 @@ struct PostArgs {
 };
 hipError_t launch_post_fast(const PostArgs &a, hipStream_t st);
 
+// Launch options of the hole-filling march (dsx_inpaint.hip), carried by PostFullArgs too.
+struct InpaintOpts {
+    unsigned spin_limit = 0;            // grid-barrier spin bound of the persistent tail (0: default)
+    int steps = -1;                     // step launches before the tail (-1: the previous call's count + 3)
+    const void *status_key = nullptr;   // whose sticky timeout flag / step history (nullptr: the workspace)
+};
+
 // Full post-processing (speckles + outliers + median + depth), dsx_post.hip.
 struct PostFullArgs {
     const float *disp;
@@ -152,6 +159,7 @@ struct PostFullArgs {
     float fB, doffs, eps, max_depth;
     int has_max;
     int fill_radius;  // > 0: Telea hole filling (radius) between the outlier removal and the median
+    InpaintOpts fill_opts;  // status key (nullptr: the post-processing workspace), spin bound
     int tail_t1;      // post_tail writes the outlier-cleaned map to t1 instead of the median (set internally)
     // workspace views (set by launch_post_full)
     int *parent, *count, *root, *lsz;
@@ -193,14 +201,20 @@ hipError_t launch_post_full(PostFullArgs a, void *ws, hipStream_t st, LaunchHook
 // true when launch_post_full runs the two-launch speckle form (else the four-launch union-find)
 bool post_full_two_launch(const PostFullArgs &a);
 
-// Hole filling (dsx_inpaint.hip): fill_holes(method='inpaint') on d <= 0, layered Telea marching.
-// Asynchronous: nothing is read back to the host.
+// Hole filling (dsx_inpaint.hip): fill_holes(method='inpaint') on d <= 0, Telea's march in
+// arrival-time order (T-buckets, fixed-point sweeps).  Asynchronous: nothing is read back to the host.
 size_t inpaint_workspace(int H, int W);
-constexpr int kInpaintMaxW = 19200;  // the row pass stages a row (8 B / px) in LDS
-hipError_t launch_inpaint(const float *in, int64_t pitch, int H, int W, int radius, float *out, void *ws, hipStream_t st);
-// 1 if a persistent march (inp_rest) timed out in a grid barrier since the last call - its remaining
-// layers stayed unfilled - and clears the flag; else 0
-int inpaint_take_timeout();
+constexpr int kInpaintMaxW = 1 << 20;              // no row staging: only the pixel count is bounded
+constexpr int64_t kInpaintMaxPixels = 1ll << 30;   // 30-bit pixel indices in the march's keys
+hipError_t launch_inpaint(const float *in, int64_t pitch, int H, int W, int radius, float *out, void *ws, hipStream_t st,
+                          const InpaintOpts &o = InpaintOpts{});
+// 1 if a march with status key `key` (the caller's workspace, or a handle's) timed out (grid barrier
+// or step cap) since the last call - its remaining holes stayed unfilled - and clears that flag; else 0
+int inpaint_take_timeout(const void *key);
+// the same over every key of the process (dsx_fill_holes_status)
+int inpaint_take_timeout_any();
+// drop the mapped status words of a key whose workspace is being freed
+void inpaint_forget(const void *key);
 
 // Birchfield-Tomasi block costs into K1's volume layout (dsx_bt.hip, oracle/bt_cost.py)
 struct BtArgs {

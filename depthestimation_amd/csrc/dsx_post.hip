@@ -1146,7 +1146,9 @@ hipError_t launch_post_full(PostFullArgs a, void *ws, hipStream_t st, LaunchHook
         // fill_holes (postprocess.py:160-166) on the cleaned map: t1 (or t0) -> t0, then the median
         float *dst = med_in == a.t0 ? a.t1 : a.t0;
         mark("fill_holes");
-        hipError_t e = launch_inpaint(med_in, Wc, a.H, Wc, a.fill_radius, dst, inpaint_ws, st);
+        InpaintOpts fo = a.fill_opts;
+        if (!fo.status_key) fo.status_key = ws;
+        hipError_t e = launch_inpaint(med_in, Wc, a.H, Wc, a.fill_radius, dst, inpaint_ws, st, fo);
         if (hook) hook->after(st);
         if (e != hipSuccess) return e;
         med_in = dst;

@@ -218,7 +218,7 @@ class HipBlockMatcher:
     def process_pair_device(self, left, right, fast_mode=False, max_speckle_size=100, max_diff=1.0,
                             apply_outlier_removal=True, outlier_threshold=2.5, outlier_kernel=5, fill_radius=0,
                             focal_length=None, baseline=None, doffs=0.0, eps=1e-6, max_depth=None, out_disp=None,
-                            out_depth=None, stream=None):
+                            out_depth=None, stream=None, fill_spin_limit=0, fill_steps=0):
         """StereoCore._process_pair (stereo_core.py:162-200) in ONE C-ABI call
         (dsx_process_pair_device): matcher -> crop [:, num_disp:] -> fast-mode median or
         postprocess_disparity (speckles, outliers, Telea hole filling when ``fill_radius`` > 0,
@@ -257,12 +257,21 @@ class HipBlockMatcher:
         pp.eps = float(eps)
         pp.max_depth = float(max_depth or 0.0)
         pp.has_max_depth = int(max_depth is not None)
+        pp.fill_spin_limit = int(fill_spin_limit)
+        pp.fill_steps = int(fill_steps)
         sptr = None if stream is None else (stream if isinstance(stream, int) else stream.cuda_stream)
         rc = _dsx.lib().dsx_process_pair_device(self._handle(), left.data_ptr(), right.data_ptr(), H, W,
                                                 left.stride(0), ctypes.byref(pp), _ptr(out_disp),
                                                 _ptr(out_depth) if want_depth else None, sptr)
         _dsx.check(rc, "dsx_process_pair_device")
         return out_disp, (out_depth if want_depth else None)
+
+    def fill_status(self):
+        """Raise RuntimeError if this handle's hole filling (process_pair_device with fill_radius > 0)
+        timed out since the last check (dsx_fill_holes_status_handle): that frame's holes were left
+        unfilled.  Call it once the stream has passed the frame; the condition is cleared."""
+        if self._h is not None:
+            _dsx.check(_dsx.lib().dsx_fill_holes_status_handle(self._h), "hole filling")
 
     def right_map_device(self, left, right, out_dR, stream=None):
         """Right-view winner map dR (int16 H x W, -1 where the search range is empty)."""
@@ -373,12 +382,14 @@ def _keep_until_done(t, stream):
 
 def postprocess_full_device(disp, crop, max_speckle_size=50, max_diff=1.0, apply_outlier_removal=True,
                             outlier_threshold=3.0, outlier_kernel=5, focal_length=None, baseline=None, doffs=0.0,
-                            eps=1e-6, max_depth=None, stream=None, apply_hole_filling=False, fill_kernel=3):
+                            eps=1e-6, max_depth=None, stream=None, apply_hole_filling=False, fill_kernel=3,
+                            workspace=None):
     """postprocess_disparity (postprocess.py:120-171) + depth on the device
     (dsx_postprocess_full_ex_device): speckles -> outliers -> hole filling
     (Telea 'inpaint' with radius ``fill_kernel`` when ``apply_hole_filling``) -> 3x3 median -> depth,
     all enqueued on ``stream`` without host synchronisation.  ``disp``: float32 H x W HIP tensor.
-    Returns (disp_cropped, depth or None) as HIP tensors."""
+    Returns (disp_cropped, depth or None) as HIP tensors.  ``workspace``: a ``FillWorkspace`` (default:
+    one per device and stream), whose flag ``fill_holes_status(workspace)`` reports a timed-out fill."""
     import torch
 
     if disp.dtype != torch.float32 or disp.dim() != 2 or disp.stride(1) != 1 or not disp.is_cuda:
@@ -392,8 +403,9 @@ def postprocess_full_device(disp, crop, max_speckle_size=50, max_diff=1.0, apply
         return out_disp, out_depth
     L = _dsx.lib()
     nbytes = L.dsx_postprocess_workspace_bytes(H, W, int(crop))
-    ws = torch.empty(nbytes, dtype=torch.uint8, device=disp.device)
-    sptr = None if stream is None else (stream if isinstance(stream, int) else stream.cuda_stream)
+    wsobj = workspace if workspace is not None else default_workspace(disp.device, stream, "post")
+    ws = wsobj.get(nbytes, disp.device, stream)
+    sptr = _stream_ptr(stream)
     rc = L.dsx_postprocess_full_ex_device(
         disp.data_ptr(), H, W, disp.stride(0), int(crop), int(max_speckle_size), float(max_diff),
         int(bool(apply_outlier_removal)), float(outlier_threshold), int(outlier_kernel),
@@ -406,17 +418,64 @@ def postprocess_full_device(disp, crop, max_speckle_size=50, max_diff=1.0, apply
     return out_disp, out_depth
 
 
-def fill_holes_status():
-    """Raise RuntimeError if a hole-filling call's persistent march timed out since the last check
-    (dsx_fill_holes_status: its remaining holes were left unfilled); the condition is cleared."""
-    _dsx.check(_dsx.lib().dsx_fill_holes_status(), "hole filling")
+def fill_holes_status(workspace=None):
+    """Raise RuntimeError if a hole-filling march timed out since the last check (its remaining
+    holes were left unfilled); the condition is cleared.  ``workspace``: a ``FillWorkspace`` (its
+    own flag, dsx_fill_holes_status_ws); None: every flag of the process (dsx_fill_holes_status)."""
+    L = _dsx.lib()
+    rc = L.dsx_fill_holes_status() if workspace is None else L.dsx_fill_holes_status_ws(workspace.ptr)
+    _dsx.check(rc, "hole filling")
 
 
-def fill_holes_device(disp, radius=5, out=None, stream=None):
+class FillWorkspace:
+    """Device workspace of the hole-filling march on one device, grown on demand.  It carries the
+    march's timeout flag and step history (both keyed by the workspace in the library), so calls
+    that share one report to it: ``fill_holes_status(ws)``.  One stream at a time."""
+
+    def __init__(self, device=None):
+        self.device = device
+        self.buf = None
+
+    def get(self, nbytes, device, stream=None):
+        import torch
+        if self.buf is None or self.buf.numel() < nbytes or self.buf.device != device:
+            if self.buf is not None:
+                _keep_until_done(self.buf, stream)
+            self.buf = torch.empty(nbytes, dtype=torch.uint8, device=device)
+        return self.buf
+
+    @property
+    def ptr(self):
+        return None if self.buf is None else self.buf.data_ptr()
+
+
+_fill_ws = {}
+
+
+def _stream_ptr(stream):
+    return None if stream is None else (stream if isinstance(stream, int) else stream.cuda_stream)
+
+
+def default_workspace(device, stream, kind="fill"):
+    """The workspace shared by the ``kind`` calls ("fill": fill_holes_device, "post":
+    postprocess_full_device) on one (device, stream): a stable key for the library's step history
+    and timeout flag."""
+    import torch
+    key = (kind, device.index, _stream_ptr(stream) or torch.cuda.current_stream(device).cuda_stream)
+    ws = _fill_ws.get(key)
+    if ws is None:
+        ws = _fill_ws[key] = FillWorkspace(device)
+    return ws
+
+
+def fill_holes_device(disp, radius=5, out=None, stream=None, workspace=None, spin_limit=0, steps=0):
     """fill_holes(disparity, method='inpaint', kernel_size=radius) on the device
-    (postprocess.py:72-118; dsx_fill_holes_device): Telea inpainting of the pixels <= 0, equal to
-    the host restatement (postprocess._telea_inpaint).  ``disp``: float32 H x W HIP tensor (unit
-    column stride).  Asynchronous on ``stream``; returns the filled float32 H x W tensor."""
+    (postprocess.py:72-118; dsx_fill_holes_ex_device): Telea inpainting of the pixels <= 0 in
+    cv2.inpaint's arrival-time order, equal to the host restatement (postprocess._telea_inpaint).
+    ``disp``: float32 H x W HIP tensor (unit column stride).  Asynchronous on ``stream``; returns the
+    filled float32 H x W tensor.  ``workspace``: a ``FillWorkspace`` (default: one per device and
+    stream).  ``spin_limit`` / ``steps``: dsx_fill_opts (tests: force a timeout / the persistent
+    launch)."""
     import torch
 
     if disp.dtype != torch.float32 or disp.dim() != 2 or disp.stride(1) != 1 or not disp.is_cuda:
@@ -430,10 +489,13 @@ def fill_holes_device(disp, radius=5, out=None, stream=None):
         return out
     L = _dsx.lib()
     nbytes = L.dsx_fill_holes_workspace_bytes(H, W)
-    ws = torch.empty(nbytes, dtype=torch.uint8, device=disp.device)
-    sptr = None if stream is None else (stream if isinstance(stream, int) else stream.cuda_stream)
-    rc = L.dsx_fill_holes_device(disp.data_ptr(), H, W, disp.stride(0), int(radius), out.data_ptr(), ws.data_ptr(),
-                                 nbytes, sptr)
-    _dsx.check(rc, "dsx_fill_holes_device")
+    wsobj = workspace if workspace is not None else default_workspace(disp.device, stream, "fill")
+    ws = wsobj.get(nbytes, disp.device, stream)
+    opts = _dsx.DsxFillOpts()
+    opts.spin_limit = int(spin_limit)
+    opts.steps = int(steps)
+    rc = L.dsx_fill_holes_ex_device(disp.data_ptr(), H, W, disp.stride(0), int(radius), out.data_ptr(), ws.data_ptr(),
+                                    nbytes, ctypes.byref(opts), _stream_ptr(stream))
+    _dsx.check(rc, "dsx_fill_holes_ex_device")
     _keep_until_done(ws, stream)
     return out

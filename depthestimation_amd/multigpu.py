@@ -352,14 +352,16 @@ class DepthPipeline:
         # other streams use shallow copies of ``core`` (same parameters and rectification cache) with
         # a handle of their own.
         # With several streams every stream gets a copy with its own in-flight handle (dsx_params.in_flight:
-        # the balance for a lone frame is dropped); the caller's core keeps its own handle untouched.
+        # the balance for a lone frame is dropped) on the pipeline's device; the caller's core keeps its
+        # own handle untouched.  The copies freeze the core's parameters as they are now: a later
+        # core.configure_sgbm does not reach them (build a new pipeline after reconfiguring).
         self.cores = [core]
         self._own = []
         if len(self.streams) > 1 and getattr(core, "sgbm", None) is not None and hasattr(core.sgbm, "params"):
             self.cores = []
             for _ in self.streams:
                 c = copy.copy(core)
-                c.sgbm = HipBlockMatcher(**dict(core.sgbm.params, in_flight=True))
+                c.sgbm = HipBlockMatcher(**dict(core.sgbm.params, in_flight=True, device=self.dev.index))
                 self._own.append(c.sgbm)
                 self.cores.append(c)
         self.shape = None
@@ -373,9 +375,10 @@ class DepthPipeline:
         self.hout = [None] * self.depth  # pinned depth maps, allocated on first use (size known then)
 
     def _finish(self, slot: int):
-        i, ev, z = self.pending[slot]
+        i, ev, z, core = self.pending[slot]
         ev.synchronize()
         self.pending[slot] = None
+        core.check_fill_status()  # a frame whose hole filling timed out raises instead of being yielded
         return i, (None if z is None else self.hout[slot][: z[0], : z[1]].numpy().copy())
 
     def push(self, i: int, pair) -> List[Tuple[int, Optional[np.ndarray]]]:
@@ -407,7 +410,7 @@ class DepthPipeline:
                 zshape = tuple(z.shape)
             ev = torch.cuda.Event()
             ev.record(st)
-        self.pending[slot] = (i, ev, zshape)
+        self.pending[slot] = (i, ev, zshape, self.cores[k])
         done.extend(self.poll(keep=i))
         return done
 

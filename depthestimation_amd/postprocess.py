@@ -11,17 +11,19 @@ each function restates the documented OpenCV semantics with numpy/scipy:
                           a region.
 * ``detect_outliers``   - normalised k x k box mean / mean of squares with BORDER_REFLECT_101
                           (cv2.boxFilter default): exact float64 window sums x 1/k^2 -> float32.
-* ``fill_holes``        - 'inpaint': Telea fast-marching inpainting, marched in 4-connected
-                          distance layers (see _telea_inpaint); 'nearest': iterated elliptical
-                          dilation (postprocess.py:106-116).
+* ``fill_holes``        - 'inpaint': Telea fast-marching inpainting in cv2.inpaint's arrival-time
+                          order (see _telea_inpaint); 'nearest': iterated elliptical dilation
+                          (postprocess.py:106-116).
 * ``median_blur3``      - 3 x 3 median with BORDER_REPLICATE (cv2.medianBlur, ksize 3).
 
 Parity against OpenCV is unpinned (cv2 absent); the reference's own behavioural test
 (tests/test_postproc_logic.py:35-42: the post-processed map is smoother than the fast-mode
-one) is re-run in tests/test_host_api.py. These run on the host: SURVEY.md section 8 row F2
-(GPU post-processing) is the next step for them.
+one) is re-run in tests/test_host_api.py.  These are the host forms; the device forms
+(csrc/dsx_post.hip, csrc/dsx_inpaint.hip) equal them bit for bit.
 """
 from __future__ import annotations
+
+import math
 
 import numpy as np
 from scipy import ndimage
@@ -83,13 +85,6 @@ def detect_outliers(disparity, threshold=3.0, kernel_size=5):
     return (np.abs(d - mean) > np.float32(threshold) * std) & valid
 
 
-def _telea_offsets(radius: int):
-    """Offsets (dy, dx) of the inpainting neighbourhood, 0 < dy^2 + dx^2 <= radius^2, row-major -
-    the summation order the device kernel uses too."""
-    return [(dy, dx) for dy in range(-radius, radius + 1) for dx in range(-radius, radius + 1)
-            if 0 < dy * dy + dx * dx <= radius * radius]
-
-
 def _telea_solve(t1, t2):
     """Telea's upwind eikonal update from two neighbour arrival times (1e6 = not available)."""
     both = (t1 < 1e6) & (t2 < 1e6)
@@ -100,85 +95,146 @@ def _telea_solve(t1, t2):
     return np.where(ok, s, 1.0 + np.minimum(t1, t2))
 
 
-def _telea_inpaint(img: np.ndarray, hole: np.ndarray, radius: int) -> np.ndarray:
-    """Telea (2004) fast-marching inpainting of float32 ``img`` where ``hole`` is True, marched in
-    4-connected distance layers (the form the GPU runs, csrc/dsx_inpaint.hip).
+_TELEA_DELTA = 0.7          # T-bucket width: below the least T step sqrt(2)/2 of a popped pixel's child
+_TELEA_MAX_SWEEPS = 1 << 16  # safety bound on one bucket's fixed-point sweeps (a DAG: never reached)
 
-    cv2.inpaint(INPAINT_TELEA) (postprocess.py:104) pops the narrow band from a heap ordered by
-    the arrival time T.  Here every hole pixel next to the previous layer forms the next layer and
-    the whole layer is filled at once from pixels of earlier layers only:
-      * T(p) = min over the 4 quadrants of solve(T_vertical, T_horizontal), neighbours of earlier
-        layers only (solve: Telea's first-order upwind update, float64);
-      * grad T at p from central / one-sided differences of earlier-layer neighbours' T;
-      * value(p) = sum w(q) v(q) / sum w(q) over earlier-layer q with 0 < |p - q|^2 <= radius^2,
-        w = max(|(p - q) . grad T| / |p - q| * 1 / |p - q|^2 * 1 / (1 + |T(q) - T(p)|), 1e-6)
-        (direction, distance and level-set factors), summed in float64 row by row (each window
-        row's cells left to right from 0.0, then the row sums top to bottom - the order the GPU
-        sums in, one lane per window row), rounded to float32 once.
-    Hole pixels no layer reaches (no known pixel in their region) keep their value.  Parity with
-    OpenCV's heap order is unpinned (cv2 absent); the device kernel equals this bit for bit."""
-    H, W = img.shape
-    out = np.asarray(img, np.float32).copy()
-    hole = np.asarray(hole, bool)
-    INF = np.iinfo(np.int32).max
-    layer = np.where(hole, INF, 0).astype(np.int64)
-    T = np.where(hole, 1e6, 0.0)
-    offs = _telea_offsets(radius)
-    k = 0
-    while True:
-        k += 1
-        prev = layer == k - 1
-        nb = np.zeros_like(prev)
-        nb[1:, :] |= prev[:-1, :]
-        nb[:-1, :] |= prev[1:, :]
-        nb[:, 1:] |= prev[:, :-1]
-        nb[:, :-1] |= prev[:, 1:]
-        front = (layer == INF) & nb
-        if not front.any():
-            break
-        ys, xs = np.nonzero(front)
 
-        def tv(dy, dx):
-            yy, xx = ys + dy, xs + dx
+def _telea_front(T, avail, cy, cx, H, W):
+    """T, grad T of pixels (cy, cx) from the 4-neighbours ``avail`` marks (Telea's upwind solve)."""
+    def tv(dy, dx):
+        yy, xx = cy + dy, cx + dx
+        inb = (yy >= 0) & (yy < H) & (xx >= 0) & (xx < W)
+        q = np.clip(yy, 0, H - 1) * W + np.clip(xx, 0, W - 1)
+        ok = inb & avail(q)
+        return ok, np.where(ok, T[q], 1e6)
+    (ou, tu), (od, td), (ol, tl), (orr, tr) = tv(-1, 0), tv(1, 0), tv(0, -1), tv(0, 1)
+    tp = np.minimum(np.minimum(_telea_solve(tu, tl), _telea_solve(td, tl)),
+                    np.minimum(_telea_solve(tu, tr), _telea_solve(td, tr)))
+    gx = np.where(orr & ol, (tr - tl) * 0.5, np.where(orr, tr - tp, np.where(ol, tp - tl, 0.0)))
+    gy = np.where(od & ou, (td - tu) * 0.5, np.where(od, td - tp, np.where(ou, tp - tu, 0.0)))
+    return tp, gx, gy
+
+
+def _telea_value(out, T, avail, cy, cx, tp, gx, gy, H, W, radius, rows, keep):
+    """Telea's weighted average over the disc cells ``avail`` marks: float64, each window row summed
+    left to right from 0.0, the row sums added top to bottom; float32(num / den) where den > 0, else
+    ``keep``."""
+    num = np.zeros(cy.size)
+    den = np.zeros(cy.size)
+    for row in rows:
+        rn = np.zeros(cy.size)
+        rd = np.zeros(cy.size)
+        for oy, ox in row:
+            yy, xx = cy + oy, cx + ox
             inb = (yy >= 0) & (yy < H) & (xx >= 0) & (xx < W)
-            yc, xc = np.clip(yy, 0, H - 1), np.clip(xx, 0, W - 1)
-            ok = inb & (layer[yc, xc] < k)
-            return ok, np.where(ok, T[yc, xc], 1e6)
+            q = np.clip(yy, 0, H - 1) * W + np.clip(xx, 0, W - 1)
+            ok = inb & avail(q)
+            ry, rx = -oy, -ox
+            d2 = ry * ry + rx * rx
+            w = np.maximum(np.abs(ry * gy + rx * gx) / math.sqrt(float(d2)) * (1.0 / d2)
+                           * (1.0 / (1.0 + np.abs(T[q] - tp))), 1e-6)
+            rn = np.where(ok, rn + w * out[q].astype(np.float64), rn)
+            rd = np.where(ok, rd + w, rd)
+        num = num + rn  # +0.0 for a row without terms: exact
+        den = den + rd
+    return np.where(den > 0, (num / np.where(den > 0, den, 1.0)).astype(np.float32), keep)
 
-        (ou, tu), (od, td), (ol, tl), (orr, tr) = tv(-1, 0), tv(1, 0), tv(0, -1), tv(0, 1)
-        tp = np.minimum(np.minimum(_telea_solve(tu, tl), _telea_solve(td, tl)),
-                        np.minimum(_telea_solve(tu, tr), _telea_solve(td, tr)))
-        gx = np.where(orr & ol, (tr - tl) * 0.5, np.where(orr, tr - tp, np.where(ol, tp - tl, 0.0)))
-        gy = np.where(od & ou, (td - tu) * 0.5, np.where(od, td - tp, np.where(ou, tp - tu, 0.0)))
-        num = np.zeros(ys.size)
-        den = np.zeros(ys.size)
-        for oyr in range(-radius, radius + 1):
-            rn = np.zeros(ys.size)
-            rd = np.zeros(ys.size)
-            for oy, ox in offs:
-                if oy != oyr:
-                    continue
-                yy, xx = ys + oy, xs + ox
-                inb = (yy >= 0) & (yy < H) & (xx >= 0) & (xx < W)
-                yc, xc = np.clip(yy, 0, H - 1), np.clip(xx, 0, W - 1)
-                ok = inb & (layer[yc, xc] < k)
-                ry, rx = -oy, -ox
-                d2 = ry * ry + rx * rx
-                w_dir = np.abs(ry * gy + rx * gx) / np.sqrt(float(d2))
-                w_dst = 1.0 / d2
-                w_lev = 1.0 / (1.0 + np.abs(T[yc, xc] - tp))
-                w = np.maximum(w_dir * w_dst * w_lev, 1e-6)
-                rn = np.where(ok, rn + w * out[yc, xc].astype(np.float64), rn)
-                rd = np.where(ok, rd + w, rd)
-            num = num + rn  # +0.0 for a row without terms: exact
-            den = den + rd
-        fill = den > 0
-        vals = out[ys, xs]
-        vals[fill] = (num[fill] / den[fill]).astype(np.float32)
-        out[ys, xs] = vals
-        T[ys, xs] = tp
-        layer[ys, xs] = k
-    return out
+
+def _telea_inpaint(img: np.ndarray, hole: np.ndarray, radius: int) -> np.ndarray:
+    """Telea (2004) fast-marching inpainting of float32 ``img`` where ``hole`` is True, in the
+    arrival-time order of cv2.inpaint(INPAINT_TELEA) (postprocess.py:104), restated for a parallel
+    machine (the form csrc/dsx_inpaint.hip runs; the sequential heap march is oracle/telea_heap.py).
+
+    The heap pops the narrow band by (T, push order); popping p fills each still-INSIDE 4-neighbour q
+    (up, left, down, right) from the pixels filled so far: T(q) by the upwind solve over its filled
+    4-neighbours, value(q) = sum w v / sum w over the filled pixels of its radius disc,
+    w = max(|(q-n).grad T| / |q-n| * 1/|q-n|^2 * 1/(1 + |T(n) - T(q)|), 1e-6).  A child's T exceeds its
+    parent's by at least sqrt(2)/2 (both upwind neighbours are at least the parent's T), so the pops of
+    one T-bucket [k*D, (k+1)*D), D = 0.7 < sqrt(2)/2, are exactly the band pixels in it when the bucket
+    starts, and their children land in later buckets.  Per bucket:
+      * order.  The push order inside a bucket is the lexicographic chain (T, T of the parent, ..., 0,
+        the seed's raster index, the directions back down); it is kept to one generation:
+        pop key (T, T_parent, root seed, direction from the parent, raster index), seeds (0, -1, raster,
+        0, raster);
+      * children.  Every INSIDE 4-neighbour of a pop; its parent is the pop neighbour with the least
+        pop key, its fill key (parent's pop key, its direction);
+      * values.  A child sees the pixels filled before the bucket and the bucket's children with a
+        smaller fill key - a DAG, so T and value are the unique fixed point of those equations.  Sweep
+        0 uses the pre-bucket pixels only; sweeps repeat (Jacobi) until no T or value bit changes.
+    Equal to ``telea_heap`` bit for bit on the C2 / C4 matcher maps and the tests' random maps
+    (tests/test_telea_heap.py); parity with OpenCV's own output is unpinned (cv2 absent).  Hole pixels
+    no known pixel reaches keep their value."""
+    H, W = img.shape
+    n = H * W
+    out = np.asarray(img, np.float32).ravel().copy()
+    hole = np.asarray(hole, bool).ravel()
+    INSIDE = np.iinfo(np.int64).max
+    fb = np.where(hole, INSIDE, -1).astype(np.int64)   # fill bucket: -1 known, INSIDE unfilled
+    T = np.where(hole, 1e6, 0.0)
+    Tp = np.full(n, -1.0)                              # pop key fields (seeds: T_parent -1, root = self)
+    root = np.arange(n, dtype=np.int64)
+    dirc = np.zeros(n, np.int64)
+    rows = [[(dy, dx) for dx in range(-radius, radius + 1) if 0 < dy * dy + dx * dx <= radius * radius]
+            for dy in range(-radius, radius + 1)]
+    h2 = hole.reshape(H, W)
+    nb = np.zeros((H, W), bool)
+    nb[1:, :] |= h2[:-1, :]
+    nb[:-1, :] |= h2[1:, :]
+    nb[:, 1:] |= h2[:, :-1]
+    nb[:, :-1] |= h2[:, 1:]
+    band = np.nonzero(~hole & nb.ravel())[0]            # the narrow band: seeds, then the filled pixels
+    ys_all, xs_all = np.divmod(np.arange(n, dtype=np.int64), W)
+    DIRS = ((-1, 0), (0, -1), (1, 0), (0, 1))           # OpenCV's neighbour order: up, left, down, right
+    k = 0
+    while band.size:
+        k = max(k, int(math.floor(T[band].min() / _TELEA_DELTA)))
+        bound = (k + 1) * _TELEA_DELTA
+        is_pop = T[band] < bound
+        P, band = band[is_pop], band[~is_pop]
+        # pop order (T, T_parent, root, direction, raster)
+        P = P[np.lexsort((P, dirc[P], root[P], Tp[P], T[P]))]
+        prank = np.full(n, -1, np.int64)
+        prank[P] = np.arange(P.size)
+        # children: INSIDE 4-neighbours of the pops; parent = least-ranked pop neighbour
+        ckey = np.full(n, INSIDE, np.int64)
+        py, px = ys_all[P], xs_all[P]
+        for di, (dy, dx) in enumerate(DIRS):
+            cy, cx = py + dy, px + dx
+            ok = (cy >= 0) & (cy < H) & (cx >= 0) & (cx < W)
+            c = cy[ok] * W + cx[ok]
+            kk = np.arange(P.size, dtype=np.int64)[ok] * 4 + di
+            m = fb[c] == INSIDE
+            np.minimum.at(ckey, c[m], kk[m])
+        C = np.nonzero(ckey != INSIDE)[0]
+        k += 1
+        if C.size == 0:
+            continue
+        fb[C] = k
+        kc = ckey[C]
+        cy, cx = ys_all[C], xs_all[C]
+        pre = lambda q: fb[q] < k                      # filled before this bucket (or known)
+        cur = lambda q: (fb[q] < k) | ((fb[q] == k) & (ckey[q] < kc))
+        Tn, vn = T.copy(), out.copy()
+        avail = pre
+        for _ in range(_TELEA_MAX_SWEEPS):
+            tp, gx, gy = _telea_front(Tn, avail, cy, cx, H, W)
+            v = _telea_value(vn, Tn, avail, cy, cx, tp, gx, gy, H, W, radius, rows, out[C])
+            changed = (tp != Tn[C]) | (v.view(np.int32) != vn[C].view(np.int32))
+            Tn[C] = tp
+            vn[C] = v
+            if avail is cur and not changed.any():
+                break
+            avail = cur
+        else:
+            raise RuntimeError("Telea march: a bucket did not converge")
+        T[C] = Tn[C]
+        out[C] = vn[C]
+        par = P[kc // 4]
+        Tp[C] = T[par]
+        root[C] = root[par]
+        dirc[C] = kc % 4
+        band = np.concatenate([band, C])
+    return out.reshape(H, W)
 
 
 def fill_holes(disparity, mask=None, method="inpaint", kernel_size=5):

@@ -39,8 +39,8 @@ from typing import Dict, Optional, Tuple
 
 import numpy as np
 
-from .matcher import (HipBlockMatcher, fill_holes_status, postprocess_fast_device, postprocess_full_device,
-                      rectify_device)
+from .matcher import (HipBlockMatcher, default_workspace, fill_holes_status, postprocess_fast_device,
+                      postprocess_full_device, rectify_device)
 from .postprocess import median_blur3, postprocess_disparity
 from .rectify import RectificationCache, rectify_images, to_grayscale_bgr
 
@@ -281,19 +281,26 @@ class StereoCore:
         p = self.sgbm_params
         f, B = p.get('focal_length'), p.get('baseline')
         doffs, eps, max_depth = p.get('doffs', 0.0), p.get('min_disp', 5.0), p.get('max_depth')
+        fill = bool(p.get('hole_filling', False)) and not self.fast_mode
         if 'compute_disparity_device' not in self.__dict__ and self.sgbm is not None and \
-                getattr(self.sgbm, 'process_pair_device', None) is not None:
+                getattr(self.sgbm, 'process_pair_device', None) is not None and \
+                getattr(self.sgbm, 'params', {}).get('float_mode', 'fixed') == 'fixed':
             # one C-ABI call per frame (dsx_process_pair_device): the handle owns the float map and
-            # the post-processing workspace
+            # the post-processing workspace, and the hole filling's timeout flag
+            self._fill_check = self.sgbm.fill_status if fill else None
             return self.sgbm.process_pair_device(
                 left, right, fast_mode=self.fast_mode, max_speckle_size=int(100 * self.downscale_factor),
                 max_diff=1.0, apply_outlier_removal=True, outlier_threshold=2.5, outlier_kernel=5,
                 fill_radius=3 if p.get('hole_filling', False) else 0, focal_length=f, baseline=B, doffs=doffs,
                 eps=eps, max_depth=max_depth, stream=stream)
         disp = self.compute_disparity_device(left, right, stream=stream)
+        self._fill_check = None
         if self.fast_mode:
             return postprocess_fast_device(disp, p['num_disp'], f, B, doffs, eps, max_depth, stream=stream)
         # fill_kernel 3: postprocess_disparity's default as _process_pair calls it (postprocess.py:165)
+        if fill:
+            ws = default_workspace(disp.device, stream, "post")
+            self._fill_check = lambda: fill_holes_status(ws)
         return postprocess_full_device(disp, p['num_disp'], max_speckle_size=int(100 * self.downscale_factor),
                                        max_diff=1.0, apply_outlier_removal=True, outlier_threshold=2.5,
                                        outlier_kernel=5, focal_length=f, baseline=B, doffs=doffs, eps=eps,
@@ -329,11 +336,18 @@ class StereoCore:
             self.right_rectified = _HostView(self.right_rectified)
             self.disparity_map = d.cpu().numpy()
             self.depth_map = None if z is None else z.cpu().numpy()
-            if self.sgbm_params.get('hole_filling', False) and not self.fast_mode:
-                fill_holes_status()  # the copies above waited for the march: a timed-out fill raises
+            self.check_fill_status()  # the copies above waited for the march: a timed-out fill raises
             return self.disparity_map, self.depth_map
         self.left_rectified, self.right_rectified = self._prepare_rectified(left_source, right_source)
         return self._process_pair(self.left_rectified, self.right_rectified)
+
+    def check_fill_status(self) -> None:
+        """Raise RuntimeError if the hole filling of this core's last device frame timed out (its
+        holes were left unfilled): the matcher handle's flag (one-call path) or the post-processing
+        workspace's (two-step path).  Call it once the frame's stream has finished."""
+        chk = getattr(self, '_fill_check', None)
+        if chk is not None:
+            chk()
 
     def _device_pipeline_ok(self, left, right) -> bool:
         if 'compute_disparity' in self.__dict__:

@@ -32,7 +32,8 @@
 extern "C" {
 #endif
 
-#define DSX_VERSION 104 /* 1.0.4: dsx_params.in_flight; 1.0.3: dsx_process_pair_device, dsx_fill_holes_status */
+#define DSX_VERSION 105 /* 1.0.5: arrival-order hole filling, per-workspace / per-handle fill status, dsx_fill_opts;
+                           1.0.4: dsx_params.in_flight; 1.0.3: dsx_process_pair_device, dsx_fill_holes_status */
 
 #define DSX_OK 0
 #define DSX_EINVAL (-1) /* bad argument (mirrors ValueError / cv2.error on bad input) */
@@ -206,21 +207,37 @@ int dsx_postprocess_full_ex_device(const void *d_disp, int32_t H, int32_t W, int
                                    void *d_workspace, size_t workspace_bytes, void *hip_stream);
 
 /* fill_holes(disparity, method='inpaint', kernel_size=radius) on the device (postprocess.py:72-118,
- * cv2.inpaint INPAINT_TELEA on d <= 0): Telea fast-marching inpainting marched in 4-connected
- * distance layers, equal bit for bit to the host restatement (postprocess.py _telea_inpaint).
- * d_disp: float32 H x W, row pitch `in_pitch` elements; d_out: contiguous float32 H x W.
- * d_workspace: >= dsx_fill_holes_workspace_bytes(H, W).  Asynchronous on hip_stream: the layers come
- * from an L1 distance transform on the device, the march runs as per-layer launches plus one
- * persistent launch for any layers beyond them; nothing is read back to the host. */
+ * cv2.inpaint INPAINT_TELEA on d <= 0): Telea fast-marching inpainting in cv2.inpaint's arrival-time
+ * (heap) order, equal bit for bit to the host restatement (postprocess.py _telea_inpaint) and, on every
+ * map tested, to the sequential heap march (oracle/telea_heap.py).
+ * d_disp: float32 H x W, row pitch `in_pitch` elements; d_out: contiguous float32 H x W; H * W < 2^30.
+ * d_workspace: >= dsx_fill_holes_workspace_bytes(H, W).  Asynchronous on hip_stream: the march runs
+ * as step launches (as many as the previous call on this workspace needed) plus one persistent
+ * launch for any steps beyond them; nothing is read back to the host. */
 size_t dsx_fill_holes_workspace_bytes(int32_t H, int32_t W);
 int dsx_fill_holes_device(const void *d_disp, int32_t H, int32_t W, int64_t in_pitch, int32_t radius, void *d_out,
                           void *d_workspace, size_t workspace_bytes, void *hip_stream);
 
-/* 1 if a hole-filling call's persistent march timed out in a grid barrier (its remaining holes were
- * left unfilled) since the last check: returns DSX_EHIP with a message and clears the condition;
- * DSX_OK otherwise.  The next hole-filling call (dsx_fill_holes_device, dsx_postprocess_full_ex_device
- * or dsx_process_pair_device with fill_radius > 0) checks it too and fails the same way.  The march
- * runs asynchronously, so the condition is known once the stream has passed that call. */
+/* Launch shape of the march (tests and experiments; zero-initialised = the defaults). */
+typedef struct dsx_fill_opts {
+    uint32_t spin_limit; /* grid-barrier spin bound of the persistent launch (0: default, ~2 s)    */
+    int32_t steps;       /* step launches before it: 0 adaptive, > 0 that many, < 0 none           */
+    int32_t reserved[6];
+} dsx_fill_opts;
+int dsx_fill_holes_ex_device(const void *d_disp, int32_t H, int32_t W, int64_t in_pitch, int32_t radius, void *d_out,
+                             void *d_workspace, size_t workspace_bytes, const dsx_fill_opts *opts, void *hip_stream);
+
+/* Timeout reports.  A march whose persistent launch times out (a grid barrier, or the step bound)
+ * leaves the holes of that call unfilled and raises a sticky flag that belongs to the caller's
+ * workspace (dsx_fill_holes_device, dsx_fill_holes_ex_device, dsx_postprocess_full_ex_device) or to
+ * the handle (dsx_process_pair_device).  The next hole-filling call with the same workspace / handle
+ * fails with DSX_EHIP and clears it; so do these queries (DSX_OK when clear).  The march runs
+ * asynchronously: the flag is known once the stream has passed that call.
+ *   dsx_fill_holes_status_ws      - the workspace's flag
+ *   dsx_fill_holes_status_handle  - the handle's flag (dsx_process_pair_device)
+ *   dsx_fill_holes_status         - every flag of the process (reports and clears them all) */
+int dsx_fill_holes_status_ws(const void *d_workspace);
+int dsx_fill_holes_status_handle(dsx_handle *h);
 int dsx_fill_holes_status(void);
 
 /* The per-frame call of the drop-in path, StereoCore._process_pair on the device (stereo_core.py:
@@ -247,7 +264,9 @@ typedef struct dsx_post_params {
     int32_t fill_radius;       /* 0, or 3 with hole_filling=True (postprocess.py:165 fill_kernel 3) */
     int32_t has_depth;         /* focal_length and baseline are set (stereo_core.py:186)            */
     int32_t has_max_depth;
-    int32_t reserved[5];
+    uint32_t fill_spin_limit;  /* hole filling's persistent-launch spin bound (0: default; tests)    */
+    int32_t fill_steps;        /* hole filling's step launches: 0 adaptive, > 0 that many, < 0 none */
+    int32_t reserved[3];
 } dsx_post_params;
 
 /* dL, dR: device uint8 H x W (row stride `stride_bytes`), rectified.  d_out_disp / d_out_depth:

@@ -16,17 +16,16 @@ structure OpenCV's fast-marching implementation is documented to have:
 
 The per-pixel arithmetic - the T solve, the gradient of T, the weights
 w = max(|r . grad T| / |r| * 1 / |r|^2 * 1 / (1 + |T(q) - T(p)|), 1e-6), float64 sums per window row
-(left to right) added top to bottom, one float32 rounding - is exactly that of the layered
-restatement the GPU runs (depthestimation_amd/postprocess._telea_inpaint).  So ``telea_heap`` and the
-layered march differ ONLY in the order: here one pixel at a time by arrival time (a pixel can use a
-neighbour filled earlier in the same distance layer), there every pixel of an L1 distance layer at
-once from the earlier layers.  tools/telea_divergence.py measures that difference on the C2 / C4
-matcher maps.  Parity of either form with OpenCV's own output is unpinned.
+(left to right) added top to bottom, one float32 rounding - is that of the product's parallel form
+(depthestimation_amd/postprocess._telea_inpaint, which the GPU runs); here it runs one pixel at a
+time in heap order, there bucket by bucket with fixed-point sweeps.  tests/test_inpaint.py holds the
+two equal bit for bit; tools/telea_divergence.py measures them on the C2 / C4 matcher maps.  Parity
+with OpenCV's own output is unpinned.
 
 ``telea_heap`` is pinned by ``telea_heap_list``: the same march with the queue kept as an explicitly
 sorted Python list (OpenCV's queue is a sorted list with first-in-first-out ties), and by the
-single-layer case (holes of isolated pixels more than 2r apart), where both orders must agree with the
-layered form bit for bit (tests/test_telea_heap.py).
+isolated-pixel case (holes more than 2r apart), where every order computes the same thing
+(tests/test_telea_heap.py).
 """
 from __future__ import annotations
 

@@ -1,72 +1,14 @@
 """Hole filling (fill_holes method 'inpaint', postprocess.py:72-118 -> cv2.inpaint INPAINT_TELEA):
-the layered Telea restatement on the host, pinned by an independent per-pixel loop restatement
-(CPU), and the device kernel against it bit for bit (GPU).  Parity with OpenCV is unpinned (cv2 is
-absent); the reference's own behavioural check (holes filled between their neighbours' values) is
+the arrival-time (T-bucket, fixed-point) restatement on the host, pinned bit for bit by the
+sequential heap march (oracle/telea_heap.py, the order cv2.inpaint pops its narrow band), and the
+device kernel against both (GPU).  Parity with OpenCV's own output is unpinned (cv2 is absent); the
+reference's own behavioural check (holes filled between their neighbours' values) is
 tests/test_host_api.py::test_fill_holes_inpaint_and_nearest."""
-import math
-
 import numpy as np
 import pytest
 
 from depthestimation_amd import postprocess as pp
-
-
-def _loop_inpaint(img, hole, radius, row_sums=True):
-    """Per-pixel, per-layer loop form of the layered Telea marching (plain Python floats).
-    row_sums=False: the round-2 summation order (every window cell in row-major order into one
-    float64 sum), kept as a second, independent oracle for the sums."""
-    H, W = img.shape
-    out = [[float(v) for v in row] for row in np.asarray(img, np.float32)]
-    INF = 1 << 40
-    layer = [[INF if hole[y][x] else 0 for x in range(W)] for y in range(H)]
-    T = [[1e6 if hole[y][x] else 0.0 for x in range(W)] for y in range(H)]
-    offs = [(dy, dx) for dy in range(-radius, radius + 1) for dx in range(-radius, radius + 1)
-            if 0 < dy * dy + dx * dx <= radius * radius]
-
-    def solve(t1, t2):
-        if t1 < 1e6 and t2 < 1e6:
-            r = 2.0 - (t1 - t2) * (t1 - t2)
-            if r > 0:
-                s = (t1 + t2 + math.sqrt(r)) / 2.0
-                if s >= t1 and s >= t2:
-                    return s
-        return 1.0 + min(t1, t2)
-
-    k = 0
-    while True:
-        k += 1
-        front = [(y, x) for y in range(H) for x in range(W) if layer[y][x] == INF and any(
-            0 <= y + dy < H and 0 <= x + dx < W and layer[y + dy][x + dx] == k - 1
-            for dy, dx in ((-1, 0), (1, 0), (0, -1), (0, 1)))]
-        if not front:
-            break
-        new = []
-        for y, x in front:
-            def t(yy, xx):
-                ok = 0 <= yy < H and 0 <= xx < W and layer[yy][xx] < k
-                return ok, (T[yy][xx] if ok else 1e6)
-            (ou, tu), (od, td), (ol, tl), (orr, tr) = t(y - 1, x), t(y + 1, x), t(y, x - 1), t(y, x + 1)
-            tp = min(min(solve(tu, tl), solve(td, tl)), min(solve(tu, tr), solve(td, tr)))
-            gx = (tr - tl) * 0.5 if (orr and ol) else (tr - tp if orr else (tp - tl if ol else 0.0))
-            gy = (td - tu) * 0.5 if (od and ou) else (td - tp if od else (tp - tu if ou else 0.0))
-            num = den = 0.0
-            for oyr in (range(-radius, radius + 1) if row_sums else [None]):  # window rows, each from 0.0
-                rn = rd = 0.0
-                for oy, ox in offs:
-                    qy, qx = y + oy, x + ox
-                    if (row_sums and oy != oyr) or not (0 <= qy < H and 0 <= qx < W) or layer[qy][qx] >= k:
-                        continue
-                    ry, rx = -oy, -ox
-                    d2 = ry * ry + rx * rx
-                    w = max(abs(ry * gy + rx * gx) / math.sqrt(d2) * (1.0 / d2) * (1.0 / (1.0 + abs(T[qy][qx] - tp))), 1e-6)
-                    rn += w * out[qy][qx]
-                    rd += w
-                num += rn
-                den += rd
-            new.append((y, x, tp, float(np.float32(num / den)) if den > 0 else out[y][x]))
-        for y, x, tp, v in new:
-            T[y][x], out[y][x], layer[y][x] = tp, v, k
-    return np.array(out, np.float32)
+from oracle.telea_heap import telea_heap
 
 
 def _holey(H, W, seed, frac=0.15):
@@ -79,29 +21,64 @@ def _holey(H, W, seed, frac=0.15):
     return d
 
 
-@pytest.mark.parametrize("shape,radius,seed", [((12, 17), 3, 1), ((9, 23), 5, 2), ((15, 11), 1, 3), ((7, 7), 2, 4)])
-def test_layered_inpaint_matches_loop_restatement(shape, radius, seed):
+def _bits(a):
+    return np.asarray(a, np.float32).view(np.int32)
+
+
+@pytest.mark.parametrize("shape,radius,seed", [((12, 17), 3, 1), ((9, 23), 5, 2), ((15, 11), 1, 3), ((7, 7), 2, 4),
+                                               ((30, 41), 3, 5), ((25, 19), 4, 6)])
+def test_inpaint_equals_heap_march(shape, radius, seed):
     d = _holey(*shape, seed)
-    np.testing.assert_array_equal(pp.fill_holes(d, method="inpaint", kernel_size=radius),
-                                  _loop_inpaint(d, d <= 0, radius))
+    np.testing.assert_array_equal(_bits(pp.fill_holes(d, method="inpaint", kernel_size=radius)),
+                                  _bits(telea_heap(d, d <= 0, radius)))
 
 
-def _ulps(a, b):
-    a = np.asarray(a, np.float32).view(np.int32).astype(np.int64)
-    b = np.asarray(b, np.float32).view(np.int32).astype(np.int64)
-    return np.abs(a - b)
+@pytest.mark.parametrize("seed", range(12))
+def test_inpaint_equals_heap_march_random(seed):
+    """Random sizes, radii and hole kinds (scattered, dense, blocks, a border band)."""
+    rng = np.random.default_rng(100 + seed)
+    H, W = int(rng.integers(5, 36)), int(rng.integers(5, 44))
+    r = int(rng.choice([1, 2, 3, 3, 4, 5]))
+    d = (10 + 0.3 * np.arange(W)[None, :] + 0.1 * np.arange(H)[:, None]
+         + rng.integers(-4, 5, (H, W)) / 16.0).astype(np.float32)
+    kind = seed % 4
+    if kind == 0:
+        d[rng.random((H, W)) < 0.3] = 0
+    elif kind == 1:
+        d[rng.random((H, W)) < 0.6] = 0
+    elif kind == 2:
+        for _ in range(3):
+            y0, x0 = rng.integers(0, H), rng.integers(0, W)
+            d[y0:y0 + rng.integers(1, 12), x0:x0 + rng.integers(1, 12)] = 0
+    else:
+        d[:, :rng.integers(1, 8)] = 0
+        d[rng.random((H, W)) < 0.1] = 0
+    np.testing.assert_array_equal(_bits(pp.fill_holes(d, method="inpaint", kernel_size=r)),
+                                  _bits(telea_heap(d, d <= 0, r)))
 
 
-@pytest.mark.parametrize("shape,radius,seed", [((12, 17), 3, 1), ((9, 23), 5, 2), ((15, 11), 1, 3), ((20, 30), 3, 5),
-                                               ((25, 19), 3, 6)])
-def test_row_sum_order_within_one_ulp_of_offset_order(shape, radius, seed):
-    """The row-blocked float64 sums the GPU reproduces (lane per window row) against the round-2
-    offset-order sums: at most 1 float32 ulp apart on every filled pixel (the oracle was
-    reordered to match the kernel; this keeps the old order as an independent check)."""
-    d = _holey(*shape, seed)
-    a = pp.fill_holes(d, method="inpaint", kernel_size=radius)
-    b = _loop_inpaint(d, d <= 0, radius, row_sums=False)
-    assert _ulps(a, b).max() <= 1
+@pytest.mark.parametrize("case", ["center", "square", "disc", "diagonal", "grid", "corner"])
+def test_inpaint_equals_heap_march_symmetric(case):
+    """Symmetric holes: many pixels share an arrival time, so the push order inside a bucket decides
+    which of them see each other."""
+    yy, xx = np.mgrid[0:41, 0:41]
+    d = (5 + 0.2 * xx + 0.1 * yy).astype(np.float32)
+    if case == "center":
+        d[:] = 0
+        d[20, 20] = 5
+    elif case == "square":
+        d[8:33, 8:33] = 0
+    elif case == "disc":
+        d[(xx - 20) ** 2 + (yy - 20) ** 2 < 200] = 0
+    elif case == "diagonal":
+        d[np.abs(xx - yy) < 4] = 0
+    elif case == "grid":
+        d[::3, :] = 0
+        d[:, ::4] = 0
+    else:
+        d[1:, 1:] = 0
+    np.testing.assert_array_equal(_bits(pp.fill_holes(d, method="inpaint", kernel_size=3)),
+                                  _bits(telea_heap(d, d <= 0, 3)))
 
 
 def test_inpaint_edge_cases():
@@ -112,6 +89,10 @@ def test_inpaint_edge_cases():
     np.testing.assert_array_equal(f, np.full_like(d, 7.5))
     g = np.arange(20, dtype=np.float32).reshape(4, 5) + 1  # no holes: unchanged
     np.testing.assert_array_equal(pp.fill_holes(g, method="inpaint", kernel_size=3), g)
+    n = _holey(10, 12, 3)
+    n[4, 4] = np.nan                                       # NaN is not <= 0: a known pixel, as in the mask
+    np.testing.assert_array_equal(_bits(pp.fill_holes(n, method="inpaint", kernel_size=3)),
+                                  _bits(telea_heap(n, n <= 0, 3)))
 
 
 def test_inpaint_fills_between_neighbours():
@@ -124,60 +105,65 @@ def test_inpaint_fills_between_neighbours():
     assert np.all(f[~known] >= d[10:20, 15:25].min() - 1) and np.all(f[~known] <= d[10:20, 15:25].max() + 1)
 
 
+# ---- device ----------------------------------------------------------------------------------
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("shape,radius,seed", [((60, 140), 3, 5), ((97, 333), 5, 6), ((33, 41), 1, 7),
-                                               ((720, 1152), 3, 8)])
+                                               ((20, 30), 9, 8), ((720, 1152), 3, 8)])
 def test_fill_holes_device_matches_host(shape, radius, seed):
     import torch
     from depthestimation_amd.matcher import fill_holes_device
     d = _holey(*shape, seed, frac=0.2)
     ref = pp.fill_holes(d, method="inpaint", kernel_size=radius)
     got = fill_holes_device(torch.from_numpy(d).cuda(), radius=radius)
-    np.testing.assert_array_equal(got.cpu().numpy(), ref)
+    np.testing.assert_array_equal(_bits(got.cpu().numpy()), _bits(ref))
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("shape,radius,seed", [((20, 30), 3, 5), ((25, 19), 3, 6), ((9, 23), 5, 2)])
-def test_fill_holes_device_within_one_ulp_of_offset_order(shape, radius, seed):
+@pytest.mark.parametrize("seed", range(6))
+def test_fill_holes_device_equals_heap_march(seed):
     import torch
     from depthestimation_amd.matcher import fill_holes_device
-    d = _holey(*shape, seed)
-    got = fill_holes_device(torch.from_numpy(d).cuda(), radius=radius).cpu().numpy()
-    assert _ulps(got, _loop_inpaint(d, d <= 0, radius, row_sums=False)).max() <= 1
+    rng = np.random.default_rng(200 + seed)
+    H, W = int(rng.integers(20, 60)), int(rng.integers(20, 80))
+    r = int(rng.choice([1, 2, 3, 5]))
+    d = _holey(H, W, 300 + seed, frac=float(rng.choice([0.1, 0.3, 0.6])))
+    got = fill_holes_device(torch.from_numpy(d).cuda(), radius=r).cpu().numpy()
+    np.testing.assert_array_equal(_bits(got), _bits(telea_heap(d, d <= 0, r)))
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("H", [1, 63, 1030, 2100, 3100])
+@pytest.mark.parametrize("H", [1, 63, 1030, 2100])
 def test_fill_holes_device_tall_maps(H):
-    """Every form of the column pass: a thread's row segment (ceil(H / 64) rows) held in registers
-    as 16, 32 or 48 rows, or walked by a row loop past 48 (H > 3072)."""
     import torch
     from depthestimation_amd.matcher import fill_holes_device
     d = _holey(H, 37, 20 + H % 7, frac=0.25)
-    d[H // 3: H // 3 + min(H, 300), 5:20] = 0  # a tall hole: layers across row segments
+    d[H // 3: H // 3 + min(H, 300), 5:20] = 0  # a tall hole
     e = d.copy()
     e[:, 30:] = 0                                # columns with no known pixel in any row ...
     e[: H // 2, :] = 0                           # ... and rows with none
     for m in (d, e, np.zeros_like(d)):
         ref = pp.fill_holes(m, method="inpaint", kernel_size=3)
         got = fill_holes_device(torch.from_numpy(m).cuda(), radius=3)
-        np.testing.assert_array_equal(got.cpu().numpy(), ref)
+        np.testing.assert_array_equal(_bits(got.cpu().numpy()), _bits(ref))
 
 
 @pytest.mark.gpu
 def test_fill_holes_device_edge_cases():
     import torch
     from depthestimation_amd.matcher import fill_holes_device
+    n = _holey(10, 12, 3)
+    n[4, 4] = np.nan
     for d in (np.zeros((6, 8), np.float32), np.arange(12, dtype=np.float32).reshape(3, 4) + 1,
-              np.where(np.eye(9, 13) > 0, 4.0, 0.0).astype(np.float32), np.full((1, 50), -1.0, np.float32)):
+              np.where(np.eye(9, 13) > 0, 4.0, 0.0).astype(np.float32), np.full((1, 50), -1.0, np.float32), n):
         ref = pp.fill_holes(d, method="inpaint", kernel_size=3)
         got = fill_holes_device(torch.from_numpy(d).cuda(), radius=3)
-        np.testing.assert_array_equal(got.cpu().numpy(), ref)
+        np.testing.assert_array_equal(_bits(got.cpu().numpy()), _bits(ref))
     # a pitched (column-sliced) input
     d = _holey(40, 90, 9)
     t = torch.from_numpy(d).cuda()[:, 10:]
-    np.testing.assert_array_equal(fill_holes_device(t, radius=3).cpu().numpy(),
-                                  pp.fill_holes(d[:, 10:], method="inpaint", kernel_size=3))
+    np.testing.assert_array_equal(_bits(fill_holes_device(t, radius=3).cpu().numpy()),
+                                  _bits(pp.fill_holes(d[:, 10:], method="inpaint", kernel_size=3)))
 
 
 @pytest.mark.gpu
@@ -209,28 +195,32 @@ def test_process_pair_device_with_hole_filling_matches_host():
     hd, hz = core._process_pair(L, R)
     dd, dz = core.process_pair_device(torch.from_numpy(L).cuda(), torch.from_numpy(R).cuda())
     torch.cuda.synchronize()
+    core.check_fill_status()
     np.testing.assert_array_equal(dd.cpu().numpy(), hd)
     np.testing.assert_array_equal(dz.cpu().numpy(), hz)
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("l0", ["0", "3", "5000"])
-def test_fill_holes_device_layer_split(l0, monkeypatch):
-    """The march's two forms: per-layer launches for layers 1..L0 and the persistent kernel (grid
-    barrier per layer) for the rest - all of them in the persistent kernel (L0 = 0), a split
-    (L0 = 3) and none (L0 = 5000) - on maps whose deepest layer is 1 to ~400."""
+@pytest.mark.parametrize("steps", [-1, 3, 5000])
+def test_fill_holes_device_step_split(steps):
+    """The march's two forms: step launches, then the persistent kernel (a grid barrier per step)
+    for the rest - all steps in the persistent kernel (steps < 0), a split (3) and none (5000) - on
+    maps whose march takes 2 to several hundred steps."""
     import torch
-    from depthestimation_amd.matcher import fill_holes_device
-    monkeypatch.setenv("DSX_INPAINT_L0", l0)
+    from depthestimation_amd.matcher import FillWorkspace, fill_holes_device
     d1 = np.zeros((160, 240), np.float32)
-    d1[7, 200] = 5.0                                   # one known pixel: ~390 layers
+    d1[7, 200] = 5.0                                   # one known pixel: hundreds of buckets
     d1[150, 3] = 9.0
-    d2 = _holey(90, 130, 11, frac=0.3)                 # scattered holes: few layers
+    d2 = _holey(90, 130, 11, frac=0.3)                 # scattered holes: few buckets
     d3 = np.zeros((64, 64), np.float32)                # nothing known: nothing reached
+    ws = FillWorkspace()
     for d, r in ((d1, 3), (d2, 5), (d3, 3), (_holey(50, 70, 12), 9)):
         ref = pp.fill_holes(d, method="inpaint", kernel_size=r)
-        got = fill_holes_device(torch.from_numpy(d).cuda(), radius=r)
-        np.testing.assert_array_equal(got.cpu().numpy(), ref)
+        got = fill_holes_device(torch.from_numpy(d).cuda(), radius=r, workspace=ws, steps=steps)
+        torch.cuda.synchronize()
+        from depthestimation_amd.matcher import fill_holes_status
+        fill_holes_status(ws)
+        np.testing.assert_array_equal(_bits(got.cpu().numpy()), _bits(ref))
 
 
 @pytest.mark.gpu
@@ -250,18 +240,13 @@ def test_fill_holes_device_does_not_block():
         busy = not st.query()
     st.synchronize()
     assert busy
-    np.testing.assert_array_equal(got.cpu().numpy(), ref)
+    np.testing.assert_array_equal(_bits(got.cpu().numpy()), _bits(ref))
 
 
-@pytest.mark.gpu
-@pytest.mark.parametrize("config", ["c4", "c2"])
-def test_fill_holes_device_on_matcher_output(config):
-    """The bench's hole-filling input: the matcher's own map at the config's size after the default
-    post-processing (speckles + outliers), radius 3 as _process_pair passes it - against the host
-    restatement, bit for bit (C4: ~180k holes over ~40 layers)."""
+def _matcher_fill_input(config):
     import torch
     from depthestimation_amd.configs import CONFIGS, matcher_kwargs
-    from depthestimation_amd.matcher import HipBlockMatcher, fill_holes_device, postprocess_full_device
+    from depthestimation_amd.matcher import HipBlockMatcher, postprocess_full_device
     from depthestimation_amd.synthetic import stereo_pair
     cfg = CONFIGS[config]
     H, W, D = cfg["H"], cfg["W"], cfg["num_disp"]
@@ -270,40 +255,84 @@ def test_fill_holes_device_on_matcher_output(config):
     dsp = torch.empty((H, W), dtype=torch.float32, device="cuda")
     bm.compute_device(torch.from_numpy(L).cuda(), torch.from_numpy(R).cuda(), out_float=dsp)
     clean, _ = postprocess_full_device(dsp, D, max_speckle_size=100, max_diff=1.0, outlier_threshold=2.5)
-    got = fill_holes_device(clean, radius=3)
     torch.cuda.synchronize()
     bm.close()
-    c = clean.cpu().numpy()
-    assert (c <= 0).sum() > 1000
-    np.testing.assert_array_equal(got.cpu().numpy(), pp.fill_holes(c, method="inpaint", kernel_size=3))
+    return clean
 
 
 @pytest.mark.gpu
-def test_fill_holes_timeout_is_reported_not_silent(monkeypatch):
-    """A persistent march whose grid barrier times out (forced: spin bound 0, every layer in the
-    persistent kernel) leaves holes unfilled; that must surface as an error - from
-    dsx_fill_holes_status and from the next hole-filling call - never as a silent success."""
+@pytest.mark.parametrize("config", ["c4", "c2"])
+def test_fill_holes_device_on_matcher_output(config):
+    """The bench's hole-filling input: the matcher's own map at the config's size after the default
+    post-processing (speckles + outliers), radius 3 as _process_pair passes it - against the host
+    restatement and the sequential heap march, bit for bit (C4: ~228k holes, 47 T-buckets)."""
+    from depthestimation_amd.matcher import fill_holes_device
+    clean = _matcher_fill_input(config)
+    got = fill_holes_device(clean, radius=3).cpu().numpy()
+    c = clean.cpu().numpy()
+    assert (c <= 0).sum() > 1000
+    np.testing.assert_array_equal(_bits(got), _bits(pp.fill_holes(c, method="inpaint", kernel_size=3)))
+    np.testing.assert_array_equal(_bits(got), _bits(telea_heap(c, c <= 0, 3)))
+
+
+@pytest.mark.gpu
+def test_fill_holes_timeout_is_reported_per_workspace():
+    """A persistent march whose grid barrier times out (forced: spin bound 1, every step in the
+    persistent kernel) leaves holes unfilled; that must surface as an error - from the workspace's
+    status and from the next call with that workspace - never as a silent success, and never on
+    another workspace."""
     import torch
-    from depthestimation_amd.matcher import fill_holes_device, fill_holes_status
+    from depthestimation_amd.matcher import FillWorkspace, fill_holes_device, fill_holes_status
     d = np.zeros((160, 240), np.float32)
-    d[7, 200] = 5.0  # ~390 layers: hundreds of barriers
-    fill_holes_status()  # clean state
-    monkeypatch.setenv("DSX_INPAINT_L0", "0")
-    monkeypatch.setenv("DSX_INPAINT_SPINS", "0")
-    got = fill_holes_device(torch.from_numpy(d).cuda(), radius=3)
+    d[7, 200] = 5.0  # hundreds of steps: hundreds of barriers
+    bad, good = FillWorkspace(), FillWorkspace()
+    x = torch.from_numpy(d).cuda()
+    got = fill_holes_device(x, radius=3, workspace=bad, spin_limit=1, steps=-1)
+    ok = fill_holes_device(x, radius=3, workspace=good)
     torch.cuda.synchronize()
     assert (got.cpu().numpy() <= 0).any()  # the march stopped early
+    fill_holes_status(good)                 # the other workspace is clean
     with pytest.raises(RuntimeError, match="timed out"):
-        fill_holes_status()
-    fill_holes_status()  # cleared by the report
-    # the sticky flag also fails the next hole-filling call
-    fill_holes_device(torch.from_numpy(d).cuda(), radius=3)
+        fill_holes_status(bad)
+    fill_holes_status(bad)  # cleared by the report
+    # the sticky flag also fails the next hole-filling call on that workspace
+    fill_holes_device(x, radius=3, workspace=bad, spin_limit=1, steps=-1)
     torch.cuda.synchronize()
-    monkeypatch.delenv("DSX_INPAINT_SPINS")
     with pytest.raises(RuntimeError, match="timed out"):
-        fill_holes_device(torch.from_numpy(d).cuda(), radius=3)
+        fill_holes_device(x, radius=3, workspace=bad)
     # with the normal bound everything is filled again and equals the host
-    got = fill_holes_device(torch.from_numpy(d).cuda(), radius=3)
+    ref = pp.fill_holes(d, method="inpaint", kernel_size=3)
+    got = fill_holes_device(x, radius=3, workspace=bad)
     torch.cuda.synchronize()
-    fill_holes_status()
-    np.testing.assert_array_equal(got.cpu().numpy(), pp.fill_holes(d, method="inpaint", kernel_size=3))
+    fill_holes_status(bad)
+    np.testing.assert_array_equal(_bits(got.cpu().numpy()), _bits(ref))
+    np.testing.assert_array_equal(_bits(ok.cpu().numpy()), _bits(ref))
+
+
+@pytest.mark.gpu
+def test_fill_timeout_is_per_handle():
+    """Two matcher handles on one device: a forced timeout in one handle's
+    process_pair hole filling fails only that handle's next call; the other handle's calls succeed."""
+    import torch
+    from depthestimation_amd.matcher import HipBlockMatcher
+    from depthestimation_amd.synthetic import stereo_pair
+    L, R, _ = stereo_pair(120, 300, 0, 64, seed=52)
+    tl, tr = torch.from_numpy(L).cuda(), torch.from_numpy(R).cuda()
+    a = HipBlockMatcher(num_disp=64, block_size=5)
+    b = HipBlockMatcher(num_disp=64, block_size=5)
+    kw = dict(fill_radius=3, max_speckle_size=100)
+    a.process_pair_device(tl, tr, fill_spin_limit=1, fill_steps=-1, **kw)
+    db, _ = b.process_pair_device(tl, tr, **kw)
+    torch.cuda.synchronize()
+    b.fill_status()
+    with pytest.raises(RuntimeError, match="timed out"):
+        a.process_pair_device(tl, tr, **kw)          # the sticky flag fails a's next call
+    db2, _ = b.process_pair_device(tl, tr, **kw)     # b is unaffected
+    da, _ = a.process_pair_device(tl, tr, **kw)      # a works again once reported
+    torch.cuda.synchronize()
+    a.fill_status()
+    b.fill_status()
+    np.testing.assert_array_equal(db2.cpu().numpy(), db.cpu().numpy())
+    np.testing.assert_array_equal(da.cpu().numpy(), db.cpu().numpy())
+    a.close()
+    b.close()

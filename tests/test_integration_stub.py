@@ -15,7 +15,7 @@ import pytest
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 FIELDS = ("min_disp", "num_disp", "block_size", "cost", "uniqueness_ratio", "disp12_max_diff", "subpixel",
           "float_mode", "path", "timing", "grid_blocks", "aggregation", "p1", "p2", "prefilter_cap", "sgbm_post",
-          "speckle_window_size", "speckle_range", "lr_form", "reserved")
+          "speckle_window_size", "speckle_range", "lr_form", "in_flight", "reserved")
 
 
 @pytest.fixture(scope="module")
@@ -27,12 +27,12 @@ def stub(dsx_lib_path):
     return mod
 
 
-def c_layout(tmp_path):
-    src = tmp_path / "probe.c"
-    body = "".join(f'printf("{f} %zu\\n", offsetof(dsx_params, {f}));' for f in FIELDS)
+def c_layout(tmp_path, struct="dsx_params", fields=FIELDS):
+    src = tmp_path / f"probe_{struct}.c"
+    body = "".join(f'printf("{f} %zu\\n", offsetof({struct}, {f}));' for f in fields)
     src.write_text('#include <stdio.h>\n#include <stddef.h>\n#include "dsx.h"\n'
-                   f'int main(void){{printf("size %zu\\n", sizeof(dsx_params));{body}return 0;}}\n')
-    exe = tmp_path / "probe"
+                   f'int main(void){{printf("size %zu\\n", sizeof({struct}));{body}return 0;}}\n')
+    exe = tmp_path / f"probe_{struct}"
     subprocess.run(["gcc", "-std=c99", "-I", os.path.join(ROOT, "include"), str(src), "-o", str(exe)], check=True)
     out = subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout
     return {k: int(v) for k, v in (ln.split() for ln in out.splitlines())}
@@ -47,6 +47,17 @@ def test_stub_struct_matches_header(stub, tmp_path):
     assert ctypes.sizeof(_dsx.DsxParams) == lay["size"]
     for f in FIELDS:
         assert getattr(_dsx.DsxParams, f).offset == lay[f], f
+
+
+def test_post_and_fill_structs_match_header(tmp_path):
+    """The Python bindings of dsx_post_params and dsx_fill_opts against a compiled C probe."""
+    from depthestimation_amd import _dsx
+    for struct, cls in (("dsx_post_params", _dsx.DsxPostParams), ("dsx_fill_opts", _dsx.DsxFillOpts)):
+        names = tuple(f[0] for f in cls._fields_)
+        lay = c_layout(tmp_path, struct, names)
+        assert ctypes.sizeof(cls) == lay["size"], struct
+        for f in names:
+            assert getattr(cls, f).offset == lay[f], (struct, f)
 
 
 def test_stub_defaults_and_validation(stub):
