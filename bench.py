@@ -288,6 +288,8 @@ def main():
     ap.add_argument("--in-flight", default="auto", choices=["auto", "0", "1"],
                     help="the timed lanes' handles carry dsx_params.in_flight (auto: when --streams > 1)")
     ap.add_argument("--breakdown-steps", type=int, default=500, help="launches of the one-stream kernel timing pass")
+    ap.add_argument("--video-frames", type=int, default=600,
+                    help="frames of the C4 video-facade secondary per rank (0: skip)")
     ap.add_argument("--no-dropin", action="store_true",
                     help="skip the drop-in pipeline secondary (StereoCore defaults, one call per frame)")
     ap.add_argument("--selftest-launch", action="store_true", help=argparse.SUPPRESS)
@@ -425,8 +427,10 @@ def main():
         mism = rk.allreduce(int(np.count_nonzero(got != want)), "sum")
         ref0 = torch.from_numpy(want).to(dev)
         parity = {"mismatches": mism, "frames_checked": ws, "pixels_checked": ws * H * W,
-                  "compared": "int16 x16 map of each rank's frame 0 from the timed matcher, bit for bit, before the "
-                              "timed region and again (on the device) after it",
+                  "compared": "int16 x16 maps, bit for bit: each rank's frame 0 from the lone-frame handle `matcher` "
+                              "before the timed region and again (on the device) after it, and the LAST output of "
+                              "every timed lane (the handles the region times: in_flight ones with --streams > 1) "
+                              "against the oracle map of its frame (timed_lanes)",
                   "oracle": "oracle/bm_ref.c (C restatement of the A5' contract; tests/test_oracle.py pins it)"}
 
     # secondary measurements (never `value`) run BEFORE the headline's warmup, so the timed region
@@ -488,6 +492,31 @@ def main():
     elapsed = rk.allreduce(float(elapsed), "max")
 
     if ref0 is not None:
+        # every timed lane's LAST output of the region (its own handle, in_flight when the lanes carry
+        # it) against the oracle map of the frame that step computed
+        lane_parity = []
+        want_of = {0: ref0}
+        for li, (_, _, of, _) in enumerate(lanes):
+            last = max((i for i in range(args.steps) if i % S == li), default=None)
+            if last is None:
+                continue
+            fi = last % len(frames) if B == 1 else None
+            if fi is None:  # batched lanes: the group's frames
+                gi = last % len(groups)
+                fis = list(range(gi * B, gi * B + B))
+            else:
+                fis = [fi]
+            mm = 0
+            for j, f in enumerate(fis):
+                if f not in want_of:
+                    want_of[f] = torch.from_numpy(CRef()(hostL[f], hostR[f], nthreads=th, **kw)["fixed"]).to(dev)
+                mm += int(torch.count_nonzero(of[j] != want_of[f]).item())
+            lane_parity.append({"lane": li, "handle": "in_flight" if lane_ifl else "lone-frame", "step": last,
+                                "frames": fis, "mismatches": mm})
+        lane_mm = rk.allreduce(sum(lp["mismatches"] for lp in lane_parity), "sum")
+        parity["timed_lanes"] = lane_parity
+        parity["mismatches_timed_lanes"] = lane_mm
+        parity["mismatches"] += lane_mm
         step(0)
         torch.cuda.synchronize(dev)
         after = rk.allreduce(int(torch.count_nonzero(out_fixed[0] != ref0).item()), "sum")
@@ -788,6 +817,9 @@ def secondaries(args, cfg, rk, matcher, frames, hostL, hostR, allL, allR, out_fi
     if args.config == "c2" and args.path == "fused" and B == 1 and not args.sgm and not args.no_dropin:
         out["dropin"] = dropin_figures(rk, dev, stream)
 
+    if args.config == "c2" and args.path == "fused" and B == 1 and not args.sgm and args.video_frames > 0:
+        out["video_c4"] = video_c4_figure(rk, args.video_frames)
+
     if B == 1 and args.path == "fused" and not args.no_batched and rk.rank == 0:
         # the same workload with 4 frame pairs per launch (video streams)
         Bb = 4
@@ -840,6 +872,68 @@ def secondaries(args, cfg, rk, matcher, frames, hostL, hostR, allL, allR, out_fi
         out["roofline_volume"] = rv
         vm.close()
     return out
+
+
+def video_c4_figure(rk, nframes: int, warm: int = 24) -> dict:
+    """BASELINE.json configs[3] as stated: a 720p stereo video stream through the reference's facade
+    (StereoDepthEstimatorVideo.py:69-147 fed by ThreadedStereoCapture, threaded_stereo.py:49-80) with
+    use_threading=True, target_fps=0 and devices=[this rank's GPU] (multigpu.DepthPipeline: frames in
+    flight), the reference's defaults (SAD 5x5, D 128, uniqueness 10, disp12MaxDiff 1, default
+    post-processing) and depth.  Host BGR frames in, host depth maps out.  Every rank runs its own
+    stream (weak scaling: frames sharded by rank, as the video path shards them); the rate is the
+    frames of all ranks over the slowest rank's time.  Frame 0's depth is checked against the oracle
+    matcher + the host post-processing chain."""
+    import torch
+    from depthestimation_amd import StereoDepthEstimatorVideo
+    from depthestimation_amd.postprocess import postprocess_disparity
+    from depthestimation_amd.rectify import to_grayscale_bgr
+    from depthestimation_amd.stereo_core import StereoCore
+    from oracle.cref import CRef
+    H, W, D, f, Bl = 720, 1280, 128, 1000.0, 0.1
+    base = [stereo_pair(H, W, 0, D, seed=9000 + 8 * rk.rank + i)[:2] for i in range(8)]
+    n = nframes + warm
+    Ls = [np.repeat(np.roll(base[i % 8][0], i // 8, 0)[:, :, None], 3, 2) for i in range(n)]
+    Rs = [np.repeat(np.roll(base[i % 8][1], i // 8, 0)[:, :, None], 3, 2) for i in range(n)]
+    torch.cuda.synchronize(rk.dev)
+    v = StereoDepthEstimatorVideo(Ls, Rs, fast_mode=False, target_fps=0, use_threading=True, devices=[rk.dev_index])
+    v.configure_sgbm(num_disp=D, block_size=5, focal_length=f, baseline=Bl)
+    it = v.estimate_depth()
+    z0 = next(it)
+    for _ in range(warm - 1):
+        next(it)
+    rk.barrier()
+    t0 = time.perf_counter()
+    k = sum(1 for _ in it)
+    dt = time.perf_counter() - t0
+    rk.barrier()
+    dt_max = rk.allreduce(float(dt), "max")
+    k_all = rk.allreduce(int(k), "sum")
+    # frame 0 on the host: BGR-weights gray, the oracle matcher, crop, postprocess_disparity as
+    # _process_pair calls it (hole filling off by default), disparity_to_depth
+    core = v.core
+    p = core.sgbm_params
+    gl, gr = to_grayscale_bgr(Ls[0]), to_grayscale_bgr(Rs[0])
+    th = max(1, min(16, cpu_threads_available() // rk.ws))
+    fixed = CRef()(gl, gr, nthreads=th, **{k_: v_ for k_, v_ in core.sgbm.params.items()
+                                            if k_ in ("min_disp", "num_disp", "block_size", "cost", "uniqueness_ratio",
+                                                      "disp12_max_diff", "subpixel")})["fixed"]
+    disp = (fixed.astype(np.float32) / np.float32(16.0))[:, p['num_disp']:]
+    disp = postprocess_disparity(disp, max_speckle_size=int(100 * core.downscale_factor), max_diff=1.0,
+                                 outlier_threshold=2.5, fill_method='inpaint', apply_outlier_removal=True,
+                                 apply_hole_filling=p.get('hole_filling', False))
+    want = StereoCore.disparity_to_depth(None, disp, p['focal_length'], p['baseline'], p.get('doffs', 0.0),
+                                         eps=p.get('min_disp', 5.0), max_depth=p.get('max_depth'))
+    mism = rk.allreduce(int(np.count_nonzero(np.asarray(z0).view(np.int32) != want.view(np.int32))), "sum")
+    return {"value": round(H * W * k_all / dt_max / 1e6, 1), "unit": "Mpix/s",
+            "fps": round(k_all / dt_max, 1), "fps_per_gpu": round(k_all / dt_max / rk.ws, 1),
+            "frames_per_rank": k, "warmup_frames": warm, "seconds": round(dt_max, 3),
+            "workload": "C4: 1280x720 BGR stereo stream, SAD 5x5, D 128, uniqueness 10, disp12MaxDiff 1 (the "
+                        "reference defaults), default post-processing + depth, StereoDepthEstimatorVideo("
+                        "use_threading=True, target_fps=0, devices=[local GPU]); host frames in, host depth out",
+            "scaling": "weak (each rank runs its own stream of frames_per_rank frames)",
+            "parity": {"mismatches": mism, "frames_checked": rk.ws,
+                       "compared": "float32 depth of each rank's frame 0 (bits) against oracle/bm_ref.c + the host "
+                                   "restatement of postprocess_disparity + disparity_to_depth"}}
 
 
 def dropin_figures(rk, dev, stream) -> dict:
@@ -895,7 +989,7 @@ def dropin_figures(rk, dev, stream) -> dict:
             import copy
             pcores = [copy.copy(core) for _ in range(3)]
             for c in pcores:
-                c.sgbm = HipBlockMatcher(**dict(core.sgbm.params, in_flight=True))
+                c.sgbm = HipBlockMatcher(**dict(core.sgbm.params, in_flight=True, device=core.sgbm.device))
             pst = [stream, torch.cuda.Stream(dev), torch.cuda.Stream(dev)]
             for i in range(30):
                 pcores[i % 3].estimate_depth_device(pairs[i % 2][2], pairs[i % 2][3], stream=pst[i % 3])

@@ -37,45 +37,8 @@
 // Register budget (waves per SIMD) the fused pass is compiled for, measured per cost (r01e): SAD at 4
 // waves spills in the row loop (C2 +45 %); SSD blocks of >= 4 waves (D > 128) gain at 4 despite init
 // spills (C3 392 -> 350 us); other SSD shapes were not measured and keep 3.
-#ifndef DSX_LR_KEYS  // key-tree argmin on the LR pass (experiment switch)
-#define DSX_LR_KEYS 1
-#endif
-#ifndef DSX_WPE
-#define DSX_WPE 3
-#endif
-#ifndef DSX_XB4  // SAD LR pass: exits parked 4 at a time (one b128 store) in a per-wave region
-#define DSX_XB4 1
-#endif
-#ifndef DSX_SSD_XB  // SSD / SAD1 LR pass: the SAD form of the diagonal move (DPP min + parked exits)
-#define DSX_SSD_XB 0  // measured slower at C3 (326 -> 349 us with 14 % fewer VALU per row step, r03m)
-#endif
-#ifndef DSX_EXP  // experiment bits (tools/exp_build.sh; timing only, results wrong): 1 no LR exit
-#define DSX_EXP 0  // stores, 2 no LR atomics, 4 no diagonal minima, 8 no dstar store, 16 scan argmin on LR
-#endif
-#ifndef DSX_WPE_SSD
-#define DSX_WPE_SSD 4
-#endif
-#ifndef DSX_LANE_REBUILD  // 4-wave SSD builds: lane index rebuilt per segment (wave index SGPR + mbcnt)
-#define DSX_LANE_REBUILD 1
-#endif
-#ifndef DSX_SEG_KARG  // LR pass: launch arguments reloaded per segment as well as per row
-#define DSX_SEG_KARG 1
-#endif
-#ifndef DSX_SADINIT_ABS  // SAD1 builds: transposed v_sad_u8 segment init (see SADINIT)
-#define DSX_SADINIT_ABS 1
-#endif
-#ifndef DSX_INIT_SB  // SSD segment init: scheduling barrier between column chunks
-#define DSX_INIT_SB 1
-#endif
-#ifndef DSX_LRCOAL  // SAD LR pass: the row's partial keys staged per wave in LDS, atomics on contiguous words
-#define DSX_LRCOAL 0  // WRITE_SIZE C4 -29 %, but C4 +6 %, C2r +9 % in time (r04ah): the LDS round trip sits in the row step
-#endif
-#ifndef DSX_T4B  // one-wave SAD builds whose slow-path staging indices are recomputed per load: 1 LR, 2 others
-#define DSX_T4B 1
-#endif
-#ifndef DSX_SSD_LDSDIAG  // SSD LR pass (NW >= 2): right-view winners read from the finished tile
-#define DSX_SSD_LDSDIAG 0  // measured slower (C3 325 -> 383 us): the reads wait in pairs at 128 VGPRs
-#endif
+constexpr int kWpe = 3;     // waves per SIMD the fused pass is compiled for (SAD, and SSD below 4 waves)
+constexpr int kWpeSsd = 4;  // SSD blocks of >= 4 waves
 
 #include <algorithm>
 #include <cstdio>
@@ -117,33 +80,6 @@ __device__ __forceinline__ uint32_t min_shr1(uint32_t src, uint32_t key) {
     return key;
 }
 __host__ __device__ constexpr int rnd16(int v) { return (v + 15) & ~15; }
-template <int N, typename F, int... I>
-__device__ __forceinline__ void static_for_impl(F &&f, std::integer_sequence<int, I...>) {
-    (f(std::integral_constant<int, I>{}), ...);
-}
-template <int N, typename F>
-__device__ __forceinline__ void static_for(F &&f) {
-    static_for_impl<N>(f, std::make_integer_sequence<int, N>{});
-}
-// A = min(A, ka) in the lanes of m, B = min(B, kb) in the others: the lane split as exec masks (a
-// constant SGPR pair), 2 VALU instead of 2 selects + 2 minima.  exec is restored before the asm ends.
-// The mask is built inside (lanes below 64 - K: ~0 >> K), so hipcc cannot hoist 32 of them out of
-// the row loop as 64 SGPRs.
-template <int K>
-__device__ __forceinline__ void min_split(uint32_t &A, uint32_t &B, uint32_t ka, uint32_t kb) {
-    uint64_t sv, m;
-    asm volatile(
-        "s_lshr_b64 %[m], -1, %[k]\n\t"
-        "s_and_saveexec_b64 %[sv], %[m]\n\t"
-        "v_min_u32 %[A], %[A], %[ka]\n\t"
-        "s_andn2_b64 exec, %[sv], %[m]\n\t"
-        "v_min_u32 %[B], %[B], %[kb]\n\t"
-        "s_mov_b64 exec, %[sv]"
-        : [A] "+v"(A), [B] "+v"(B), [sv] "=&s"(sv), [m] "=&s"(m)
-        : [k] "n"(K), [ka] "v"(ka), [kb] "v"(kb)
-        : "scc");
-}
-
 template <int R, bool SSD, int NW>
 struct Geo {
     static constexpr int TX = 32;
@@ -167,8 +103,8 @@ struct Geo {
     static constexpr int SLOT = SROW + REFB;
     static constexpr int SMEM0 = 4 * SLOT + TX * PITCH;
     static constexpr int SMEM = SMEM0 > (2 * R + 1) * SLOT ? SMEM0 : (2 * R + 1) * SLOT;
-    // LR pass, per-wave region after SMEM: the 31 exits (+ with DSX_LRCOAL the 128 end-of-row keys)
-    static constexpr int XRB = (!SSD && DSX_LRCOAL) ? 640 : 128;
+    // SAD LR pass, per-wave region after SMEM: the 31 exits
+    static constexpr int XRB = 128;
 };
 
 // Diagnostic build (-DDSX_STAMPS, libdsx_diag.so): per-phase s_memtime sums per block.
@@ -227,9 +163,6 @@ typedef const __attribute__((address_space(4))) uint32_t cu32;
 // loads through a pointer the compiler cannot hoist) instead of keeping them live across the loop,
 // where the SGPR budget spilled them to VGPR lanes: one v_readlane (a VALU op) per reuse, ~70 per
 // row step.
-#ifndef DSX_KARG
-#define DSX_KARG 1
-#endif
 template <bool RELOAD>
 __device__ __forceinline__ Bm2Args kargs_row(const Bm2Args &a) {
     if constexpr (RELOAD) {
@@ -256,7 +189,7 @@ __device__ __forceinline__ void bm2_segment(const Bm2Args &a_in, uint8_t *smem, 
     constexpr int side = SIDE;
     // the LR pass reloads the launch arguments per segment too: values derived from them in the
     // segment prologue would otherwise be hoisted out of the block's segment loop and spilled
-    const Bm2Args a = kargs_row<SIDE == 3 && DSX_KARG && DSX_SEG_KARG>(a_in);
+    const Bm2Args a = kargs_row<SIDE == 3>(a_in);
     // FSS: SSD sums in f32.  Squared differences, column sums and (offset) box sums are integers
     // below 2^24, so v_sub_f32 / v_fma_f32 / v_add_f32 (full rate, ~2 cycles) are exact and
     // replace the quarter-rate v_mad_i32_i24.  Box sums carry a +2^23 offset: for box < 2^23
@@ -267,9 +200,6 @@ __device__ __forceinline__ void bm2_segment(const Bm2Args &a_in, uint8_t *smem, 
     // where the packed pairs would leave half of the wave on padding disparities
     constexpr bool FSS = SSD && !ABS && R <= 5 && (SIDE == 0 || SIDE == 3 || SIDE == 4);
     constexpr bool SGK = SIDE == 4;  // left pass + OpenCV-form LR keys (lr_form 'sgbm' on the fused path)
-    // LDSD: the SSD LR pass takes the right-view winners from the finished tile in the epilogue
-    // (2 VALU per cost on most waves) instead of tracking the diagonals through the row loop (5)
-    constexpr bool LDSD = SIDE == 3 && SSD && !ABS && NW >= 2 && DSX_SSD_LDSDIAG;
     constexpr uint32_t OFF = FSS ? 0x4B000000u : 0u;
     typedef typename std::conditional<FSS, float, typename std::conditional<SSD, uint32_t, u16x2>::type>::type acc_t;
     uint8_t *tile = smem + 4 * SLOT;
@@ -278,7 +208,7 @@ __device__ __forceinline__ void bm2_segment(const Bm2Args &a_in, uint8_t *smem, 
     // SGPR) and mbcnt, so tid-derived values are computed per segment instead of held (and spilled)
     // across the kernel: 0 B of scratch.  The other builds keep threadIdx.x - the rebuild measured
     // slower there (C2r +6 %, C1 +14 %: fewer VGPRs, different occupancy and schedule).
-    constexpr bool LANE_RB = DSX_LANE_REBUILD && SSD && !ABS && NW >= 4;
+    constexpr bool LANE_RB = SSD && !ABS && NW >= 4;
     int ln = 0;
     if constexpr (LANE_RB)  // mbcnt inside the asm: not hoisted out of the segment loop
         asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(ln));
@@ -322,11 +252,11 @@ __device__ __forceinline__ void bm2_segment(const Bm2Args &a_in, uint8_t *smem, 
         } else {
             uint32_t v[4];
             // The one-wave SAD LR builds recompute 4 * tid per load: hoisted, the 4 clamped indices
-            // below are held across the kernel (with DSX_LRCOAL they spilled).  C4 19.5k -> 21.5k
+            // below are held across the kernel.  C4 19.5k -> 21.5k
             // Mpix/s with 3 frames in flight, C2r +1.5 %; the R >= 6 and two-wave builds measured
             // slower with it (C5 -0.5 %, C1 at D = 140 with the checks +2.5 %: profiles/r04ai_*)
             int t4 = 4 * tid;
-            if constexpr (!SSD && NW == 1 && (((DSX_T4B & 1) && SIDE == 3) || ((DSX_T4B & 2) && SIDE != 3)))
+            if constexpr (!SSD && NW == 1 && SIDE == 3)
                 asm volatile("" : "+v"(t4));
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
@@ -438,16 +368,13 @@ __device__ __forceinline__ void bm2_segment(const Bm2Args &a_in, uint8_t *smem, 
     acc_t cs[NC];
 #pragma unroll
     for (int c = 0; c < NC; ++c) cs[c] = acc_t(0);
-#ifndef DSX_SADINIT
-#define DSX_SADINIT 1
-#endif
     // Measured per instantiation (r02, tools/si_ab.sh, same box): C1 (R=2) 20.5 -> 19.5 us, C4 (R=2)
     // 57.3 -> 56.3 us, C5 (R=7) 610 -> 581 us; but the R=4 instantiation (C2) runs 72.9 -> 79.0 us
     // with it - its row loop is scheduled worse (more full vmcnt drains), not its init - so R=4 keeps
     // the row-by-row init.
     // SAD1 (ABS, one disparity per lane) takes the same transposed init with one v_sad_u8 per column
     // and row group (the pair's first entry only)
-    constexpr bool SADINIT = DSX_SADINIT && (ABS ? DSX_SADINIT_ABS : R != 4);
+    constexpr bool SADINIT = ABS || R != 4;
     if constexpr ((!SSD || ABS) && side != 1 && SADINIT) {
         // SAD (left / volume passes): rows in groups of 4, bytes transposed so that one v_sad_u8
         // sums a column's 4 row terms for one disparity: TP_g[j] = {P(j), P(j+1)} with P(j) the
@@ -570,11 +497,7 @@ __device__ __forceinline__ void bm2_segment(const Bm2Args &a_in, uint8_t *smem, 
     block_sync<NW>();
     {
         // groups of IG rows in flight: bounds the init phase's VGPRs below the main loop's
-#ifdef DSX_IG
-        constexpr int IG = DSX_IG;
-#else
         constexpr int IG = 3;
-#endif
 #pragma unroll 1
         for (int i0 = 0; i0 <= 2 * R; i0 += IG) {
             uint32_t iw[IG][5];
@@ -615,7 +538,7 @@ __device__ __forceinline__ void bm2_segment(const Bm2Args &a_in, uint8_t *smem, 
                 }
             }
             // SSD: one chunk's LDS words in flight at a time (hoisting them all spilled at 4 waves)
-            if constexpr (SSD && DSX_INIT_SB) __builtin_amdgcn_sched_barrier(0);
+            if constexpr (SSD) __builtin_amdgcn_sched_barrier(0);
         }
     }
     }
@@ -634,7 +557,7 @@ __device__ __forceinline__ void bm2_segment(const Bm2Args &a_in, uint8_t *smem, 
     const bool lane_writes = d0 < D;
 
     for (int y = yb; y < ye; ++y) {
-        const Bm2Args &a = kargs_row<SIDE == 3 && DSX_KARG>(a_in);
+        const Bm2Args &a = kargs_row<SIDE == 3>(a_in);
 #ifdef DSX_STAMPS
         ++nsteps;
 #endif
@@ -735,7 +658,7 @@ __device__ __forceinline__ void bm2_segment(const Bm2Args &a_in, uint8_t *smem, 
                 if constexpr (SSD) acc += cs[c];
                 else acc = as2(as1(acc) + as1(cs[c]));
             }
-            if constexpr (side == 3 && !LDSD) {
+            if constexpr (side == 3) {
                 // Right-view winners along the tile's diagonals: C_R(xr, d) = C(xr + m + d, d), so
                 // right pixel xr collects keys (C << s | d) from (x, d) with x - m - d = xr.  Each
                 // lane keeps the running key minimum of the diagonal through its slot(s); moving to
@@ -760,10 +683,9 @@ __device__ __forceinline__ void bm2_segment(const Bm2Args &a_in, uint8_t *smem, 
                 const bool lane0 = ln == 0;
                 const bool top = ln == 63;
                 // SAD exits: pixel k's at xq + k * XST - a 128-B region per wave after the block's LDS
-                // (DSX_XB4: the full-strip loop keeps 4 exits in registers and parks them with one
-                // single-lane b128 store; r03: 31 exec-masked b32 stores per row cost ~6 % at C2r),
-                // else this wave's slot in each tile row's padding
-                constexpr bool XREG = SSD ? DSX_SSD_XB : DSX_XB4;  // exits in the per-wave region
+                // (the full-strip loop keeps 4 exits in registers and parks them with one single-lane
+                // b128 store; r03: 31 exec-masked b32 stores per row cost ~6 % at C2r)
+                constexpr bool XREG = !SSD;  // exits in the per-wave region
                 uint8_t *xq = XREG ? smem + G::SMEM + G::XRB * wv : tile + Dp * CB + 4 * wv;
                 constexpr int XST = XREG ? 4 : PITCH;
                 uint32_t X[4] = {0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu};
@@ -783,21 +705,7 @@ __device__ __forceinline__ void bm2_segment(const Bm2Args &a_in, uint8_t *smem, 
                             if constexpr (SSD) *reinterpret_cast<uint32_t *>(tb + k * PITCH) = abits(acc);
                             else *reinterpret_cast<uint32_t *>(tb + k * PITCH) = as1(acc);
                         }
-                        if constexpr (SSD && DSX_SSD_XB) {
-                            // one slot per lane: the SAD move (min_shr1) with this lane's new key, and
-                            // the top lane's diagonal parked in LDS (4 at a time on full strips)
-                            const uint32_t key = (FULL || x0 + k < W) ? ((abits(acc) << ks) | dmE) : 0xFFFFFFFFu;
-                            Ae = k > 0 ? min_shr1(Ae, key) : key;
-                            if (k < TX - 1) {
-                                if constexpr (FULL) {
-                                    X[k & 3] = Ae;
-                                    if (((k & 3) == 3 || k == TX - 2) && top)
-                                        *reinterpret_cast<uint4 *>(xq + (k & ~3) * 4) = make_uint4(X[0], X[1], X[2], X[3]);
-                                } else if (top) {
-                                    *reinterpret_cast<uint32_t *>(xq + k * XST) = Ae;
-                                }
-                            }
-                        } else if constexpr (SSD) {
+                        if constexpr (SSD) {
                             if (FULL || x0 + k < W) Ae = umin2(Ae, (abits(acc) << ks) | dmE);
                             if (k < TX - 1) {
                                 const uint32_t F = (uint32_t)__builtin_amdgcn_mov_dpp((int)Ae, 0x13C, 0xF, 0xF, false);  // wave_ror:1
@@ -808,10 +716,7 @@ __device__ __forceinline__ void bm2_segment(const Bm2Args &a_in, uint8_t *smem, 
                             // (C << 16) | d by byte permute
                             const uint32_t kE = __builtin_amdgcn_perm(as1(acc), (uint32_t)d0, selE);
                             const uint32_t kO = __builtin_amdgcn_perm(as1(acc), (uint32_t)(d0 + 1), selO);
-                            if constexpr (DSX_EXP & 4) {
-                                Ae = kE;
-                                Ao = kO;
-                            } else if constexpr (FULL) {
+                            if constexpr (FULL) {
                                 if (k > 0) {
                                     const uint32_t nE = min_shr1(Ao, kE);
                                     Ao = umin2(Ae, kO);
@@ -831,8 +736,8 @@ __device__ __forceinline__ void bm2_segment(const Bm2Args &a_in, uint8_t *smem, 
                                     Ao = umin2(Ao, kO);
                                 }
                             }
-                            if (!(DSX_EXP & 1) && k < TX - 1) {  // exit
-                                if constexpr (DSX_XB4 && FULL) {
+                            if (k < TX - 1) {  // exit
+                                if constexpr (FULL) {
                                     X[k & 3] = Ao;
                                     if (((k & 3) == 3 || k == TX - 2) && top)
                                         *reinterpret_cast<uint4 *>(xq + (k & ~3) * 4) = make_uint4(X[0], X[1], X[2], X[3]);
@@ -850,27 +755,7 @@ __device__ __forceinline__ void bm2_segment(const Bm2Args &a_in, uint8_t *smem, 
                 else diag_loop(std::false_type{});
                 uint32_t *krow = a.lr_keys + fout + (long)y * W;
                 const int dtop = (wv + 1) * G::LDW - 1;  // disparity of the wave's top slot
-                if constexpr (DSX_EXP & 2) {
-                } else if constexpr (!SSD && XREG && DSX_LRCOAL) {
-                    // The row's 159 partial keys name the right pixels base .. base + 158 in order:
-                    // exit k at base + k, lane l's Ao / Ae at base + 157 - 2l / 158 - 2l.  Staged at word
-                    // j of the wave's region, they leave as three atomics on consecutive words: 10-11
-                    // 64-B requests a row step instead of 18-19 for the two stride-8-B pair atomics +
-                    // the exits
-                    uint32_t *xw = reinterpret_cast<uint32_t *>(xq);
-                    xw[157 - 2 * ln] = Ao;
-                    xw[158 - 2 * ln] = Ae;
-                    const int base = x0 - m - dtop;
-#pragma unroll
-                    for (int i = 0; i < 3; ++i) {
-                        const int j = 64 * i + ln;
-                        if (i < 2 || ln < 31) {
-                            const uint32_t K = xw[j];
-                            const int xk = base + j;
-                            if (K != 0xFFFFFFFFu && xk >= 0 && xk < W) atomicMin(krow + xk, K);
-                        }
-                    }
-                } else if constexpr (SSD && !DSX_SSD_XB) {
+                if constexpr (SSD) {
                     const int xe = x0 + (TX - 2 - ln) - m - dtop;  // E lane j: exit of pixel TX-2-j
                     if (ln < TX - 1 && E != 0xFFFFFFFFu && xe >= 0 && xe < W) atomicMin(krow + xe, E);
                 } else if (ln < TX - 1) {
@@ -879,9 +764,8 @@ __device__ __forceinline__ void bm2_segment(const Bm2Args &a_in, uint8_t *smem, 
                     if (E != 0xFFFFFFFFu && xe >= 0 && xe < W) atomicMin(krow + xe, E);
                 }
                 const int xa = x0 + TX - 1 - m - d0;
-                if constexpr (!SSD && XREG && DSX_LRCOAL) {
-                } else if (!(DSX_EXP & 2) && Ae != 0xFFFFFFFFu && xa >= 0 && xa < W) atomicMin(krow + xa, Ae);
-                if constexpr (!SSD && !(DSX_EXP & 2) && !(XREG && DSX_LRCOAL)) {
+                if (Ae != 0xFFFFFFFFu && xa >= 0 && xa < W) atomicMin(krow + xa, Ae);
+                if constexpr (!SSD) {
                     if (Ao != 0xFFFFFFFFu && xa - 1 >= 0 && xa - 1 < W) atomicMin(krow + xa - 1, Ao);
                 }
             } else if (lane_writes) {
@@ -948,7 +832,7 @@ __device__ __forceinline__ void bm2_segment(const Bm2Args &a_in, uint8_t *smem, 
             // Two argmin forms, chosen per instantiation from measurements (r01e): the key tree
             // wins on the LR pass (C3, C4) and 15x15 windows (C5); the compare/select scan keeps
             // the SIDE 0 pass at <= 11x11 at 151 VGPRs (the key tree costs C2 +7 %).
-            constexpr bool KEYS = (SIDE == 3 && DSX_LR_KEYS && !(DSX_EXP & 16)) || R >= 6;
+            constexpr bool KEYS = SIDE == 3 || R >= 6;
             uint32_t cb, dl;
             if constexpr (KEYS) {
                 // lowest-d argmin without compare/select scans: keys (cost << GB | global block) give
@@ -1075,7 +959,7 @@ __device__ __forceinline__ void bm2_segment(const Bm2Args &a_in, uint8_t *smem, 
                     if (a.float_mode == 1) pf = (float)(m + b) + (float)(cm - cp) / (float)(2 * den);
                 }
                 if (h == 0 && x < W) {
-                    if (lr_on && !(DSX_EXP & 8)) a.dstar[o] = valid ? (int16_t)b : (int16_t)-1;  // LR check: lr_fixup
+                    if (lr_on) a.dstar[o] = valid ? (int16_t)b : (int16_t)-1;  // LR check: lr_fixup
                     const int16_t fx = valid ? (int16_t)(m * 16 + f) : (int16_t)((m - 1) * 16);
                     if constexpr (SGK) {
                         // OpenCV's LR form: a unique winner offers (cost, d) to right pixel x - m - d
@@ -1090,58 +974,6 @@ __device__ __forceinline__ void bm2_segment(const Bm2Args &a_in, uint8_t *smem, 
                 }
             }
         }
-        if constexpr (LDSD) {
-            // ---- right-view winners from the finished tile (SSD LR pass) ----
-            // Right pixel xr collects keys (C << s | d) from the tile entries (k, d) with
-            // x0 + k - m - d = xr, a diagonal of the tile.  Lane i follows the wrapped diagonal
-            // (k, (k + i) mod Dp), k = 0..TX-1 (consecutive lanes, consecutive banks): part A, d = k + i
-            // < Dp, belongs to xr = x0 - m - i; part B, the wrapped rest (k >= L = Dp - i, d = k - L),
-            // to xr = x0 - m + L.  Only the wave holding i > Dp - TX has B parts; it splits its lanes
-            // by exec masks, and the role rotates over the waves row by row.  Keys carry k in the low
-            // bits while minimising (same order as d along one diagonal) and d on the way out.
-            const int ks = a.kshift;
-            int wi = wv + (y % NW);
-            wi = wi >= NW ? wi - NW : wi;
-            const int i = wi * 64 + ln, L = Dp - i;
-            constexpr int DS = PITCH + 4;  // one pixel and one disparity further
-            const uint8_t *pa = tile + 4 * i, *pb = pa - 4 * Dp;
-            uint32_t A = 0xFFFFFFFFu, B = 0xFFFFFFFFu;
-            if constexpr (LRFULL) {
-                // 8 entries per group: bounded reads in flight (the row loop is at its VGPR budget)
-                if (__builtin_amdgcn_readfirstlane(wi) != NW - 1) {
-                    static_for<TX / 8>([&](auto g) __attribute__((always_inline)) {
-                        constexpr int k0 = 8 * decltype(g)::value;
-#pragma unroll
-                        for (int k = k0; k < k0 + 8; ++k)
-                            A = umin2(A, (*reinterpret_cast<const uint32_t *>(pa + k * DS) << ks) | (uint32_t)k);
-                        __builtin_amdgcn_sched_barrier(0);
-                    });
-                } else {
-                    // lanes ln < 64 - k are still on part A (L > k)
-                    static_for<TX>([&](auto kc) __attribute__((always_inline)) {
-                        constexpr int k = decltype(kc)::value;
-                        const uint32_t ca = *reinterpret_cast<const uint32_t *>(pa + k * DS);
-                        const uint32_t cb = *reinterpret_cast<const uint32_t *>(pb + k * DS);
-                        min_split<k>(A, B, (ca << ks) | (uint32_t)k, (cb << ks) | (uint32_t)k);
-                        if constexpr ((k & 7) == 7) __builtin_amdgcn_sched_barrier(0);
-                    });
-                }
-            } else {
-                // partial strip or D < Dp: per-entry bounds (x0 + k < W, d < D)
-                const int nA = min(min(L, D - i), W - x0);
-                const int bE = min(W - x0, D + L);
-                for (int k = 0; k < TX; ++k) {
-                    const uint32_t ca = *reinterpret_cast<const uint32_t *>(pa + k * DS);
-                    const uint32_t cb = *reinterpret_cast<const uint32_t *>(pb + k * DS);
-                    if (k < nA) A = umin2(A, (ca << ks) | (uint32_t)k);
-                    if (k >= L && k < bE) B = umin2(B, (cb << ks) | (uint32_t)k);
-                }
-            }
-            uint32_t *krow = a.lr_keys + fout + (long)y * W;
-            const int xa = x0 - m - i, xb = x0 - m + L;
-            if (A != 0xFFFFFFFFu && xa >= 0 && xa < W) atomicMin(krow + xa, A + (uint32_t)i);
-            if (B != 0xFFFFFFFFu && xb >= 0 && xb < W) atomicMin(krow + xb, B - (uint32_t)L);
-        }
         DSX_STAMP(5);
         if (more) {
             st(par ^ 2, pn0, pn1, pn2, pn3, pnr);
@@ -1154,7 +986,7 @@ __device__ __forceinline__ void bm2_segment(const Bm2Args &a_in, uint8_t *smem, 
 }
 
 template <int R, bool SSD, int NW, int SIDE, bool ABS>
-__global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu((SSD && NW >= 4) ? DSX_WPE_SSD : DSX_WPE))) void bm2(Bm2Args a) {
+__global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu((SSD && NW >= 4) ? kWpeSsd : kWpe))) void bm2(Bm2Args a) {
     using G = Geo<R, SSD, NW>;
     constexpr int TX = G::TX, NT = G::NT, NC = G::NC, NJ = G::NJ;
     constexpr int side = SIDE;
@@ -1319,8 +1151,7 @@ template <int R, bool SSD, int NW, int SIDE, bool ABS = false>
 static hipError_t launch_bm2_side(const Bm2Args &a, hipStream_t st) {
     using G = Geo<R, SSD, NW>;
     // + the LR exit region; the LDS-diagonal SSD LR pass reads up to TX * 4 - 24 B past the tile
-    constexpr bool LDSD = SIDE == 3 && SSD && !ABS && NW >= 2 && DSX_SSD_LDSDIAG;
-    constexpr int SM = G::SMEM + ((SIDE == 3 && (SSD ? DSX_SSD_XB : DSX_XB4)) ? G::XRB * NW : 0) + (LDSD ? 128 : 0);
+    constexpr int SM = G::SMEM + ((SIDE == 3 && !SSD) ? G::XRB * NW : 0);
     const void *fn = (const void *)bm2<R, SSD, NW, SIDE, ABS>;
     static int blocks_per_cu[64] = {};
     static int num_cu[64] = {};

@@ -136,3 +136,30 @@ def test_lr_handle_on_alternating_streams(torch_dev):
     for i in range(12):
         _assert_same(outs[i].cpu().numpy(), refs[i % 3], f"call {i}")
     m.close()
+
+
+@pytest.mark.parametrize("name,checks", [("c2", False), ("c2", True), ("c4", False), ("c3", False)])
+def test_in_flight_handles_at_stated_size(torch_dev, cref, name, checks):
+    """Handles with dsx_params.in_flight (the bench's timed lanes and DepthPipeline's per-stream
+    handles: the grid partition drops the lone-frame balance) at the config's full size, three of
+    them with frames overlapping on three streams, every output against the oracle (VERDICT r4
+    item 4)."""
+    torch = torch_dev
+    from depthestimation_amd.matcher import HipBlockMatcher
+    over = REFERENCE_CHECKS if checks else {}
+    kw = matcher_kwargs(CONFIGS[name], **over)
+    L, R = _frame(name)
+    want = _ref(cref, name, **over)
+    H, W = L.shape
+    dL, dR = torch.from_numpy(L).cuda(), torch.from_numpy(R).cuda()
+    handles = [HipBlockMatcher(in_flight=True, **kw) for _ in range(3)]
+    streams = [torch.cuda.Stream() for _ in range(3)]
+    outs = [torch.empty((H, W), dtype=torch.int16, device="cuda") for _ in range(6)]
+    torch.cuda.synchronize()
+    for i in range(6):
+        handles[i % 3].compute_device(dL, dR, out_fixed=outs[i], stream=streams[i % 3])
+    torch.cuda.synchronize()
+    for i in range(6):
+        _assert_same(outs[i].cpu().numpy(), want, f"{name} in_flight handle {i % 3} call {i // 3}")
+    for h in handles:
+        h.close()
