@@ -14,12 +14,13 @@
 //   SWEEP 0  each child picks its parent (the pop neighbour with the least pop key (T, T_parent, root
 //            seed, direction, raster)), stores its fill key (the parent's pop key + its direction) and
 //            computes T / value from the pixels filled before the bucket;
-//   SWEEP i  each child recomputes from the pre-bucket pixels and the bucket's children with a
-//            smaller fill key - a DAG, so the fixed point is unique: sweeps repeat until one changes no
-//            bit.  A child recomputes only when a child it reads changed in the previous sweep (the
-//            per-pixel stamp of its last change), so late sweeps touch few pixels.  Updates are in
-//            place (a child may read a neighbour's value of this sweep or the last): the fixed point
-//            is the same, and a sweep without a change proves it.
+//   SWEEP 1  each child recomputes from the pre-bucket pixels and the bucket's children with a
+//            smaller fill key - a DAG, so the fixed point is unique - and caches which cells of its
+//            disc those are (a bit mask per window row);
+//   SWEEP i  only the children queued by the last sweep recompute: a child whose T or value changed
+//            queues the bucket's children that read it.  Updates are in place (a child may read a
+//            neighbour's value of this sweep or the last): the fixed point is the same, and a sweep
+//            that changes no bit (queues nothing) proves it.
 // The steps are launches of one kernel, `tl_step`, that reads a small state machine the previous step
 // left in the workspace (triple-buffered by step index: step s reads slot s%3, accumulates into
 // (s+1)%3 and clears (s+2)%3) and does the next POP or sweep; the host enqueues the step count the
@@ -51,15 +52,16 @@ enum Phase : int { kPhInit = 0, kPhPop = 1, kPhSweep = 2, kPhDone = 3 };
 // One state slot (written by step s-1, read by step s).  Counters and minima are accumulated by the
 // blocks of the writing step; the rest is carried by block 0.
 struct alignas(128) State {
-    int phase, k, b, sweep, lsel, nF, nC, changed;
+    int phase, k, b, nb, sweep, lsel, nF, nC, nA;  // nb: buckets started; nA: children queued for the next sweep
     double bound;
-    unsigned long long minF, minC;  // bit patterns of non-negative doubles (monotone as integers)
+    unsigned long long minF;                      // bit patterns of non-negative doubles (monotone as integers)
 };
 struct Ctl {
     State st[3];
-    unsigned bar, pad0[31];  // grid-barrier arrival counter (own line)
-    unsigned gen, pad1[31];  // barrier generation (own line)
-    int tmo, pad2[31];       // barrier timed out: every block leaves
+    unsigned long long minC[3], pad3[13];  // min T over a bucket's children, slot = bucket ordinal % 3
+    unsigned bar, pad0[31];                // grid-barrier arrival counter (own line)
+    unsigned gen, pad1[31];                // barrier generation (own line)
+    int tmo, pad2[31];                     // barrier timed out: every block leaves
 };
 
 struct Args {
@@ -67,8 +69,10 @@ struct Args {
     int *fb;               // fill bucket: -1 known, kInside unfilled, b filled in bucket b
     double *T, *Tpar, *Tgp;
     unsigned long long *lowkey;  // root << 34 | dir(parent) << 32 | parent << 2 | dir(self)
-    int *stamp;            // sweep of the pixel's last change
-    int *F[2], *C[2];      // frontier (unpopped band) and children lists, ping-pong
+    int *pos;              // a child's position in its bucket's list
+    uint16_t *lessm;       // per position and window row: the row's cells that are children filled earlier
+    unsigned long long *queued;  // per position: (bucket ordinal << 32 | sweep) it was last queued for
+    int *F[2], *C[2], *A[2];  // frontier (unpopped band), children and active-children lists, ping-pong
     Ctl *ctl;
     int *host;             // mapped host words of this workspace (nullable)
     int H, W, radius;
@@ -118,11 +122,8 @@ __global__ __launch_bounds__(256) void tl_init(const float *in, int64_t pitch, A
     const int H = a.H, W = a.W;
     const int64_t n = (int64_t)H * W;
     State &s0 = a.ctl->st[0];
-    if (blockIdx.x == 0 && threadIdx.x < 2) {
-        State &s = a.ctl->st[1 + threadIdx.x];
-        s.minF = ~0ull;
-        s.minC = ~0ull;
-    }
+    if (blockIdx.x == 0 && threadIdx.x < 2) a.ctl->st[1 + threadIdx.x].minF = ~0ull;
+    if (blockIdx.x == 0 && threadIdx.x < 3) a.ctl->minC[threadIdx.x] = ~0ull;
     for (int64_t p0 = (int64_t)blockIdx.x * 256; p0 < n; p0 += (int64_t)gridDim.x * 256) {  // block-uniform
         const int64_t p = p0 + threadIdx.x;
         bool seed = false;
@@ -155,30 +156,39 @@ __global__ __launch_bounds__(256) void tl_init(const float *in, int64_t pitch, A
 
 struct Mode {
     int what;  // kPhPop, kPhSweep, kPhDone
-    int k, b, sweep, lsel, nIn, nPrev;
+    int k, b, nb, sweep, lsel;
+    int nIn;    // POP: survivors; sweeps: list length (the bucket's children, or the active list)
+    int nPrev;  // POP: the last bucket's children
+    bool full;  // sweep over the bucket's whole list (positions 0..nIn), else over the active list
     double bound;
 };
 
 // The step's mode from the slot the previous step wrote (every block computes the same).
-__device__ __forceinline__ Mode decide(const State &S) {
+template <int G>
+__device__ __forceinline__ Mode decide(const State &S, const Ctl *ctl) {
     Mode m{};
     m.k = S.k;
     m.b = S.b;
+    m.nb = S.nb;
     m.lsel = S.lsel;
     m.bound = S.bound;
     if (S.phase == kPhDone) {
         m.what = kPhDone;
         return m;
     }
-    if (S.phase == kPhSweep && (S.sweep == 0 || S.changed > 0)) {
+    if (S.phase == kPhSweep && (S.sweep == 0 || S.nA > 0)) {
         m.what = kPhSweep;
         m.sweep = S.sweep + 1;
-        m.nIn = S.nC;
+        // sweep 1 runs over every child (their dependency masks are built there); later sweeps over the
+        // children queued by the last one (G = 0: every child again, nA counts the changed blocks)
+        m.full = G == 0 || m.sweep == 1;
+        m.nIn = m.full ? S.nC : S.nA;
         return m;
     }
-    if (S.phase == kPhPop && S.nC > 0) {
+    if (S.phase == kPhPop && S.nC > 0) {  // the POP ran sweep 0 of its children
         m.what = kPhSweep;
-        m.sweep = 0;
+        m.sweep = 1;
+        m.full = true;
         m.nIn = S.nC;
         return m;
     }
@@ -192,13 +202,17 @@ __device__ __forceinline__ Mode decide(const State &S) {
         return m;
     }
     unsigned long long mn = S.minF;
-    if (after_sweep && S.minC < mn) mn = S.minC;
+    if (after_sweep) {
+        const unsigned long long mc = __hip_atomic_load(&ctl->minC[S.nb % 3], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        mn = mc < mn ? mc : mn;
+    }
     const int kf = (int)floor(bitsd(mn) / kDelta);
     const int kn = S.k > kf ? S.k : kf;
     m.what = kPhPop;
     m.bound = (double)(kn + 1) * kDelta;
     m.k = kn + 1;
     m.b = kn + 1;
+    m.nb = S.nb + 1;
     return m;
 }
 
@@ -221,44 +235,17 @@ __device__ __forceinline__ unsigned long long wave_min_u64(unsigned long long v)
     return v;
 }
 
-// POP: entries of F[lsel] (nIn) then C[lsel] (nPrev); T < bound pops (marks children), the rest
-// survives into F[lsel^1].  T of a known seed is 0.
-__device__ void do_pop(const Args &a, const Mode &m, State &N, int blk, int nblk) {
-    const int *Fi = a.F[m.lsel], *Ci = a.C[m.lsel];
-    int *Fo = a.F[m.lsel ^ 1], *Co = a.C[m.lsel ^ 1];
-    const int tot = m.nIn + m.nPrev;
-    const int W = a.W, H = a.H;
-    unsigned long long mn = ~0ull;
-    for (int base = blk * 256; base < tot; base += nblk * 256) {  // block-uniform trip count
-        const int i = base + (int)threadIdx.x;
-        bool keep = false;
-        int p = 0;
-        bool marks[4] = {false, false, false, false};
-        int kids[4] = {0, 0, 0, 0};
-        if (i < tot) {
-            p = i < m.nIn ? Fi[i] : Ci[i - m.nIn];
-            const double t = a.fb[p] < 0 ? 0.0 : a.T[p];
-            if (t < m.bound) {
-                const int y = p / W, x = p - y * W;
-                const int nb[4] = {y > 0 ? p - W : -1, x > 0 ? p - 1 : -1, y < H - 1 ? p + W : -1, x < W - 1 ? p + 1 : -1};
+// Wave-wide exclusive prefix sum of v (and the wave total).
+__device__ __forceinline__ int wave_excl_scan(int v, int &total) {
+    const int lane = threadIdx.x & 63;
+    int incl = v;
 #pragma unroll
-                for (int d = 0; d < 4; ++d) {
-                    if (nb[d] >= 0 && a.fb[nb[d]] == kInside) {
-                        marks[d] = atomicCAS(&a.fb[nb[d]], kInside, m.b) == kInside;
-                        kids[d] = nb[d];
-                    }
-                }
-            } else {
-                keep = true;
-                mn = dbits(t);
-            }
-        }
-        wave_append(keep, Fo, &N.nF, p);
-#pragma unroll
-        for (int d = 0; d < 4; ++d) wave_append(marks[d], Co, &N.nC, kids[d]);
+    for (int o = 1; o < 64; o <<= 1) {
+        const int u = __shfl_up(incl, o);
+        incl += lane >= o ? u : 0;
     }
-    mn = wave_min_u64(mn);
-    if ((threadIdx.x & 63) == 0 && mn != ~0ull) atomicMin(&N.minF, mn);
+    total = __shfl(incl, 63);
+    return incl - v;
 }
 
 // Pop key of a band pixel p (known seed or filled): (T, T_parent, root << 32 | dir << 30 | p).
@@ -270,12 +257,211 @@ __device__ __forceinline__ bool pop_less(const PopKey &a, const PopKey &b) {
     return a.t < b.t || (a.t == b.t && (a.tp < b.tp || (a.tp == b.tp && a.lo < b.lo)));
 }
 
-// One child (group of G lanes, lane j = window row j - radius; G = 0: one thread does every row).
-// Returns (via lane 0 / the thread) whether T or the value changed, and the child's T.
+// Sweep 0: child c's parent - the pop neighbour with the least pop key (a band neighbour below the
+// bound is a pop of this bucket: one popped earlier would have filled c then) - and its fill key.
+// Branch-free: only the least key is carried through the candidates; the parent's raster index is
+// the key's low 30 bits (kInpaintMaxPixels) and the direction follows from it.
+__device__ __forceinline__ Key parent_key(const Args &a, const Mode &m, int c, const int (&nbp)[4]) {
+    // every neighbour's words load at once (clamped to c), then the candidates are picked
+    int fn[4];
+    double tn[4], tpn[4];
+    unsigned long long lkn[4];
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+        const int p = nbp[d] >= 0 ? nbp[d] : c;
+        fn[d] = a.fb[p];
+        tn[d] = a.T[p];
+        tpn[d] = a.Tpar[p];
+        lkn[d] = a.lowkey[p];
+    }
+    PopKey best{0.0, 0.0, ~0ull};
+    bool have = false;
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+        const int p = nbp[d];
+        const int f = fn[d];
+        const bool known = f < 0;
+        PopKey k;
+        k.t = known ? 0.0 : tn[d];
+        k.tp = known ? -1.0 : tpn[d];
+        const unsigned long long proot = known ? (unsigned long long)(unsigned)p : lkn[d] >> 34;
+        const unsigned long long pdir = known ? 0ull : (lkn[d] & 3ull);
+        k.lo = proot << 32 | pdir << 30 | (unsigned long long)(unsigned)p;
+        const bool cand = p >= 0 && f < m.b && k.t < m.bound;
+        const bool take = cand && (!have || pop_less(k, best));
+        best.t = take ? k.t : best.t;
+        best.tp = take ? k.tp : best.tp;
+        best.lo = take ? k.lo : best.lo;
+        have = have || cand;
+    }
+    const int bp = (int)(best.lo & ((1ull << 30) - 1ull));
+    // direction from the parent to the child (up, left, down, right): parent above -> down, ...
+    const int W = a.W;
+    const int dirc = bp == c - W ? 2 : (bp == c + W ? 0 : (bp == c - 1 ? 3 : 1));
+    Key me;
+    me.tp = best.t;
+    me.tg = best.tp;
+    const unsigned long long root = best.lo >> 32, pdir = (best.lo >> 30) & 3;
+    me.lo = root << 34 | pdir << 32 | (unsigned long long)(unsigned)bp << 2 | (unsigned long long)dirc;
+    return me;
+}
+
+// One child with G lanes (lane j = window row j - radius; G = 8 up to radius 3, 16 up to 7): the
+// row's cells load at once (clamped addresses, masked afterwards), availability comes from the fill
+// bucket (before this bucket) and the cached `lessm` row mask (this bucket's children filled earlier,
+// built in sweep 1 from the fill keys), the 4-neighbours' T from the centre rows by shuffles.
+// Returns (lane 0) whether T or the value changed, and the child's T.
 template <int G>
-__device__ __forceinline__ void sweep_child(const Args &a, const Mode &m, int c, bool &changed, double &tc) {
-    constexpr int RM = G > 0 ? (G - 2) / 2 : 0;  // widest radius of the group form: 3 (G 8), 7 (G 16)
-    const int j = G > 0 ? (int)(threadIdx.x & (G - 1)) : 0;
+struct Cells {
+    static constexpr int RM = (G - 2) / 2;  // widest radius of the group form: 3 (G 8), 7 (G 16)
+    static constexpr int NCELL = 2 * RM + 1;
+};
+
+template <int G>
+__device__ __forceinline__ void sweep_child(const Args &a, const Mode &m, int i, int c, double &tc, uint32_t &won,
+                                            int (&pq)[Cells<G>::NCELL]) {
+    constexpr int RM = Cells<G>::RM;
+    constexpr int NCELL = Cells<G>::NCELL;
+    const int j = (int)(threadIdx.x & (G - 1));
+    const int H = a.H, W = a.W, radius = a.radius, r2 = radius * radius;
+    const int y = c / W, x = c - y * W;
+    const int b = m.b, sweep = m.sweep;
+    const int oy = j - radius, qy = y + oy;
+    const bool rowin = j <= 2 * radius && qy >= 0 && qy < H;
+    const int64_t rowq = (int64_t)(rowin ? qy : y) * W;
+
+    Key me{0, 0, 0};
+    if (sweep == 0) {
+        const int nbp[4] = {y > 0 ? c - W : -1, x > 0 ? c - 1 : -1, y < H - 1 ? c + W : -1, x < W - 1 ? c + 1 : -1};
+        me = parent_key(a, m, c, nbp);
+        if (j == 0) {
+            a.Tpar[c] = me.tp;
+            a.Tgp[c] = me.tg;
+            a.lowkey[c] = me.lo;
+            a.pos[c] = i;
+            a.queued[i] = 0;
+        }
+    } else if (sweep == 1) {
+        me = load_key(a, c);
+    }
+    const double Told = a.T[c];
+    const float vold = a.out[c];
+    uint32_t less = sweep >= 2 ? a.lessm[(int64_t)i * G + j] : 0u;
+
+    // the row's cells: fill bucket, T, value (and the fill keys in sweep 1), all loads in flight
+    int fq[NCELL];
+    double tq[NCELL];
+    float vq[NCELL];
+    uint32_t inw = 0;  // cells inside the disc and the image
+#pragma unroll
+    for (int cc = 0; cc < NCELL; ++cc) {
+        const int ox = cc - RM, qx = x + ox;
+        const int d2 = oy * oy + ox * ox;
+        const bool ok = rowin && qx >= 0 && qx < W && d2 > 0 && d2 <= r2;
+        const int64_t q = rowq + (qx < 0 ? 0 : (qx >= W ? W - 1 : qx));
+        fq[cc] = a.fb[q];
+        tq[cc] = a.T[q];
+        vq[cc] = a.out[q];
+        inw |= (uint32_t)ok << cc;
+    }
+    // the centre cell (ox = 0, oy = 0) is outside the disc: d2 = 0
+    if (sweep == 1) {
+        Key kq[NCELL];
+#pragma unroll
+        for (int cc = 0; cc < NCELL; ++cc) {
+            const int ox = cc - RM, qx = x + ox;
+            const int64_t q = rowq + (qx < 0 ? 0 : (qx >= W ? W - 1 : qx));
+            kq[cc] = load_key(a, q);
+        }
+#pragma unroll
+        for (int cc = 0; cc < NCELL; ++cc)
+            if (((inw >> cc) & 1u) && fq[cc] == b && key_less(kq[cc], me)) less |= 1u << cc;
+        a.lessm[(int64_t)i * G + j] = (uint16_t)less;
+    }
+    uint32_t avail = 0, intra = 0;
+#pragma unroll
+    for (int cc = 0; cc < NCELL; ++cc) {
+        const bool in = (inw >> cc) & 1u;
+        avail |= (uint32_t)(in && (fq[cc] < b || (fq[cc] == b && ((less >> cc) & 1u)))) << cc;
+        intra |= (uint32_t)(in && fq[cc] == b) << cc;
+        if (fq[cc] < 0) tq[cc] = 0.0;  // known pixels: T = 0 (not stored)
+    }
+    tc = Told;
+    // sweep 1: a child with no earlier child in its disc keeps its sweep-0 result
+    if (sweep == 1) {
+        int any = less != 0;
+#pragma unroll
+        for (int o = 1; o < G; o <<= 1) {
+            const int other = __shfl_xor(any, o, G);  // every lane takes part: no short circuit
+            any = any | other;
+        }
+        if (!any) return;
+    }
+
+    // ---- T and grad T from the 4-neighbours (centre rows), shuffled from the lanes that hold them ----
+    const int lc = radius;  // lane of the centre row
+    const double tcm = (avail >> RM) & 1u ? tq[RM] : 1e6;
+    const double tcl = (avail >> (RM - 1)) & 1u ? tq[RM - 1] : 1e6;
+    const double tcr = (avail >> (RM + 1)) & 1u ? tq[RM + 1] : 1e6;
+    const double tu = __shfl(tcm, lc - 1, G), tdn = __shfl(tcm, lc + 1, G);
+    const double tl = __shfl(tcl, lc, G), tr = __shfl(tcr, lc, G);
+    const bool ou = tu < 1e6, od = tdn < 1e6, ol = tl < 1e6, orr = tr < 1e6;
+    const double ta = telea_solve(tu, tl), tb = telea_solve(tdn, tl);
+    const double tc2 = telea_solve(tu, tr), td = telea_solve(tdn, tr);
+    const double m01 = ta < tb ? ta : tb, m23 = tc2 < td ? tc2 : td;
+    const double tp = m01 < m23 ? m01 : m23;
+    const double gx = (orr && ol) ? (tr - tl) * 0.5 : (orr ? tr - tp : (ol ? tp - tl : 0.0));
+    const double gy = (od && ou) ? (tdn - tu) * 0.5 : (od ? tdn - tp : (ou ? tp - tu : 0.0));
+
+    double rn = 0.0, rd = 0.0;
+#pragma unroll
+    for (int cc = 0; cc < NCELL; ++cc) {
+        const int ox = cc - RM;
+        const int d2 = oy * oy + ox * ox;
+        const double ry = (double)(-oy), rx = (double)(-ox);
+        const double w_dir = __builtin_fabs(ry * gy + rx * gx) / __builtin_sqrt((double)(d2 > 0 ? d2 : 1));
+        const double w_dst = 1.0 / (double)(d2 > 0 ? d2 : 1);
+        const double w_lev = 1.0 / (1.0 + __builtin_fabs(tq[cc] - tp));
+        double w = w_dir * w_dst * w_lev;
+        w = w > 1e-6 ? w : 1e-6;
+        const bool use = (avail >> cc) & 1u;
+        rn = use ? rn + w * (double)vq[cc] : rn;
+        rd = use ? rd + w : rd;
+    }
+    double num = 0.0, den = 0.0;
+#pragma unroll
+    for (int q = 0; q < G; ++q) {  // rows past 2 radius add +0.0: exact
+        num = num + __shfl(rn, q, G);
+        den = den + __shfl(rd, q, G);
+    }
+    const float v = den > 0 ? (float)(num / den) : vold;
+    tc = tp;
+    const bool changed = sweep == 0 || __double_as_longlong(tp) != __double_as_longlong(Told) ||
+                         __float_as_int(v) != __float_as_int(vold);
+    if (!changed) return;
+    if (j == 0) {
+        a.T[c] = tp;
+        a.out[c] = v;
+    }
+    if (sweep == 0) return;  // sweep 1 visits every child anyway
+    // the children that read this one (this bucket's, filled later) go to the next sweep's list: a
+    // per-position tag keeps each once; the caller appends them with one counter add per wave
+    const uint32_t dep = intra & ~less;
+    const unsigned long long tag = (unsigned long long)m.nb << 32 | (unsigned)(sweep + 1);
+#pragma unroll
+    for (int cc = 0; cc < NCELL; ++cc) {
+        if ((dep >> cc) & 1u) {
+            const int qx = x + cc - RM;
+            const int p = a.pos[rowq + qx];
+            pq[cc] = p;
+            if (atomicMax(&a.queued[p], tag) < tag) won |= 1u << cc;
+        }
+    }
+}
+
+// Radii above 7: one thread per child, every row; availability from the fill keys each sweep and
+// every child in every sweep (nA counts the blocks that changed something).
+__device__ __forceinline__ void sweep_child_wide(const Args &a, const Mode &m, int i, int c, bool &changed, double &tc) {
     const int H = a.H, W = a.W, radius = a.radius, r2 = radius * radius;
     const int y = c / W, x = c - y * W;
     const int b = m.b;
@@ -283,65 +469,18 @@ __device__ __forceinline__ void sweep_child(const Args &a, const Mode &m, int c,
     const int nbp[4] = {y > 0 ? c - W : -1, x > 0 ? c - 1 : -1, y < H - 1 ? c + W : -1, x < W - 1 ? c + 1 : -1};
     Key me;
     if (first) {
-        // the parent: the pop neighbour with the least pop key (any band neighbour below the bound is
-        // a pop of this bucket: one popped earlier would have filled c then)
-        PopKey best{0, 0, 0};
-        int bp = -1, bd = 0;
-#pragma unroll
-        for (int d = 0; d < 4; ++d) {
-            const int p = nbp[d];
-            if (p < 0) continue;
-            const int f = a.fb[p];
-            if (f >= b) continue;
-            PopKey k;
-            int pdir;
-            unsigned long long proot;
-            if (f < 0) {
-                k.t = 0.0;
-                k.tp = -1.0;
-                proot = (unsigned long long)p;
-                pdir = 0;
-            } else {
-                k.t = a.T[p];
-                k.tp = a.Tpar[p];
-                const unsigned long long lk = a.lowkey[p];
-                proot = lk >> 34;
-                pdir = (int)(lk & 3);
-            }
-            if (!(k.t < m.bound)) continue;
-            k.lo = proot << 32 | (unsigned long long)pdir << 30 | (unsigned long long)p;
-            if (bp < 0 || pop_less(k, best)) {
-                best = k;
-                bp = p;
-                bd = d;
-            }
-        }
-        // direction from the parent to the child (up, left, down, right): parent above -> down, ...
-        const int dirc = bd ^ 2;
-        me.tp = best.t;
-        me.tg = best.tp;
-        const unsigned long long root = best.lo >> 32, pdir = (best.lo >> 30) & 3;
-        me.lo = root << 34 | pdir << 32 | (unsigned long long)bp << 2 | (unsigned long long)dirc;
-        if (j == 0) {
-            a.Tpar[c] = me.tp;
-            a.Tgp[c] = me.tg;
-            a.lowkey[c] = me.lo;
-        }
+        me = parent_key(a, m, c, nbp);
+        a.Tpar[c] = me.tp;
+        a.Tgp[c] = me.tg;
+        a.lowkey[c] = me.lo;
+        a.pos[c] = i;
     } else {
         me = load_key(a, c);
     }
-
-    // ---- does anything this child reads change? (sweeps >= 1; a child of no intra-bucket pixel is
-    // settled after sweep 0) ----
     const double Told = a.T[c];
     const float vold = a.out[c];
-    tc = Told;
-    changed = false;
-
-    // ---- T and grad T from the 4-neighbours filled before this child ----
     double tn[4];
     bool on[4];
-    bool need = first;
 #pragma unroll
     for (int d = 0; d < 4; ++d) {
         const int p = nbp[d];
@@ -352,53 +491,8 @@ __device__ __forceinline__ void sweep_child(const Args &a, const Mode &m, int c,
         if (filled_before(a, p, f, b, !first, me)) {
             on[d] = true;
             tn[d] = f < 0 ? 0.0 : a.T[p];
-            if (f == b && a.stamp[p] >= m.sweep - 1) need = true;
         }
     }
-
-    // ---- the disc rows ----
-    constexpr int NCELL = 2 * RM + 1;
-    const int row0 = G > 0 ? j - radius : -radius, row1 = G > 0 ? j - radius : radius;
-    // group form: one row per lane, its cells in registers; G = 0: rows looped below
-    int fq[G > 0 ? NCELL : 1];
-    if constexpr (G > 0) {
-        const int oy = row0;
-        const int qy = y + oy;
-        const bool rowin = j <= 2 * radius && qy >= 0 && qy < H;
-#pragma unroll
-        for (int cc = 0; cc < NCELL; ++cc) {
-            const int ox = cc - RM, qx = x + ox;
-            const int d2 = oy * oy + ox * ox;
-            fq[cc] = kInside;
-            if (rowin && qx >= 0 && qx < W && d2 > 0 && d2 <= r2) {
-                const int64_t q = (int64_t)qy * W + qx;
-                const int f = a.fb[q];
-                if (filled_before(a, q, f, b, !first, me)) {
-                    fq[cc] = f;
-                    if (f == b && a.stamp[q] >= m.sweep - 1) need = true;
-                }
-            }
-        }
-    } else {
-        for (int oy = -radius; oy <= radius && !need; ++oy)
-            for (int ox = -radius; ox <= radius; ++ox) {
-                const int qy = y + oy, qx = x + ox, d2 = oy * oy + ox * ox;
-                if (d2 == 0 || d2 > r2 || qy < 0 || qy >= H || qx < 0 || qx >= W) continue;
-                const int64_t q = (int64_t)qy * W + qx;
-                const int f = a.fb[q];
-                if (f == b && filled_before(a, q, f, b, !first, me) && a.stamp[q] >= m.sweep - 1) need = true;
-            }
-    }
-    if constexpr (G > 0) {
-        // group-uniform decision
-#pragma unroll
-        for (int o = 1; o < G; o <<= 1) {
-            const int other = __shfl_xor((int)need, o, G);  // every lane must take part: no short circuit
-            need = need || other != 0;
-        }
-    }
-    if (!need) return;
-
     const double ta = telea_solve(tn[0], tn[1]), tb = telea_solve(tn[2], tn[1]);
     const double tc2 = telea_solve(tn[0], tn[3]), td = telea_solve(tn[2], tn[3]);
     const double m01 = ta < tb ? ta : tb, m23 = tc2 < td ? tc2 : td;
@@ -407,83 +501,195 @@ __device__ __forceinline__ void sweep_child(const Args &a, const Mode &m, int c,
     const double tu = tn[0], tl = tn[1], tdn = tn[2], tr = tn[3];
     const double gx = (orr && ol) ? (tr - tl) * 0.5 : (orr ? tr - tp : (ol ? tp - tl : 0.0));
     const double gy = (od && ou) ? (tdn - tu) * 0.5 : (od ? tdn - tp : (ou ? tp - tu : 0.0));
-
-    auto weight = [&](int oy, int ox, double Tq) {
-        const int d2 = oy * oy + ox * ox;
-        const double ry = (double)(-oy), rx = (double)(-ox);
-        const double w_dir = __builtin_fabs(ry * gy + rx * gx) / __builtin_sqrt((double)d2);
-        const double w_dst = 1.0 / (double)d2;
-        const double w_lev = 1.0 / (1.0 + __builtin_fabs(Tq - tp));
-        double w = w_dir * w_dst * w_lev;
-        return w > 1e-6 ? w : 1e-6;
-    };
     double num = 0.0, den = 0.0;
-    if constexpr (G > 0) {
+    for (int oy = -radius; oy <= radius; ++oy) {
         double rn = 0.0, rd = 0.0;
-        const int oy = row0;
-        const int64_t rowq = (int64_t)(y + oy) * W;
-#pragma unroll
-        for (int cc = 0; cc < NCELL; ++cc) {
-            if (fq[cc] == kInside) continue;
-            const int64_t q = rowq + x + cc - RM;
-            const double Tq = fq[cc] < 0 ? 0.0 : a.T[q];
-            const double w = weight(oy, cc - RM, Tq);
+        for (int ox = -radius; ox <= radius; ++ox) {
+            const int qy = y + oy, qx = x + ox, d2 = oy * oy + ox * ox;
+            if (d2 == 0 || d2 > r2 || qy < 0 || qy >= H || qx < 0 || qx >= W) continue;
+            const int64_t q = (int64_t)qy * W + qx;
+            const int f = a.fb[q];
+            if (!filled_before(a, q, f, b, !first, me)) continue;
+            const double Tq = f < 0 ? 0.0 : a.T[q];
+            const double ry = (double)(-oy), rx = (double)(-ox);
+            const double w_dir = __builtin_fabs(ry * gy + rx * gx) / __builtin_sqrt((double)d2);
+            const double w_dst = 1.0 / (double)d2;
+            const double w_lev = 1.0 / (1.0 + __builtin_fabs(Tq - tp));
+            double w = w_dir * w_dst * w_lev;
+            w = w > 1e-6 ? w : 1e-6;
             rn = rn + w * (double)a.out[q];
             rd = rd + w;
         }
-        (void)row1;
-#pragma unroll
-        for (int q = 0; q < G; ++q) {  // rows past 2 radius add +0.0: exact
-            num = num + __shfl(rn, q, G);
-            den = den + __shfl(rd, q, G);
-        }
-    } else {
-        for (int oy = -radius; oy <= radius; ++oy) {
-            double rn = 0.0, rd = 0.0;
-            for (int ox = -radius; ox <= radius; ++ox) {
-                const int qy = y + oy, qx = x + ox, d2 = oy * oy + ox * ox;
-                if (d2 == 0 || d2 > r2 || qy < 0 || qy >= H || qx < 0 || qx >= W) continue;
-                const int64_t q = (int64_t)qy * W + qx;
-                const int f = a.fb[q];
-                if (!filled_before(a, q, f, b, !first, me)) continue;
-                const double w = weight(oy, ox, f < 0 ? 0.0 : a.T[q]);
-                rn = rn + w * (double)a.out[q];
-                rd = rd + w;
-            }
-            num = num + rn;
-            den = den + rd;
-        }
+        num = num + rn;
+        den = den + rd;
     }
     const float v = den > 0 ? (float)(num / den) : vold;
     tc = tp;
     changed = first || __double_as_longlong(tp) != __double_as_longlong(Told) || __float_as_int(v) != __float_as_int(vold);
-    if (changed && j == 0) {
+    if (changed) {
         a.T[c] = tp;
         a.out[c] = v;
-        a.stamp[c] = m.sweep;
     }
+}
+
+// POP: entries of F[lsel] (nIn) then C[lsel] (nPrev); T < bound pops (marks children), the rest
+// survives into F[lsel^1].  T of a known seed is 0.  The children a block marks get their list
+// positions with one counter add per block round and run sweep 0 right there (their parent and fill
+// key, T and value from the pixels filled before the bucket): the pops, and so every child's parent,
+// are fixed for the whole step, and sweep 0 reads no child of the bucket.
+template <int G>
+__device__ void do_pop(const Args &a, const Mode &m, State &N, int blk, int nblk) {
+    const int *Fi = a.F[m.lsel], *Ci = a.C[m.lsel];
+    int *Fo = a.F[m.lsel ^ 1], *Co = a.C[m.lsel ^ 1];
+    const int tot = m.nIn + m.nPrev;
+    const int W = a.W, H = a.H;
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    __shared__ int kidc[1024], kidi[1024];
+    __shared__ int wsum[4], kbase;
+    Mode m0 = m;
+    m0.what = kPhSweep;
+    m0.sweep = 0;
+    unsigned long long mn = ~0ull, mnc = ~0ull;
+    for (int base = blk * 256; base < tot; base += nblk * 256) {  // block-uniform trip count
+        const int i = base + (int)threadIdx.x;
+        int keep = 0, p = 0;
+        unsigned km = 0;  // the directions whose neighbour this pop marked (no dynamic register index)
+        int nb[4] = {-1, -1, -1, -1};
+        if (i < tot) {
+            p = i < m.nIn ? Fi[i] : Ci[i - m.nIn];
+            const int y = p / W, x = p - y * W;
+            nb[0] = y > 0 ? p - W : -1;
+            nb[1] = x > 0 ? p - 1 : -1;
+            nb[2] = y < H - 1 ? p + W : -1;
+            nb[3] = x < W - 1 ? p + 1 : -1;
+            int fn[4];
+#pragma unroll
+            for (int d = 0; d < 4; ++d) fn[d] = a.fb[nb[d] >= 0 ? nb[d] : p];
+            const double t = a.fb[p] < 0 ? 0.0 : a.T[p];
+            if (t < m.bound) {
+#pragma unroll
+                for (int d = 0; d < 4; ++d) {
+                    if (nb[d] >= 0 && fn[d] == kInside && atomicCAS(&a.fb[nb[d]], kInside, m.b) == kInside)
+                        km |= 1u << d;
+                }
+            } else {
+                keep = 1;
+                mn = dbits(t);
+            }
+        }
+        // survivors: one counter add per wave
+        int tf;
+        const int ef = wave_excl_scan(keep, tf);
+        int bf = 0;
+        if (lane == 0 && tf) bf = atomicAdd(&N.nF, tf);
+        bf = __shfl(bf, 0);
+        if (keep) Fo[bf + ef] = p;
+        // children: block-wide positions (one counter add), staged in LDS for sweep 0
+        int tk;
+        const int ek = wave_excl_scan(__popc(km), tk);
+        if (lane == 0) wsum[wv] = tk;
+        __syncthreads();
+        int woff = 0, btot = 0;
+#pragma unroll
+        for (int w = 0; w < 4; ++w) {
+            woff += w < wv ? wsum[w] : 0;
+            btot += wsum[w];
+        }
+        if (threadIdx.x == 0) kbase = btot ? atomicAdd(&N.nC, btot) : 0;
+        __syncthreads();
+        const int gb = kbase;
+#pragma unroll
+        for (int d = 0; d < 4; ++d) {
+            if ((km >> d) & 1u) {
+                const int li = woff + ek + __popc(km & ((1u << d) - 1u));
+                Co[gb + li] = nb[d];
+                kidc[li] = nb[d];
+                kidi[li] = gb + li;
+            }
+        }
+        __syncthreads();
+        if constexpr (G > 0) {
+            constexpr int per = 256 / G;
+            const int g = (int)threadIdx.x / G;
+            for (int k = g; k < btot; k += per) {  // group-uniform
+                constexpr int NCELL = Cells<G>::NCELL;
+                uint32_t won = 0;
+                int pq[NCELL];
+                double tc;
+                sweep_child<G>(a, m0, kidi[k], kidc[k], tc, won, pq);
+                const unsigned long long tb = dbits(tc);
+                mnc = tb < mnc ? tb : mnc;
+            }
+        } else {
+            for (int k = threadIdx.x; k < btot; k += 256) {
+                bool ch;
+                double tc;
+                sweep_child_wide(a, m0, kidi[k], kidc[k], ch, tc);
+                const unsigned long long tb = dbits(tc);
+                mnc = tb < mnc ? tb : mnc;
+            }
+        }
+        __syncthreads();  // LDS list and wsum reused by the next round
+    }
+    mn = wave_min_u64(mn);
+    if (lane == 0 && mn != ~0ull) atomicMin(&N.minF, mn);
+    mnc = wave_min_u64(mnc);
+    if (lane == 0 && mnc != ~0ull) atomicMin(&a.ctl->minC[m.nb % 3], mnc);
 }
 
 template <int G>
 __device__ void do_sweep(const Args &a, const Mode &m, State &N, int blk, int nblk) {
     const int *Cl = a.C[m.lsel];
+    const int *Al = a.A[(m.sweep - 1) & 1];  // sweeps >= 2: the children the last sweep queued
+    int *Anext = a.A[m.sweep & 1];
     constexpr int per = G > 0 ? 256 / G : 256;
     const int g = G > 0 ? (int)threadIdx.x / G : (int)threadIdx.x;
-    bool any = false;
     unsigned long long mn = ~0ull;
-    for (int base = blk * per; base < m.nIn; base += nblk * per) {  // group-uniform
-        const int i = base + g;
-        if (i >= m.nIn) continue;
-        bool ch;
-        double t;
-        sweep_child<G>(a, m, Cl[i], ch, t);
-        any = any || ch;
-        const unsigned long long tb = dbits(t);
-        mn = tb < mn ? tb : mn;
+    bool any = false;
+    for (int base = blk * per; base < m.nIn; base += nblk * per) {  // block-uniform trip count
+        const int k = base + g;
+        const bool live = k < m.nIn;
+        if constexpr (G > 0) {
+            constexpr int NCELL = Cells<G>::NCELL;
+            uint32_t won = 0;
+            int pq[NCELL];
+            if (live) {  // group-uniform
+                const int i = m.full ? k : Al[k];
+                double t;
+                sweep_child<G>(a, m, i, Cl[i], t, won, pq);
+                const unsigned long long tb = dbits(t);
+                mn = tb < mn ? tb : mn;
+            }
+            // the queued children of the whole wave: one counter add
+            int tot;
+            const int ex = wave_excl_scan(__popc(won), tot);
+            if (tot) {
+                int base_q = 0;
+                if ((threadIdx.x & 63) == 0) base_q = atomicAdd(&N.nA, tot);
+                base_q = __shfl(base_q, 0) + ex;
+#pragma unroll
+                for (int cc = 0; cc < NCELL; ++cc)
+                    if ((won >> cc) & 1u) Anext[base_q + __popc(won & ((1u << cc) - 1u))] = pq[cc];
+            }
+        } else {
+            if (live) {
+                const int i = m.full ? k : Al[k];
+                bool ch;
+                double t;
+                sweep_child_wide(a, m, i, Cl[i], ch, t);
+                any = any || ch;
+                const unsigned long long tb = dbits(t);
+                mn = tb < mn ? tb : mn;
+            }
+        }
     }
-    if (__syncthreads_or(any) && threadIdx.x == 0) atomicAdd(&N.changed, 1);
+    if constexpr (G == 0) {
+        if (__syncthreads_or(any) && threadIdx.x == 0 && m.sweep > 0) atomicAdd(&N.nA, 1);
+    }
+    // T of a child only falls over the sweeps (more neighbours filled before it), so the minimum of
+    // every T computed in the bucket is the minimum of the final ones
     mn = wave_min_u64(mn);
-    if ((threadIdx.x & 63) == 0 && mn != ~0ull) atomicMin(&N.minC, mn);
+    if ((threadIdx.x & 63) == 0 && mn != ~0ull) atomicMin(&a.ctl->minC[m.nb % 3], mn);
 }
 
 // Step s: returns the mode it ran (kPhDone: the march had finished).
@@ -492,17 +698,17 @@ __device__ int step(const Args &a, unsigned s, int blk, int nblk) {
     Ctl *ctl = a.ctl;
     const State S = ctl->st[s % 3];
     State &N = ctl->st[(s + 1) % 3];
-    const Mode m = decide(S);
+    const Mode m = decide<G>(S, ctl);
     if (blk == 0 && threadIdx.x == 0) {
         State &Z = ctl->st[(s + 2) % 3];
         Z.nF = 0;
         Z.nC = 0;
-        Z.changed = 0;
+        Z.nA = 0;
         Z.minF = ~0ull;
-        Z.minC = ~0ull;
         N.phase = m.what;
         N.k = m.k;
         N.b = m.b;
+        N.nb = m.nb;
         N.sweep = m.sweep;
         N.bound = m.bound;
         if (m.what == kPhSweep) {  // carried: the POP's outputs
@@ -512,13 +718,15 @@ __device__ int step(const Args &a, unsigned s, int blk, int nblk) {
             N.minF = S.minF;
         } else if (m.what == kPhPop) {
             N.lsel = m.lsel ^ 1;
+            // the next bucket's accumulator (this step reads slot nb-1 and fills slot nb)
+            ctl->minC[(m.nb + 1) % 3] = ~0ull;
         } else {
             N.lsel = m.lsel;
             if (S.phase != kPhDone && a.host)
                 __hip_atomic_store(a.host + kHostSteps, (int)s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         }
     }
-    if (m.what == kPhPop) do_pop(a, m, N, blk, nblk);
+    if (m.what == kPhPop) do_pop<G>(a, m, N, blk, nblk);
     else if (m.what == kPhSweep) do_sweep<G>(a, m, N, blk, nblk);
     return m.what;
 }
@@ -598,7 +806,7 @@ hipError_t dbg_sync(const char *what, hipStream_t st) {
     return e;
 }
 
-Args views(void *ws, int H, int W) {
+Args views(void *ws, int H, int W, int G) {
     const size_t n = (size_t)H * W;
     uint8_t *w = static_cast<uint8_t *>(ws);
     Args a{};
@@ -614,12 +822,18 @@ Args views(void *ws, int H, int W) {
     w += align256(n * 8);
     a.lowkey = reinterpret_cast<unsigned long long *>(w);
     w += align256(n * 8);
-    a.stamp = reinterpret_cast<int *>(w);
+    a.queued = reinterpret_cast<unsigned long long *>(w);
+    w += align256(n * 8);
+    a.pos = reinterpret_cast<int *>(w);
     w += align256(n * 4);
+    a.lessm = reinterpret_cast<uint16_t *>(w);
+    w += align256(n * 2 * (size_t)(G > 0 ? G : 1));
     for (int i = 0; i < 2; ++i) {
         a.F[i] = reinterpret_cast<int *>(w);
         w += align256(n * 4);
         a.C[i] = reinterpret_cast<int *>(w);
+        w += align256(n * 4);
+        a.A[i] = reinterpret_cast<int *>(w);
         w += align256(n * 4);
     }
     a.H = H;
@@ -678,20 +892,30 @@ hipError_t run_march(const float *in, int64_t pitch, Args a, int ncu, int *hw, c
     const int prev = hw ? __atomic_load_n(hw + kHostSteps, __ATOMIC_RELAXED) : -1;
     int nsteps = prev < 0 ? 48 : prev + 3;
     if (o.steps >= 0) nsteps = o.steps;
-    static const bool trace = getenv("DSX_INPAINT_TRACE") != nullptr;  // debugging: the state after each step
+    const bool trace = getenv("DSX_INPAINT_TRACE") != nullptr;  // debugging: the state and time of each step
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    if (trace) {
+        (void)hipEventCreate(&e0);
+        (void)hipEventCreate(&e1);
+    }
     for (int s = 0; s < nsteps; ++s) {
+        if (trace) (void)hipEventRecord(e0, st);
         hipLaunchKernelGGL(tl_step<G>, dim3(kStepBlocks), dim3(256), 0, st, a, (unsigned)s);
         if ((e = dbg_sync("tl_step", st)) != hipSuccess) return e;
         if (trace) {
+            (void)hipEventRecord(e1, st);
             State S;
             if ((e = hipMemcpyAsync(&S, &a.ctl->st[(s + 1) % 3], sizeof(State), hipMemcpyDeviceToHost, st)) != hipSuccess ||
                 (e = hipStreamSynchronize(st)) != hipSuccess)
                 return e;
-            fprintf(stderr, "step %d: phase %d k %d b %d sweep %d lsel %d nF %d nC %d changed %d bound %.3f\n", s, S.phase, S.k,
-                    S.b, S.sweep, S.lsel, S.nF, S.nC, S.changed, S.bound);
+            float ms = 0;
+            (void)hipEventElapsedTime(&ms, e0, e1);
+            fprintf(stderr, "step %d: %.1f us phase %d k %d b %d sweep %d lsel %d nF %d nC %d nA %d bound %.3f\n", s,
+                    ms * 1e3f, S.phase, S.k, S.b, S.sweep, S.lsel, S.nF, S.nC, S.nA, S.bound);
             if (S.phase == kPhDone) break;
         }
     }
+    if (getenv("DSX_INPAINT_NO_TAIL")) return hipSuccess;  // profiling only (rocprofv3 and cooperative launches)
     unsigned s0 = (unsigned)nsteps;
     void *args[] = {&a, &s0};
     if ((e = hipLaunchCooperativeKernel(reinterpret_cast<const void *>(tl_tail<G>), dim3(ncu), dim3(256), args, 0, st)) !=
@@ -704,7 +928,9 @@ hipError_t run_march(const float *in, int64_t pitch, Args a, int ncu, int *hw, c
 
 size_t inpaint_workspace(int H, int W) {
     const size_t n = (size_t)H * W;
-    return align256(sizeof(Ctl)) + align256(n * 4) + 4 * align256(n * 8) + align256(n * 4) + 4 * align256(n * 4);
+    // the widest layout (G = 16 row masks); radius <= 3 uses half of the mask area
+    return align256(sizeof(Ctl)) + align256(n * 4) + 5 * align256(n * 8) + align256(n * 4) + align256(n * 2 * 16) +
+           6 * align256(n * 4);
 }
 
 hipError_t launch_inpaint(const float *in, int64_t pitch, int H, int W, int radius, float *out, void *ws, hipStream_t st,
@@ -716,7 +942,8 @@ hipError_t launch_inpaint(const float *in, int64_t pitch, int H, int W, int radi
     if (dev < 0 || dev >= 64) return hipErrorInvalidDevice;
     const DeviceInfo &di = device_info(dev);
     if (di.err != hipSuccess) return di.err;
-    Args a = views(ws, H, W);
+    const int G = radius <= 3 ? 8 : radius <= 7 ? 16 : 0;
+    Args a = views(ws, H, W, G);
     a.out = out;
     a.radius = radius;
     int *hw = host_words(o.status_key ? o.status_key : ws);
