@@ -18,9 +18,12 @@
 //            smaller fill key - a DAG, so the fixed point is unique - and caches which cells of its
 //            disc those are (a bit mask per window row);
 //   SWEEP i  only the children queued by the last sweep recompute: a child whose T or value changed
-//            queues the bucket's children that read it.  Updates are in place (a child may read a
-//            neighbour's value of this sweep or the last): the fixed point is the same, and a sweep
-//            that changes no bit (queues nothing) proves it.
+//            tags the bucket's children that read it (a per-position word per sweep parity; no list,
+//            no counter).  Updates are in place (a child may read a neighbour's value of this sweep
+//            or the last): the fixed point is the same, and a sweep that changes no bit (tags
+//            nothing) proves it.
+// Counters and minima are reduced per block before their one atomic (single-address atomics
+// serialise across the chip); the bucket minima spread over kMinSlots words.
 // The steps are launches of one kernel, `tl_step`, that reads a small state machine the previous step
 // left in the workspace (triple-buffered by step index: step s reads slot s%3, accumulates into
 // (s+1)%3 and clears (s+2)%3) and does the next POP or sweep; the host enqueues the step count the
@@ -44,21 +47,27 @@ namespace {
 
 constexpr int kInside = 0x7FFFFFFF;  // fill-bucket word of an unfilled hole (known pixels: -1)
 constexpr double kDelta = 0.7;       // T-bucket width (postprocess._TELEA_DELTA)
-constexpr int kStepBlocks = 512;     // grid of the step launches (an empty step costs ~1.5 us at 512)
+constexpr int kStepBlocks = 1024;    // grid of the step launches: one block round for most steps
 constexpr unsigned kMaxSteps = 1u << 24;
+constexpr int kMinSlots = 16;
 
 enum Phase : int { kPhInit = 0, kPhPop = 1, kPhSweep = 2, kPhDone = 3 };
 
 // One state slot (written by step s-1, read by step s).  Counters and minima are accumulated by the
 // blocks of the writing step; the rest is carried by block 0.
 struct alignas(128) State {
-    int phase, k, b, nb, sweep, lsel, nF, nC, nA;  // nb: buckets started; nA: children queued for the next sweep
+    int phase, k, b, nb, sweep, lsel;
+    int nF, nC;  // adjacent, 8-aligned: one 64-bit add appends to both lists (nF low word)
     double bound;
     unsigned long long minF;                      // bit patterns of non-negative doubles (monotone as integers)
 };
 struct Ctl {
     State st[3];
-    unsigned long long minC[3], pad3[13];  // min T over a bucket's children, slot = bucket ordinal % 3
+    // min T over a bucket's children: [bucket ordinal % 3][block % kMinSlots] (blocks spread their
+    // atomics over the slots; the reader takes the minimum)
+    unsigned long long minC[3][kMinSlots];
+    // [step % 3][block % kMinSlots]: a child was tagged for the next sweep (G = 0: a child changed)
+    unsigned tagged[3][kMinSlots];
     unsigned bar, pad0[31];                // grid-barrier arrival counter (own line)
     unsigned gen, pad1[31];                // barrier generation (own line)
     int tmo, pad2[31];                     // barrier timed out: every block leaves
@@ -69,10 +78,10 @@ struct Args {
     int *fb;               // fill bucket: -1 known, kInside unfilled, b filled in bucket b
     double *T, *Tpar, *Tgp;
     unsigned long long *lowkey;  // root << 34 | dir(parent) << 32 | parent << 2 | dir(self)
-    int *pos;              // a child's position in its bucket's list
     uint16_t *lessm;       // per position and window row: the row's cells that are children filled earlier
-    unsigned long long *queued;  // per position: (bucket ordinal << 32 | sweep) it was last queued for
-    int *F[2], *C[2], *A[2];  // frontier (unpopped band), children and active-children lists, ping-pong
+    unsigned long long *queued;  // [sweep & 1][pixel]: (bucket ordinal << 32 | sweep) it was tagged for
+    int *F[2], *C[2];      // frontier (unpopped band) and children lists, ping-pong
+    int64_t n;             // H * W
     Ctl *ctl;
     int *host;             // mapped host words of this workspace (nullable)
     int H, W, radius;
@@ -118,38 +127,60 @@ __device__ __forceinline__ bool filled_before(const Args &a, int64_t q, int f, i
 
 // out = in; fill-bucket words; the seeds (known pixels with a hole 4-neighbour) into F[0] with their
 // count in slot 0; slots 1 and 2 get empty minima.  The control block was zeroed before (memset).
+// Block b owns pixels [b, b+1) * kInitChunk: each wave stages its seeds in LDS over the chunk's
+// rounds, and the block appends them with one counter add.
+constexpr int kInitRounds = 8, kInitChunk = 256 * kInitRounds;
 __global__ __launch_bounds__(256) void tl_init(const float *in, int64_t pitch, Args a) {
     const int H = a.H, W = a.W;
-    const int64_t n = (int64_t)H * W;
+    const int64_t n = a.n;
     State &s0 = a.ctl->st[0];
+    __shared__ int stage[4][64 * kInitRounds];
+    __shared__ int wsum[4], bbase;
     if (blockIdx.x == 0 && threadIdx.x < 2) a.ctl->st[1 + threadIdx.x].minF = ~0ull;
-    if (blockIdx.x == 0 && threadIdx.x < 3) a.ctl->minC[threadIdx.x] = ~0ull;
-    for (int64_t p0 = (int64_t)blockIdx.x * 256; p0 < n; p0 += (int64_t)gridDim.x * 256) {  // block-uniform
-        const int64_t p = p0 + threadIdx.x;
+    if (blockIdx.x == 0 && threadIdx.x < 3 * kMinSlots) a.ctl->minC[threadIdx.x / kMinSlots][threadIdx.x % kMinSlots] = ~0ull;
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int64_t p0 = (int64_t)blockIdx.x * kInitChunk + threadIdx.x;
+    // every round's loads first, from clamped addresses (no branch around a load, so they issue back
+    // to back; the stores below could alias them for all the compiler knows)
+    float v[kInitRounds];
+    bool hole_nb[kInitRounds];
+#pragma unroll
+    for (int r = 0; r < kInitRounds; ++r) {
+        const int64_t p = p0 + 256 * r;
+        const int pc = (int)(p < n ? p : n - 1);  // n <= kInpaintMaxPixels: 32-bit indices
+        const int y = pc / W, x = pc - y * W;
+        const float *row = in + (int64_t)y * pitch + x;
+        v[r] = row[0];
+        const float u = row[y > 0 ? -pitch : 0], d = row[y < H - 1 ? pitch : 0];
+        const float l = row[x > 0 ? -1 : 0], rr = row[x < W - 1 ? 1 : 0];
+        hole_nb[r] = (y > 0 && u <= 0.0f) | (y < H - 1 && d <= 0.0f) | (x > 0 && l <= 0.0f) | (x < W - 1 && rr <= 0.0f);
+    }
+    int cnt = 0;  // this wave's staged seeds (wave-uniform)
+#pragma unroll
+    for (int r = 0; r < kInitRounds; ++r) {
+        const int64_t p = p0 + 256 * r;
         bool seed = false;
         if (p < n) {
-            const int y = (int)(p / W), x = (int)(p - (int64_t)y * W);
-            const float *row = in + (int64_t)y * pitch;
-            const float v = row[x];
-            a.out[p] = v;
-            const bool known = !(v <= 0.0f);  // fill_holes' mask = disparity <= 0 (postprocess.py:96-97)
+            a.out[p] = v[r];
+            const bool known = !(v[r] <= 0.0f);  // fill_holes' mask = disparity <= 0 (postprocess.py:96-97)
             a.fb[p] = known ? -1 : kInside;
-            if (known) {
-                const bool hu = y > 0 && row[x - pitch] <= 0.0f, hd = y < H - 1 && row[x + pitch] <= 0.0f;
-                const bool hl = x > 0 && row[x - 1] <= 0.0f, hr = x < W - 1 && row[x + 1] <= 0.0f;
-                seed = hu || hd || hl || hr;
-            }
+            seed = known && hole_nb[r];
         }
-        // wave-aggregated append
         const unsigned long long m = __ballot(seed);
-        if (m) {
-            const int lane = threadIdx.x & 63;
-            int base = 0;
-            if (lane == __builtin_ctzll(m)) base = atomicAdd(&s0.nF, __popcll(m));
-            base = __shfl(base, __builtin_ctzll(m));
-            if (seed) a.F[0][base + __popcll(m & ((1ull << lane) - 1))] = (int)p;
-        }
+        if (seed) stage[wv][cnt + __popcll(m & ((1ull << lane) - 1))] = (int)p;
+        cnt += __popcll(m);
     }
+    if (lane == 0) wsum[wv] = cnt;
+    __syncthreads();
+    int woff = 0, btot = 0;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+        woff += w < wv ? wsum[w] : 0;
+        btot += wsum[w];
+    }
+    if (threadIdx.x == 0) bbase = btot ? atomicAdd(&s0.nF, btot) : 0;
+    __syncthreads();
+    for (int k = lane; k < cnt; k += 64) a.F[0][bbase + woff + k] = stage[wv][k];
 }
 
 // ---- one step ----------------------------------------------------------------------------------
@@ -163,9 +194,18 @@ struct Mode {
     double bound;
 };
 
-// The step's mode from the slot the previous step wrote (every block computes the same).
+__device__ __forceinline__ unsigned long long wave_min_u64(unsigned long long v) {
+    for (int o = 32; o > 0; o >>= 1) {
+        const unsigned long long u = __shfl_xor(v, o);
+        v = u < v ? u : v;
+    }
+    return v;
+}
+
+// The step's mode from the slot the previous step wrote (every block computes the same).  mcv: this
+// lane's word of the bucket minima, minC[lane / 16][lane % 16] (lanes < 48), loaded with the slot.
 template <int G>
-__device__ __forceinline__ Mode decide(const State &S, const Ctl *ctl) {
+__device__ __forceinline__ Mode decide(const State &S, unsigned long long mcv, bool tagged) {
     Mode m{};
     m.k = S.k;
     m.b = S.b;
@@ -176,13 +216,13 @@ __device__ __forceinline__ Mode decide(const State &S, const Ctl *ctl) {
         m.what = kPhDone;
         return m;
     }
-    if (S.phase == kPhSweep && (S.sweep == 0 || S.nA > 0)) {
+    if (S.phase == kPhSweep && (S.sweep == 0 || tagged)) {
         m.what = kPhSweep;
         m.sweep = S.sweep + 1;
         // sweep 1 runs over every child (their dependency masks are built there); later sweeps over the
-        // children queued by the last one (G = 0: every child again, nA counts the changed blocks)
+        // children the last one tagged (G = 0: every child again while some change)
         m.full = G == 0 || m.sweep == 1;
-        m.nIn = m.full ? S.nC : S.nA;
+        m.nIn = S.nC;
         return m;
     }
     if (S.phase == kPhPop && S.nC > 0) {  // the POP ran sweep 0 of its children
@@ -203,7 +243,8 @@ __device__ __forceinline__ Mode decide(const State &S, const Ctl *ctl) {
     }
     unsigned long long mn = S.minF;
     if (after_sweep) {
-        const unsigned long long mc = __hip_atomic_load(&ctl->minC[S.nb % 3], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const int lane = threadIdx.x & 63;
+        const unsigned long long mc = wave_min_u64(lane / kMinSlots == S.nb % 3 ? mcv : ~0ull);
         mn = mc < mn ? mc : mn;
     }
     const int kf = (int)floor(bitsd(mn) / kDelta);
@@ -214,25 +255,6 @@ __device__ __forceinline__ Mode decide(const State &S, const Ctl *ctl) {
     m.b = kn + 1;
     m.nb = S.nb + 1;
     return m;
-}
-
-__device__ __forceinline__ void wave_append(bool take, int *list, int *count, int item) {
-    const unsigned long long m = __ballot(take);
-    if (!m) return;
-    const int lane = threadIdx.x & 63;
-    const int lead = __builtin_ctzll(m);
-    int base = 0;
-    if (lane == lead) base = atomicAdd(count, __popcll(m));
-    base = __shfl(base, lead);
-    if (take) list[base + __popcll(m & ((1ull << lane) - 1))] = item;
-}
-
-__device__ __forceinline__ unsigned long long wave_min_u64(unsigned long long v) {
-    for (int o = 32; o > 0; o >>= 1) {
-        const unsigned long long u = __shfl_xor(v, o);
-        v = u < v ? u : v;
-    }
-    return v;
 }
 
 // Wave-wide exclusive prefix sum of v (and the wave total).
@@ -246,6 +268,22 @@ __device__ __forceinline__ int wave_excl_scan(int v, int &total) {
     }
     total = __shfl(incl, 63);
     return incl - v;
+}
+
+// Block-wide minimum of a per-thread 64-bit key, then one atomicMin on *dst by thread 0 (no return
+// value: nothing waits for it).  Call from every thread of the block.
+__device__ __forceinline__ void block_min_to(unsigned long long v, unsigned long long *dst) {
+    __shared__ unsigned long long wmin[4];
+    v = wave_min_u64(v);
+    if ((threadIdx.x & 63) == 0) wmin[threadIdx.x >> 6] = v;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        unsigned long long b = wmin[0];
+#pragma unroll
+        for (int w = 1; w < 4; ++w) b = wmin[w] < b ? wmin[w] : b;
+        if (b != ~0ull && b < __hip_atomic_load(dst, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) atomicMin(dst, b);
+    }
+    __syncthreads();
 }
 
 // Pop key of a band pixel p (known seed or filled): (T, T_parent, root << 32 | dir << 30 | p).
@@ -318,8 +356,7 @@ struct Cells {
 };
 
 template <int G>
-__device__ __forceinline__ void sweep_child(const Args &a, const Mode &m, int i, int c, double &tc, uint32_t &won,
-                                            int (&pq)[Cells<G>::NCELL]) {
+__device__ __forceinline__ void sweep_child(const Args &a, const Mode &m, int i, int c, double &tc, bool &tagged) {
     constexpr int RM = Cells<G>::RM;
     constexpr int NCELL = Cells<G>::NCELL;
     const int j = (int)(threadIdx.x & (G - 1));
@@ -338,8 +375,8 @@ __device__ __forceinline__ void sweep_child(const Args &a, const Mode &m, int i,
             a.Tpar[c] = me.tp;
             a.Tgp[c] = me.tg;
             a.lowkey[c] = me.lo;
-            a.pos[c] = i;
-            a.queued[i] = 0;
+            a.queued[c] = 0;
+            a.queued[a.n + c] = 0;
         }
     } else if (sweep == 1) {
         me = load_key(a, c);
@@ -444,23 +481,23 @@ __device__ __forceinline__ void sweep_child(const Args &a, const Mode &m, int i,
         a.out[c] = v;
     }
     if (sweep == 0) return;  // sweep 1 visits every child anyway
-    // the children that read this one (this bucket's, filled later) go to the next sweep's list: a
-    // per-position tag keeps each once; the caller appends them with one counter add per wave
+    // the children that read this one (this bucket's, filled later) are tagged for the next sweep in
+    // the word of its parity (this sweep reads the other one)
     const uint32_t dep = intra & ~less;
     const unsigned long long tag = (unsigned long long)m.nb << 32 | (unsigned)(sweep + 1);
+    unsigned long long *qn = a.queued + ((sweep + 1) & 1) * a.n;
 #pragma unroll
     for (int cc = 0; cc < NCELL; ++cc) {
         if ((dep >> cc) & 1u) {
             const int qx = x + cc - RM;
-            const int p = a.pos[rowq + qx];
-            pq[cc] = p;
-            if (atomicMax(&a.queued[p], tag) < tag) won |= 1u << cc;
+            qn[rowq + qx] = tag;
         }
     }
+    tagged = tagged || dep != 0;
 }
 
 // Radii above 7: one thread per child, every row; availability from the fill keys each sweep and
-// every child in every sweep (nA counts the blocks that changed something).
+// every child in every sweep (until one changes nothing).
 __device__ __forceinline__ void sweep_child_wide(const Args &a, const Mode &m, int i, int c, bool &changed, double &tc) {
     const int H = a.H, W = a.W, radius = a.radius, r2 = radius * radius;
     const int y = c / W, x = c - y * W;
@@ -473,7 +510,6 @@ __device__ __forceinline__ void sweep_child_wide(const Args &a, const Mode &m, i
         a.Tpar[c] = me.tp;
         a.Tgp[c] = me.tg;
         a.lowkey[c] = me.lo;
-        a.pos[c] = i;
     } else {
         me = load_key(a, c);
     }
@@ -533,10 +569,11 @@ __device__ __forceinline__ void sweep_child_wide(const Args &a, const Mode &m, i
 }
 
 // POP: entries of F[lsel] (nIn) then C[lsel] (nPrev); T < bound pops (marks children), the rest
-// survives into F[lsel^1].  T of a known seed is 0.  The children a block marks get their list
-// positions with one counter add per block round and run sweep 0 right there (their parent and fill
-// key, T and value from the pixels filled before the bucket): the pops, and so every child's parent,
-// are fixed for the whole step, and sweep 0 reads no child of the bucket.
+// survives into F[lsel^1].  T of a known seed is 0.  A block round takes as many entries as the block
+// has groups (<= 4 children each, one sweep-0 pass for the usual 1-2), appends its survivors and the
+// children it marked with one 64-bit counter add, and runs sweep 0 of those children right there
+// (their parent and fill key, T and value from the pixels filled before the bucket): the pops, and
+// so every child's parent, are fixed for the whole step, and sweep 0 reads no child of the bucket.
 template <int G>
 __device__ void do_pop(const Args &a, const Mode &m, State &N, int blk, int nblk) {
     const int *Fi = a.F[m.lsel], *Ci = a.C[m.lsel];
@@ -545,17 +582,18 @@ __device__ void do_pop(const Args &a, const Mode &m, State &N, int blk, int nblk
     const int W = a.W, H = a.H;
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     __shared__ int kidc[1024], kidi[1024];
-    __shared__ int wsum[4], kbase;
+    __shared__ int wsumF[4], wsumK[4], kbaseF, kbaseK;
     Mode m0 = m;
     m0.what = kPhSweep;
     m0.sweep = 0;
     unsigned long long mn = ~0ull, mnc = ~0ull;
-    for (int base = blk * 256; base < tot; base += nblk * 256) {  // block-uniform trip count
+    constexpr int chunk = G > 0 ? 256 / G : 256;
+    for (int base = blk * chunk; base < tot; base += nblk * chunk) {  // block-uniform trip count
         const int i = base + (int)threadIdx.x;
         int keep = 0, p = 0;
         unsigned km = 0;  // the directions whose neighbour this pop marked (no dynamic register index)
         int nb[4] = {-1, -1, -1, -1};
-        if (i < tot) {
+        if ((int)threadIdx.x < chunk && i < tot) {
             p = i < m.nIn ? Fi[i] : Ci[i - m.nIn];
             const int y = p / W, x = p - y * W;
             nb[0] = y > 0 ? p - W : -1;
@@ -567,41 +605,51 @@ __device__ void do_pop(const Args &a, const Mode &m, State &N, int blk, int nblk
             for (int d = 0; d < 4; ++d) fn[d] = a.fb[nb[d] >= 0 ? nb[d] : p];
             const double t = a.fb[p] < 0 ? 0.0 : a.T[p];
             if (t < m.bound) {
+                // the marks of the INSIDE neighbours issue together (their results are read after)
+                int old[4] = {0, 0, 0, 0};
 #pragma unroll
-                for (int d = 0; d < 4; ++d) {
-                    if (nb[d] >= 0 && fn[d] == kInside && atomicCAS(&a.fb[nb[d]], kInside, m.b) == kInside)
-                        km |= 1u << d;
-                }
+                for (int d = 0; d < 4; ++d)
+                    if (nb[d] >= 0 && fn[d] == kInside) old[d] = atomicCAS(&a.fb[nb[d]], kInside, m.b);
+#pragma unroll
+                for (int d = 0; d < 4; ++d) km |= (uint32_t)(nb[d] >= 0 && fn[d] == kInside && old[d] == kInside) << d;
             } else {
                 keep = 1;
-                mn = dbits(t);
+                const unsigned long long tb = dbits(t);
+                mn = tb < mn ? tb : mn;
             }
         }
-        // survivors: one counter add per wave
-        int tf;
+        // survivors and children: block-wide positions, one counter add for both lists
+        int tf, tk;
         const int ef = wave_excl_scan(keep, tf);
-        int bf = 0;
-        if (lane == 0 && tf) bf = atomicAdd(&N.nF, tf);
-        bf = __shfl(bf, 0);
-        if (keep) Fo[bf + ef] = p;
-        // children: block-wide positions (one counter add), staged in LDS for sweep 0
-        int tk;
         const int ek = wave_excl_scan(__popc(km), tk);
-        if (lane == 0) wsum[wv] = tk;
+        if (lane == 0) {
+            wsumF[wv] = tf;
+            wsumK[wv] = tk;
+        }
         __syncthreads();
-        int woff = 0, btot = 0;
+        int woffF = 0, woffK = 0, btotF = 0, btot = 0;
 #pragma unroll
         for (int w = 0; w < 4; ++w) {
-            woff += w < wv ? wsum[w] : 0;
-            btot += wsum[w];
+            woffF += w < wv ? wsumF[w] : 0;
+            woffK += w < wv ? wsumK[w] : 0;
+            btotF += wsumF[w];
+            btot += wsumK[w];
         }
-        if (threadIdx.x == 0) kbase = btot ? atomicAdd(&N.nC, btot) : 0;
+        if (threadIdx.x == 0) {
+            unsigned long long old = 0;
+            if (btotF | btot)
+                old = atomicAdd(reinterpret_cast<unsigned long long *>(&N.nF),
+                                (unsigned long long)btot << 32 | (unsigned)btotF);
+            kbaseF = (int)(unsigned)old;
+            kbaseK = (int)(old >> 32);
+        }
         __syncthreads();
-        const int gb = kbase;
+        if (keep) Fo[kbaseF + woffF + ef] = p;
+        const int gb = kbaseK;
 #pragma unroll
         for (int d = 0; d < 4; ++d) {
             if ((km >> d) & 1u) {
-                const int li = woff + ek + __popc(km & ((1u << d) - 1u));
+                const int li = woffK + ek + __popc(km & ((1u << d) - 1u));
                 Co[gb + li] = nb[d];
                 kidc[li] = nb[d];
                 kidi[li] = gb + li;
@@ -612,11 +660,9 @@ __device__ void do_pop(const Args &a, const Mode &m, State &N, int blk, int nblk
             constexpr int per = 256 / G;
             const int g = (int)threadIdx.x / G;
             for (int k = g; k < btot; k += per) {  // group-uniform
-                constexpr int NCELL = Cells<G>::NCELL;
-                uint32_t won = 0;
-                int pq[NCELL];
+                bool tagged = false;
                 double tc;
-                sweep_child<G>(a, m0, kidi[k], kidc[k], tc, won, pq);
+                sweep_child<G>(a, m0, kidi[k], kidc[k], tc, tagged);
                 const unsigned long long tb = dbits(tc);
                 mnc = tb < mnc ? tb : mnc;
             }
@@ -629,67 +675,54 @@ __device__ void do_pop(const Args &a, const Mode &m, State &N, int blk, int nblk
                 mnc = tb < mnc ? tb : mnc;
             }
         }
-        __syncthreads();  // LDS list and wsum reused by the next round
+        __syncthreads();  // LDS lists and sums reused by the next round
     }
-    mn = wave_min_u64(mn);
-    if (lane == 0 && mn != ~0ull) atomicMin(&N.minF, mn);
-    mnc = wave_min_u64(mnc);
-    if (lane == 0 && mnc != ~0ull) atomicMin(&a.ctl->minC[m.nb % 3], mnc);
+    block_min_to(mn, &N.minF);
+    block_min_to(mnc, &a.ctl->minC[m.nb % 3][blk % kMinSlots]);
 }
 
+// SWEEP (m.sweep >= 1) over the bucket's children C[lsel]: every one (full), or the ones tagged for
+// this sweep (a group checks its position's tag).
 template <int G>
-__device__ void do_sweep(const Args &a, const Mode &m, State &N, int blk, int nblk) {
+__device__ void do_sweep(const Args &a, const Mode &m, unsigned *tagw, int blk, int nblk) {
     const int *Cl = a.C[m.lsel];
-    const int *Al = a.A[(m.sweep - 1) & 1];  // sweeps >= 2: the children the last sweep queued
-    int *Anext = a.A[m.sweep & 1];
-    constexpr int per = G > 0 ? 256 / G : 256;
-    const int g = G > 0 ? (int)threadIdx.x / G : (int)threadIdx.x;
     unsigned long long mn = ~0ull;
-    bool any = false;
-    for (int base = blk * per; base < m.nIn; base += nblk * per) {  // block-uniform trip count
-        const int k = base + g;
-        const bool live = k < m.nIn;
-        if constexpr (G > 0) {
-            constexpr int NCELL = Cells<G>::NCELL;
-            uint32_t won = 0;
-            int pq[NCELL];
-            if (live) {  // group-uniform
-                const int i = m.full ? k : Al[k];
+    bool tagged = false;
+    if constexpr (G > 0) {
+        constexpr int per = 256 / G;
+        const int g = (int)threadIdx.x / G;
+        const unsigned long long want = (unsigned long long)m.nb << 32 | (unsigned)m.sweep;
+        const unsigned long long *qin = a.queued + (m.sweep & 1) * a.n;
+        // one child per group and block round, so a block's tagged children take one pass whatever
+        // their clustering (children of one pop sit at adjacent positions)
+        for (int base = blk * per; base < m.nIn; base += nblk * per) {  // block-uniform trip count
+            const int i = base + g;
+            const int c = i < m.nIn ? Cl[i] : 0;
+            if (i < m.nIn && (m.full || qin[c] == want)) {  // group-uniform
                 double t;
-                sweep_child<G>(a, m, i, Cl[i], t, won, pq);
+                sweep_child<G>(a, m, i, c, t, tagged);
                 const unsigned long long tb = dbits(t);
                 mn = tb < mn ? tb : mn;
             }
-            // the queued children of the whole wave: one counter add
-            int tot;
-            const int ex = wave_excl_scan(__popc(won), tot);
-            if (tot) {
-                int base_q = 0;
-                if ((threadIdx.x & 63) == 0) base_q = atomicAdd(&N.nA, tot);
-                base_q = __shfl(base_q, 0) + ex;
-#pragma unroll
-                for (int cc = 0; cc < NCELL; ++cc)
-                    if ((won >> cc) & 1u) Anext[base_q + __popc(won & ((1u << cc) - 1u))] = pq[cc];
-            }
-        } else {
-            if (live) {
-                const int i = m.full ? k : Al[k];
+        }
+    } else {
+        for (int base = blk * 256; base < m.nIn; base += nblk * 256) {  // block-uniform
+            const int i = base + (int)threadIdx.x;
+            if (i < m.nIn) {
                 bool ch;
                 double t;
                 sweep_child_wide(a, m, i, Cl[i], ch, t);
-                any = any || ch;
+                tagged = tagged || ch;
                 const unsigned long long tb = dbits(t);
                 mn = tb < mn ? tb : mn;
             }
         }
     }
-    if constexpr (G == 0) {
-        if (__syncthreads_or(any) && threadIdx.x == 0 && m.sweep > 0) atomicAdd(&N.nA, 1);
-    }
+    if (__syncthreads_or(tagged) && threadIdx.x == 0)
+        __hip_atomic_store(tagw + blk % kMinSlots, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     // T of a child only falls over the sweeps (more neighbours filled before it), so the minimum of
     // every T computed in the bucket is the minimum of the final ones
-    mn = wave_min_u64(mn);
-    if ((threadIdx.x & 63) == 0 && mn != ~0ull) atomicMin(&a.ctl->minC[m.nb % 3], mn);
+    block_min_to(mn, &a.ctl->minC[m.nb % 3][blk % kMinSlots]);
 }
 
 // Step s: returns the mode it ran (kPhDone: the march had finished).
@@ -697,13 +730,16 @@ template <int G>
 __device__ int step(const Args &a, unsigned s, int blk, int nblk) {
     Ctl *ctl = a.ctl;
     const State S = ctl->st[s % 3];
+    const int lane = threadIdx.x & 63;
+    const unsigned long long mcv = lane < 3 * kMinSlots ? (&ctl->minC[0][0])[lane] : ~0ull;
+    const unsigned tg = lane < kMinSlots ? ctl->tagged[s % 3][lane] : 0u;
     State &N = ctl->st[(s + 1) % 3];
-    const Mode m = decide<G>(S, ctl);
+    const Mode m = decide<G>(S, mcv, __ballot(tg != 0u) != 0ull);
     if (blk == 0 && threadIdx.x == 0) {
         State &Z = ctl->st[(s + 2) % 3];
         Z.nF = 0;
         Z.nC = 0;
-        Z.nA = 0;
+        for (int q = 0; q < kMinSlots; ++q) ctl->tagged[(s + 2) % 3][q] = 0u;
         Z.minF = ~0ull;
         N.phase = m.what;
         N.k = m.k;
@@ -719,7 +755,7 @@ __device__ int step(const Args &a, unsigned s, int blk, int nblk) {
         } else if (m.what == kPhPop) {
             N.lsel = m.lsel ^ 1;
             // the next bucket's accumulator (this step reads slot nb-1 and fills slot nb)
-            ctl->minC[(m.nb + 1) % 3] = ~0ull;
+            for (int q = 0; q < kMinSlots; ++q) ctl->minC[(m.nb + 1) % 3][q] = ~0ull;
         } else {
             N.lsel = m.lsel;
             if (S.phase != kPhDone && a.host)
@@ -727,7 +763,7 @@ __device__ int step(const Args &a, unsigned s, int blk, int nblk) {
         }
     }
     if (m.what == kPhPop) do_pop<G>(a, m, N, blk, nblk);
-    else if (m.what == kPhSweep) do_sweep<G>(a, m, N, blk, nblk);
+    else if (m.what == kPhSweep) do_sweep<G>(a, m, ctl->tagged[(s + 1) % 3], blk, nblk);
     return m.what;
 }
 
@@ -823,9 +859,7 @@ Args views(void *ws, int H, int W, int G) {
     a.lowkey = reinterpret_cast<unsigned long long *>(w);
     w += align256(n * 8);
     a.queued = reinterpret_cast<unsigned long long *>(w);
-    w += align256(n * 8);
-    a.pos = reinterpret_cast<int *>(w);
-    w += align256(n * 4);
+    w += align256(2 * n * 8);
     a.lessm = reinterpret_cast<uint16_t *>(w);
     w += align256(n * 2 * (size_t)(G > 0 ? G : 1));
     for (int i = 0; i < 2; ++i) {
@@ -833,11 +867,10 @@ Args views(void *ws, int H, int W, int G) {
         w += align256(n * 4);
         a.C[i] = reinterpret_cast<int *>(w);
         w += align256(n * 4);
-        a.A[i] = reinterpret_cast<int *>(w);
-        w += align256(n * 4);
     }
     a.H = H;
     a.W = W;
+    a.n = (int64_t)n;
     return a;
 }
 
@@ -883,7 +916,7 @@ hipError_t run_march(const float *in, int64_t pitch, Args a, int ncu, int *hw, c
     hipError_t e;
     const size_t n = (size_t)a.H * a.W;
     if ((e = hipMemsetAsync(a.ctl, 0, sizeof(Ctl), st)) != hipSuccess) return e;
-    const int ib = (int)std::min<size_t>((n + 255) / 256, 2048);
+    const int ib = (int)((n + kInitChunk - 1) / kInitChunk);
     hipLaunchKernelGGL(tl_init, dim3(ib), dim3(256), 0, st, in, pitch, a);
     if ((e = dbg_sync("tl_init", st)) != hipSuccess) return e;
     if (a.radius < 1) return hipSuccess;  // no neighbourhood: nothing changes (cv2 uses radius >= 1)
@@ -910,8 +943,8 @@ hipError_t run_march(const float *in, int64_t pitch, Args a, int ncu, int *hw, c
                 return e;
             float ms = 0;
             (void)hipEventElapsedTime(&ms, e0, e1);
-            fprintf(stderr, "step %d: %.1f us phase %d k %d b %d sweep %d lsel %d nF %d nC %d nA %d bound %.3f\n", s,
-                    ms * 1e3f, S.phase, S.k, S.b, S.sweep, S.lsel, S.nF, S.nC, S.nA, S.bound);
+            fprintf(stderr, "step %d: %.1f us phase %d k %d b %d sweep %d lsel %d nF %d nC %d bound %.3f\n", s,
+                    ms * 1e3f, S.phase, S.k, S.b, S.sweep, S.lsel, S.nF, S.nC, S.bound);
             if (S.phase == kPhDone) break;
         }
     }
@@ -929,8 +962,8 @@ hipError_t run_march(const float *in, int64_t pitch, Args a, int ncu, int *hw, c
 size_t inpaint_workspace(int H, int W) {
     const size_t n = (size_t)H * W;
     // the widest layout (G = 16 row masks); radius <= 3 uses half of the mask area
-    return align256(sizeof(Ctl)) + align256(n * 4) + 5 * align256(n * 8) + align256(n * 4) + align256(n * 2 * 16) +
-           6 * align256(n * 4);
+    return align256(sizeof(Ctl)) + align256(n * 4) + 4 * align256(n * 8) + align256(2 * n * 8) + align256(n * 2 * 16) +
+           4 * align256(n * 4);
 }
 
 hipError_t launch_inpaint(const float *in, int64_t pitch, int H, int W, int radius, float *out, void *ws, hipStream_t st,
