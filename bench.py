@@ -888,6 +888,7 @@ def video_c4_figure(rk, nframes: int, warm: int = 24) -> dict:
     from depthestimation_amd.postprocess import postprocess_disparity
     from depthestimation_amd.rectify import to_grayscale_bgr
     from depthestimation_amd.stereo_core import StereoCore
+    from depthestimation_amd.synthetic import stereo_pair
     from oracle.cref import CRef
     H, W, D, f, Bl = 720, 1280, 128, 1000.0, 0.1
     base = [stereo_pair(H, W, 0, D, seed=9000 + 8 * rk.rank + i)[:2] for i in range(8)]

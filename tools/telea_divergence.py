@@ -1,5 +1,6 @@
-"""How far the layered Telea march (the GPU's form, postprocess._telea_inpaint) departs from the
-heap-ordered march of cv2.inpaint (oracle/telea_heap.py) on the reference pipeline's real input: the
+"""How far the product's Telea march (the GPU's form, postprocess._telea_inpaint: the layered march
+until round 4, the arrival-time bucket march since round 5) departs from the heap-ordered march of
+cv2.inpaint (oracle/telea_heap.py) on the reference pipeline's real input: the
 C oracle's matcher map at a BASELINE config, cropped and passed through the speckle filter and the
 outlier removal exactly as _process_pair does before fill_holes (stereo_core.py:175-184,
 postprocess.py:120-171, radius 3).  Writes one JSON line per config.  CPU only.
@@ -49,7 +50,7 @@ def main():
                "p99_abs_diff_px": float(np.percentile(diff, 99)) if diff.size else 0.0,
                "after_median_frac_pixels_differ": float((pp.median_blur3(heap) != pp.median_blur3(lay)).mean()),
                "known_pixels_identical": bool((heap[~hole] == lay[~hole]).all()),
-               "seconds": {"layered": round(t1 - t0, 2), "heap": round(t2 - t1, 2)}}
+               "seconds": {"product_form": round(t1 - t0, 2), "heap": round(t2 - t1, 2)}}
         del fin
         print(json.dumps(out), flush=True)
 
