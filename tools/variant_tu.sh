@@ -8,5 +8,5 @@ C=/root/repo/depthestimation_amd/csrc
 T=/tmp/vartu_$N
 rm -rf $T && cp -rp $C/build $T
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -Wall -Wno-unused-function "$@" -c $C/$TU.hip -o $T/$TU.o
-mkdir -p /root/repo/tools/explib
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o /root/repo/tools/explib/libdsx_$N.so $T/dsx_*.o -ldl
+OUT=${OUTDIR:-/root/repo/tools/explib}; mkdir -p $OUT
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o $OUT/libdsx_$N.so $T/dsx_*.o -ldl
