@@ -24,6 +24,8 @@
 //            nothing) proves it.
 // Counters and minima are reduced per block before their one atomic (single-address atomics
 // serialise across the chip); the bucket minima spread over kMinSlots words.
+// Bucket 1's POP is decided by the input (every band pixel is a known seed of T = 0), so `tl_init` does
+// it and the first step is bucket 1's sweep 0 over the whole list.
 // The steps are launches of one kernel, `tl_step`, that reads a small state machine the previous step
 // left in the workspace (triple-buffered by step index: step s reads slot s%3, accumulates into
 // (s+1)%3 and clears (s+2)%3) and does the next POP or sweep; the host enqueues the step count the
@@ -125,10 +127,13 @@ __device__ __forceinline__ bool filled_before(const Args &a, int64_t q, int f, i
 
 // ---- setup -----------------------------------------------------------------------------------
 
-// out = in; fill-bucket words; the seeds (known pixels with a hole 4-neighbour) into F[0] with their
-// count in slot 0; slots 1 and 2 get empty minima.  The control block was zeroed before (memset).
-// Block b owns pixels [b, b+1) * kInitChunk: each wave stages its seeds in LDS over the chunk's
-// rounds, and the block appends them with one counter add.
+// out = in; fill-bucket words; and the first bucket's POP, which the input decides: every known pixel
+// with a hole 4-neighbour is a band pixel of T = 0 and pops at bound 0.7, so bucket 1's children are
+// exactly the holes with a known 4-neighbour (fill bucket 1, no CAS) and no band pixel survives.  They
+// go to C[0] with their count in slot 0, which starts bucket 1 at its sweep 0 (kPhInit); slots 1 and 2
+// get empty minima.  The control block was zeroed before (memset).  Block b owns pixels
+// [b, b+1) * kInitChunk: each wave stages its children in LDS over the chunk's rounds, and the block
+// appends them with one counter add.
 constexpr int kInitRounds = 8, kInitChunk = 256 * kInitRounds;
 __global__ __launch_bounds__(256) void tl_init(const float *in, int64_t pitch, Args a) {
     const int H = a.H, W = a.W;
@@ -136,14 +141,20 @@ __global__ __launch_bounds__(256) void tl_init(const float *in, int64_t pitch, A
     State &s0 = a.ctl->st[0];
     __shared__ int stage[4][64 * kInitRounds];
     __shared__ int wsum[4], bbase;
-    if (blockIdx.x == 0 && threadIdx.x < 2) a.ctl->st[1 + threadIdx.x].minF = ~0ull;
+    if (blockIdx.x == 0 && threadIdx.x < 3) a.ctl->st[threadIdx.x].minF = ~0ull;
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        s0.k = 1;
+        s0.b = 1;
+        s0.nb = 1;
+        s0.bound = kDelta;
+    }
     if (blockIdx.x == 0 && threadIdx.x < 3 * kMinSlots) a.ctl->minC[threadIdx.x / kMinSlots][threadIdx.x % kMinSlots] = ~0ull;
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const int64_t p0 = (int64_t)blockIdx.x * kInitChunk + threadIdx.x;
     // every round's loads first, from clamped addresses (no branch around a load, so they issue back
     // to back; the stores below could alias them for all the compiler knows)
     float v[kInitRounds];
-    bool hole_nb[kInitRounds];
+    bool known_nb[kInitRounds];
 #pragma unroll
     for (int r = 0; r < kInitRounds; ++r) {
         const int64_t p = p0 + 256 * r;
@@ -153,21 +164,22 @@ __global__ __launch_bounds__(256) void tl_init(const float *in, int64_t pitch, A
         v[r] = row[0];
         const float u = row[y > 0 ? -pitch : 0], d = row[y < H - 1 ? pitch : 0];
         const float l = row[x > 0 ? -1 : 0], rr = row[x < W - 1 ? 1 : 0];
-        hole_nb[r] = (y > 0 && u <= 0.0f) | (y < H - 1 && d <= 0.0f) | (x > 0 && l <= 0.0f) | (x < W - 1 && rr <= 0.0f);
+        known_nb[r] = (y > 0 && !(u <= 0.0f)) | (y < H - 1 && !(d <= 0.0f)) | (x > 0 && !(l <= 0.0f)) |
+                      (x < W - 1 && !(rr <= 0.0f));
     }
-    int cnt = 0;  // this wave's staged seeds (wave-uniform)
+    int cnt = 0;  // this wave's staged children (wave-uniform)
 #pragma unroll
     for (int r = 0; r < kInitRounds; ++r) {
         const int64_t p = p0 + 256 * r;
-        bool seed = false;
+        bool kid = false;
         if (p < n) {
             a.out[p] = v[r];
             const bool known = !(v[r] <= 0.0f);  // fill_holes' mask = disparity <= 0 (postprocess.py:96-97)
-            a.fb[p] = known ? -1 : kInside;
-            seed = known && hole_nb[r];
+            kid = !known && known_nb[r];
+            a.fb[p] = known ? -1 : (kid ? 1 : kInside);
         }
-        const unsigned long long m = __ballot(seed);
-        if (seed) stage[wv][cnt + __popcll(m & ((1ull << lane) - 1))] = (int)p;
+        const unsigned long long m = __ballot(kid);
+        if (kid) stage[wv][cnt + __popcll(m & ((1ull << lane) - 1))] = (int)p;
         cnt += __popcll(m);
     }
     if (lane == 0) wsum[wv] = cnt;
@@ -178,9 +190,9 @@ __global__ __launch_bounds__(256) void tl_init(const float *in, int64_t pitch, A
         woff += w < wv ? wsum[w] : 0;
         btot += wsum[w];
     }
-    if (threadIdx.x == 0) bbase = btot ? atomicAdd(&s0.nF, btot) : 0;
+    if (threadIdx.x == 0) bbase = btot ? atomicAdd(&s0.nC, btot) : 0;
     __syncthreads();
-    for (int k = lane; k < cnt; k += 64) a.F[0][bbase + woff + k] = stage[wv][k];
+    for (int k = lane; k < cnt; k += 64) a.C[0][bbase + woff + k] = stage[wv][k];
 }
 
 // ---- one step ----------------------------------------------------------------------------------
@@ -212,8 +224,15 @@ __device__ __forceinline__ Mode decide(const State &S, unsigned long long mcv, b
     m.nb = S.nb;
     m.lsel = S.lsel;
     m.bound = S.bound;
-    if (S.phase == kPhDone) {
+    if (S.phase == kPhDone || (S.phase == kPhInit && S.nC == 0)) {
         m.what = kPhDone;
+        return m;
+    }
+    if (S.phase == kPhInit) {  // bucket 1 (tl_init popped the band): its sweep 0
+        m.what = kPhSweep;
+        m.sweep = 0;
+        m.full = true;
+        m.nIn = S.nC;
         return m;
     }
     if (S.phase == kPhSweep && (S.sweep == 0 || tagged)) {
