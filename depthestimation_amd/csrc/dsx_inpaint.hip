@@ -18,7 +18,7 @@
 //            smaller fill key - a DAG, so the fixed point is unique - and caches which cells of its
 //            disc those are (a bit mask per window row);
 //   SWEEP i  only the children queued by the last sweep recompute: a child whose T or value changed
-//            tags the bucket's children that read it (a per-position word per sweep parity; no list,
+//            tags the bucket's children that read it (a per-pixel word per sweep parity; no list,
 //            no counter).  Updates are in place (a child may read a neighbour's value of this sweep
 //            or the last): the fixed point is the same, and a sweep that changes no bit (tags
 //            nothing) proves it.
