@@ -7,6 +7,7 @@ when cv2's native matcher is unavailable: ``import cv2`` at depthlib/stereo_core
 """
 from __future__ import annotations
 
+import atexit
 import ctypes
 import os
 import threading
@@ -33,7 +34,7 @@ EXPORTS = (
     "dsx_postprocess_fast_device", "dsx_postprocess_workspace_bytes", "dsx_postprocess_full_device",
     "dsx_postprocess_full_ex_device", "dsx_fill_holes_workspace_bytes", "dsx_fill_holes_device",
     "dsx_rectify_device", "dsx_fill_holes_status", "dsx_process_pair_device", "dsx_fill_holes_ex_device",
-    "dsx_fill_holes_status_ws", "dsx_fill_holes_status_handle",
+    "dsx_fill_holes_status_ws", "dsx_fill_holes_status_handle", "dsx_fill_holes_release", "dsx_shutdown",
     "dsx_kernel_times", "dsx_reset_times", "dsx_workspace_bytes", "dsx_destroy", "dsx_last_error",
     "dsx_comm_init_all", "dsx_comm_size", "dsx_bcast", "dsx_comm_destroy",
 )
@@ -139,6 +140,8 @@ def _bind(lib):
         "dsx_fill_holes_status": (ctypes.c_int, []),
         "dsx_fill_holes_status_ws": (ctypes.c_int, [vp]),
         "dsx_fill_holes_status_handle": (ctypes.c_int, [vp]),
+        "dsx_fill_holes_release": (ctypes.c_int, [vp]),
+        "dsx_shutdown": (ctypes.c_int, []),
         "dsx_fill_holes_ex_device": (ctypes.c_int, [vp, i32, i32, i64, i32, vp, vp, ctypes.c_size_t,
                                                      ctypes.POINTER(DsxFillOpts), vp]),
         "dsx_process_pair_device": (ctypes.c_int, [vp, vp, vp, i32, i32, i64, ctypes.POINTER(DsxPostParams), vp, vp,
@@ -175,6 +178,9 @@ def lib():
                     _lib = _bind(ctypes.CDLL(LIB_PATH))
                 except OSError as e:  # pragma: no cover - depends on the image
                     raise RuntimeError(f"cannot load {LIB_PATH}: {e}") from e
+                # free the per-process mapped host words before the HIP runtime's own exit-time
+                # teardown runs (atexit handlers of the interpreter run before the C library's)
+                atexit.register(_lib.dsx_shutdown)
     return _lib
 
 

@@ -479,7 +479,7 @@ int sticky_inpaint_timeout(const void *key) {
 }
 
 int check_fill_shape(int64_t H, int64_t W) {
-    if (H * W >= dsx::kInpaintMaxPixels) return fail(DSX_EINVAL, "image too large for hole filling (H * W >= 2^30)");
+    if (H * W >= dsx::kInpaintMaxPixels) return fail(DSX_EINVAL, "image too large for hole filling (H * W >= 2^27)");
     return DSX_OK;
 }
 
@@ -1025,6 +1025,33 @@ int dsx_compute_host(dsx_handle *h, const uint8_t *L, const uint8_t *R, int32_t 
 int dsx_fill_holes_status(void) {
     g_err.clear();
     return sticky_inpaint_timeout(nullptr);
+}
+
+int dsx_fill_holes_release(const void *d_workspace) {
+    g_err.clear();
+    if (!d_workspace) return fail(DSX_EINVAL, "dsx_fill_holes_release: null workspace");
+    const int rc = sticky_inpaint_timeout(d_workspace);
+    dsx::inpaint_forget(d_workspace);
+    return rc;
+}
+
+int dsx_shutdown(void) {
+    g_err.clear();
+    if (!dsx::inpaint_has_words()) return DSX_OK;  // nothing kept: no HIP call (CPU-only hosts)
+    // the device may still write a workspace's mapped words: drain every device first.  (Freeing
+    // them matters at exit: left to the HIP runtime's own teardown, the pinned mapped words were
+    // the difference between a clean exit and a SIGSEGV inside libhsa-runtime64 under rocprofv3,
+    // tools/exit_probe.py, profiles/README.md.)
+    int n = 0;
+    if (hipGetDeviceCount(&n) == hipSuccess) {
+        int prev = 0;
+        (void)hipGetDevice(&prev);
+        for (int d = 0; d < n; ++d)
+            if (hipSetDevice(d) == hipSuccess) (void)hipDeviceSynchronize();
+        (void)hipSetDevice(prev);
+    }
+    dsx::inpaint_forget_all();
+    return DSX_OK;
 }
 
 int dsx_fill_holes_status_ws(const void *d_workspace) {

@@ -1,38 +1,41 @@
 // Hole filling on the device: fill_holes(method='inpaint') (depthlib/postprocess.py:72-118, reached
 // from postprocess_disparity :160-166 when StereoCore's hole_filling is set, stereo_core.py:175-184),
-// i.e. cv2.inpaint(..., INPAINT_TELEA) on the pixels with d <= 0.
+// i.e. cv2.inpaint(float32 map, d <= 0, radius, INPAINT_TELEA), as OpenCV's inpaint.cpp does it
+// (recalled; specification and sequential oracle: oracle/telea_cv.c; host form of this parallel
+// march: depthestimation_amd/postprocess.py _telea_march / _telea_inpaint, equal bit for bit).
 //
-// Telea's fast march in cv2.inpaint's own order: by arrival time T.  The heap pops the narrow band
-// by (T, push order); popping p fills each still-INSIDE 4-neighbour q from what is filled so far:
-// T(q) by the upwind solve over its filled 4-neighbours, value(q) = sum w v / sum w over the filled
-// pixels of its radius disc.  A child's T exceeds its parent's by at least sqrt(2)/2, so with
-// T-buckets of width 0.7 the pops of a bucket are exactly the band pixels in it when the bucket starts
-// (host restatement and proof: depthestimation_amd/postprocess.py _telea_inpaint; sequential heap
-// oracle: oracle/telea_heap.py).  Per bucket:
-//   POP      band pixels with T below the bucket bound are popped; each marks its INSIDE 4-neighbours
-//            (atomic CAS on the fill-bucket word: the first one appends the child to the list);
-//   SWEEP 0  each child picks its parent (the pop neighbour with the least pop key (T, T_parent, root
-//            seed, direction, raster)), stores its fill key (the parent's pop key + its direction) and
-//            computes T / value from the pixels filled before the bucket;
+// OpenCV runs two fast marches from the band (the known pixels 4-adjacent to a hole, T = 0):
+//   1. OUTWARD over the known pixels within Chebyshev distance `radius` of a hole (the ring), T only;
+//      every pixel it pops then gets T negated (band -0, ring minus its distance);
+//   2. INWARD over the holes: popping p fills each INSIDE 4-neighbour q (up, left, down, right): T(q)
+//      by the upwind pair solve (double, rounded to float), value(q) by Telea's float32 weighted sum
+//      over the radius disc plus OpenCV's normalised gradient term and + 0.5.
+// Each queue pops (T, push order).  A child's T exceeds its parent's by at least sqrt(2)/2, so with
+// T-buckets of width 0.7 the pops of a bucket are exactly the band pixels in it when the bucket
+// starts.  Per bucket:
+//   POP      band pixels below the bound pop: each marks its INSIDE 4-neighbours (atomic CAS on the
+//            fill-bucket word; the first one appends the child), joins the bucket's pop list with its
+//            push key (its parent's pop rank * 4 + its direction; seeds: raster index) and rank base;
+//   SWEEP 0  (fused with the POP) each child picks its parent - the pop neighbour with the least
+//            (T, push key) - stores its fill key (parent T, parent push key, direction: the order in
+//            which the queue fills the bucket) and computes T / value from the pre-bucket pixels;
 //   SWEEP 1  each child recomputes from the pre-bucket pixels and the bucket's children with a
 //            smaller fill key - a DAG, so the fixed point is unique - and caches which cells of its
-//            disc those are (a bit mask per window row);
+//            window those are (a bit mask per window row).  The same step ranks the bucket's pops
+//            (dense ranks by (T, push key): pairs of 256-pop chunks compared in LDS, counts added to
+//            the base) - the children's push keys, needed from the next bucket on;
 //   SWEEP i  only the children queued by the last sweep recompute: a child whose T or value changed
-//            tags the bucket's children that read it (a per-pixel word per sweep parity; no list,
-//            no counter).  Updates are in place (a child may read a neighbour's value of this sweep
-//            or the last): the fixed point is the same, and a sweep that changes no bit (tags
-//            nothing) proves it.
-// Counters and minima are reduced per block before their one atomic (single-address atomics
-// serialise across the chip); the bucket minima spread over kMinSlots words.
-// Bucket 1's POP is decided by the input (every band pixel is a known seed of T = 0), so `tl_init` does
-// it and the first step is bucket 1's sweep 0 over the whole list.
+//            tags the bucket's children that read it (a per-pixel word per sweep parity).  A sweep
+//            that tags nothing ends the bucket.
+// Between the marches one SWITCH step negates the outward march's T, re-marks the holes and lists the
+// inward march's first bucket.  Bucket 1 of each march is decided by the input (every band pixel is
+// a seed of T = 0), so the init passes / SWITCH list it and the first step is its sweep 0.
 // The steps are launches of one kernel, `tl_step`, that reads a small state machine the previous step
-// left in the workspace (triple-buffered by step index: step s reads slot s%3, accumulates into
-// (s+1)%3 and clears (s+2)%3) and does the next POP or sweep; the host enqueues the step count the
-// previous call on this workspace needed (+3, written by the device into mapped host memory) and one
-// persistent cooperative launch, `tl_tail`, runs whatever is left with a grid barrier per step.
-// Arithmetic: float64 throughout, no contraction, window rows summed left to right, row sums top to
-// bottom - the host restatement's order, so the device equals it bit for bit.
+// left in the workspace (triple-buffered by step index); the host enqueues the step count the previous
+// call on this workspace needed (+3) and one persistent launch, `tl_tail` (one block per CU), runs
+// whatever is left with a grid barrier per step.
+// Arithmetic: OpenCV's - float32 T, values and sums (disc in row-major order), double inside the pair
+// solve and the dst / lev weights, no contraction.
 #include "dsx_internal.h"
 
 #include <algorithm>
@@ -47,142 +50,158 @@ namespace dsx {
 
 namespace {
 
-constexpr int kInside = 0x7FFFFFFF;  // fill-bucket word of an unfilled hole (known pixels: -1)
+constexpr int kInside = 0x7FFFFFFF;  // fill-bucket word of an unfilled pixel of the march (known: -1)
 constexpr double kDelta = 0.7;       // T-bucket width (postprocess._TELEA_DELTA)
+constexpr float kFar = 1.0e6f;       // T of the padding and of pixels no march reaches
 constexpr int kStepBlocks = 1024;    // grid of the step launches: one block round for most steps
 constexpr unsigned kMaxSteps = 1u << 24;
 constexpr int kMinSlots = 16;
+constexpr int kG = 16;               // lanes per child (window rows) of the grouped sweep
+constexpr int kPer = 256 / kG;       // children per block round of the grouped sweep
 
-enum Phase : int { kPhInit = 0, kPhPop = 1, kPhSweep = 2, kPhDone = 3 };
+enum Phase : int { kPhInit = 0, kPhPop = 1, kPhSweep = 2, kPhDone = 3, kPhSwitch = 4 };
+enum : uint8_t { kClsOther = 0, kClsHole = 1, kClsBand = 2, kClsRing = 3 };
 
 // One state slot (written by step s-1, read by step s).  Counters and minima are accumulated by the
 // blocks of the writing step; the rest is carried by block 0.
 struct alignas(128) State {
     int phase, k, b, nb, sweep, lsel;
-    int nF, nC;  // adjacent, 8-aligned: one 64-bit add appends to both lists (nF low word)
+    int nF, nC;         // adjacent, 8-aligned: one 64-bit add appends to both lists (nF low word)
+    int nP, march;      // pops of this bucket; 0: the outward march, 1: the inward one
+    int base, rank_on;  // rank base of this bucket's pops; whether they need ranks (not the seeds)
     double bound;
-    unsigned long long minF;                      // bit patterns of non-negative doubles (monotone as integers)
+    unsigned long long minF;  // bit patterns of non-negative doubles (monotone as integers)
 };
 struct Ctl {
     State st[3];
-    // min T over a bucket's children: [bucket ordinal % 3][block % kMinSlots] (blocks spread their
-    // atomics over the slots; the reader takes the minimum)
-    unsigned long long minC[3][kMinSlots];
-    // [step % 3][block % kMinSlots]: a child was tagged for the next sweep (G = 0: a child changed)
-    unsigned tagged[3][kMinSlots];
-    unsigned bar, pad0[31];                // grid-barrier arrival counter (own line)
-    unsigned gen, pad1[31];                // barrier generation (own line)
-    int tmo, pad2[31];                     // barrier timed out: every block leaves
+    unsigned long long minC[3][kMinSlots];  // min T of a bucket's children: [ordinal % 3][block % slots]
+    unsigned tagged[3][kMinSlots];          // [step % 3][block % slots]: a child was tagged
+    unsigned bar, pad0[31];                 // grid-barrier arrival counter (own line)
+    unsigned gen, pad1[31];                 // barrier generation (own line)
+    int tmo, pad2[31];                      // barrier timed out: every block leaves
 };
 
 struct Args {
-    float *out;
-    int *fb;               // fill bucket: -1 known, kInside unfilled, b filled in bucket b
-    double *T, *Tpar, *Tgp;
-    unsigned long long *lowkey;  // root << 34 | dir(parent) << 32 | parent << 2 | dir(self)
-    uint16_t *lessm;       // per position and window row: the row's cells that are children filled earlier
+    float *out;               // the image being filled (contiguous W): the march's current values
+    const float *in;          // the input (row pitch `pitch`): what an unfilled pixel holds
+    int64_t pitch;
+    int *fb;                  // fill bucket: -1 known, kInside unfilled, b filled in bucket b
+    float *T;
+    unsigned long long *key;  // fill key of the current bucket's children
+    unsigned *pk, *rank, *par;   // push key and pop rank of pops; parent * 4 + direction of filled pixels
     unsigned long long *queued;  // [sweep & 1][pixel]: (bucket ordinal << 32 | sweep) it was tagged for
-    int *F[2], *C[2];      // frontier (unpopped band) and children lists, ping-pong
-    int64_t n;             // H * W
+    uint16_t *lessm;          // [list position][window row]: cells that are children filled earlier
+    int *F[2], *C[2], *P;     // frontier, children (ping-pong), this bucket's pops
+    uint8_t *cls, *rowd;      // pixel class; a hole within `radius` along the row
+    int64_t n;
     Ctl *ctl;
-    int *host;             // mapped host words of this workspace (nullable)
+    int *host;                // mapped host words of this workspace (nullable)
     int H, W, radius;
     unsigned spin_limit;
 };
 
 constexpr int kHostSteps = 0, kHostTmo = 16;
 
-__device__ __forceinline__ double telea_solve(double t1, double t2) {
-    if (t1 < 1e6 && t2 < 1e6) {
-        const double d = t1 - t2;
-        const double r = 2.0 - d * d;
-        if (r > 0) {
-            const double s = (t1 + t2 + __builtin_sqrt(r)) / 2.0;
-            if (s >= t1 && s >= t2) return s;
-        }
-    }
-    return 1.0 + (t1 < t2 ? t1 : t2);
-}
-
 __device__ __forceinline__ unsigned long long dbits(double v) { return (unsigned long long)__double_as_longlong(v); }
 __device__ __forceinline__ double bitsd(unsigned long long v) { return __longlong_as_double((long long)v); }
 
-// Fill key of a child of the current bucket: (T_parent, T_grandparent, lowkey).  Lexicographic.
-struct Key {
-    double tp, tg;
-    unsigned long long lo;
-};
-__device__ __forceinline__ bool key_less(const Key &a, const Key &b) {
-    return a.tp < b.tp || (a.tp == b.tp && (a.tg < b.tg || (a.tg == b.tg && a.lo < b.lo)));
+// OpenCV's FastMarching_solve: f1 / f2 = not INSIDE; double inside, float out.
+__device__ __forceinline__ float fm_solve(float t1, bool f1, float t2, bool f2) {
+    const double a11 = t1, a22 = t2;
+    const double m12 = a11 < a22 ? a11 : a22;
+    double sol;
+    if (f1) {
+        if (f2) {
+            const double d = a11 - a22;
+            sol = __builtin_fabs(d) >= 1.0 ? 1.0 + m12 : (a11 + a22 + __builtin_sqrt(2.0 - d * d)) * 0.5;
+        } else {
+            sol = 1.0 + a11;
+        }
+    } else {
+        sol = f2 ? 1.0 + a22 : 1.0 + m12;
+    }
+    return (float)sol;
 }
-__device__ __forceinline__ Key load_key(const Args &a, int64_t q) { return Key{a.Tpar[q], a.Tgp[q], a.lowkey[q]}; }
+__device__ __forceinline__ float cmin(float a, float b) { return a < b ? a : b; }
+// min4 over the (up | down) x (left | right) pairs
+__device__ __forceinline__ float arrival(float tu, bool fu, float tl, bool fl, float td, bool fd, float tr, bool fr) {
+    const float a = cmin(fm_solve(tu, fu, tl, fl), fm_solve(td, fd, tl, fl));
+    const float c = cmin(fm_solve(tu, fu, tr, fr), fm_solve(td, fd, tr, fr));
+    return cmin(a, c);
+}
 
-// Is pixel q (fill bucket f) filled before child `me` of bucket b?  Pre-bucket pixels always; the
-// bucket's own children when their fill key is smaller (and only after sweep 0 stored the keys).
-__device__ __forceinline__ bool filled_before(const Args &a, int64_t q, int f, int b, bool keys, const Key &me) {
-    if (f < b) return true;
-    if (f != b || !keys) return false;
-    return key_less(load_key(a, q), me);
+// Push key of pixel q (fill bucket fq != kInside): seeds were pushed in raster order, a filled pixel
+// by its parent's pop (rank * 4 + its direction).  The parent popped in an earlier bucket, whose
+// ranks are final.
+__device__ __forceinline__ unsigned pushkey_of(const Args &a, int q, int fq) {
+    if (fq < 0) return (unsigned)q;
+    const unsigned pd = a.par[q];
+    const int gp = (int)(pd >> 2);
+    const unsigned rg = a.fb[gp] < 0 ? (unsigned)gp : a.rank[gp];
+    return rg * 4u + (pd & 3u);
 }
 
 // ---- setup -----------------------------------------------------------------------------------
 
-// out = in; fill-bucket words; and the first bucket's POP, which the input decides: every known pixel
-// with a hole 4-neighbour is a band pixel of T = 0 and pops at bound 0.7, so bucket 1's children are
-// exactly the holes with a known 4-neighbour (fill bucket 1, no CAS) and no band pixel survives.  They
-// go to C[0] with their count in slot 0, which starts bucket 1 at its sweep 0 (kPhInit); slots 1 and 2
-// get empty minima.  The control block was zeroed before (memset).  Block b owns pixels
-// [b, b+1) * kInitChunk: each wave stages its children in LDS over the chunk's rounds, and the block
-// appends them with one counter add.
-constexpr int kInitRounds = 8, kInitChunk = 256 * kInitRounds;
-__global__ __launch_bounds__(256) void tl_init(const float *in, int64_t pitch, Args a) {
-    const int H = a.H, W = a.W;
-    const int64_t n = a.n;
+// out = in; pixel classes hole / band / other; rowd = a hole within `radius` along the row.
+__global__ __launch_bounds__(256) void tl_init_a(Args a) {
+    const int64_t p = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (p >= a.n) return;
+    const int H = a.H, W = a.W, r = a.radius;
+    const int y = (int)(p / W), x = (int)(p - (int64_t)y * W);
+    const float *row = a.in + (int64_t)y * a.pitch;
+    const float v = row[x];
+    a.out[p] = v;
+    const bool hole = v <= 0.0f;  // fill_holes' mask = disparity <= 0 (postprocess.py:96-97)
+    bool nb = false;
+    if (!hole)
+        nb = (y > 0 && row[x - a.pitch] <= 0.0f) | (y < H - 1 && row[x + a.pitch] <= 0.0f) | (x > 0 && row[x - 1] <= 0.0f) |
+             (x < W - 1 && row[x + 1] <= 0.0f);
+    a.cls[p] = hole ? kClsHole : (nb ? kClsBand : kClsOther);
+    bool near = false;
+    const int x0 = x - r > 0 ? x - r : 0, x1 = x + r < W - 1 ? x + r : W - 1;
+    for (int xx = x0; xx <= x1 && !near; ++xx) near = row[xx] <= 0.0f;
+    a.rowd[p] = near;
+}
+
+// The ring (rect dilation of the holes minus holes and band), the outward march's fill-bucket words
+// and T, and its first bucket: every band pixel is a seed of T = 0 that pops at bound 0.7, so the
+// bucket's children are the ring pixels with a band 4-neighbour (fill bucket 1, list C[0]).  The
+// control block was zeroed before.  Block-aggregated list appends.
+__global__ __launch_bounds__(256) void tl_init_b(Args a) {
+    const int64_t p = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    const int H = a.H, W = a.W, r = a.radius;
     State &s0 = a.ctl->st[0];
-    __shared__ int stage[4][64 * kInitRounds];
-    __shared__ int wsum[4], bbase;
     if (blockIdx.x == 0 && threadIdx.x < 3) a.ctl->st[threadIdx.x].minF = ~0ull;
     if (blockIdx.x == 0 && threadIdx.x == 0) {
         s0.k = 1;
         s0.b = 1;
         s0.nb = 1;
         s0.bound = kDelta;
+        s0.base = (int)a.n;
     }
     if (blockIdx.x == 0 && threadIdx.x < 3 * kMinSlots) a.ctl->minC[threadIdx.x / kMinSlots][threadIdx.x % kMinSlots] = ~0ull;
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    const int64_t p0 = (int64_t)blockIdx.x * kInitChunk + threadIdx.x;
-    // every round's loads first, from clamped addresses (no branch around a load, so they issue back
-    // to back; the stores below could alias them for all the compiler knows)
-    float v[kInitRounds];
-    bool known_nb[kInitRounds];
-#pragma unroll
-    for (int r = 0; r < kInitRounds; ++r) {
-        const int64_t p = p0 + 256 * r;
-        const int pc = (int)(p < n ? p : n - 1);  // n <= kInpaintMaxPixels: 32-bit indices
-        const int y = pc / W, x = pc - y * W;
-        const float *row = in + (int64_t)y * pitch + x;
-        v[r] = row[0];
-        const float u = row[y > 0 ? -pitch : 0], d = row[y < H - 1 ? pitch : 0];
-        const float l = row[x > 0 ? -1 : 0], rr = row[x < W - 1 ? 1 : 0];
-        known_nb[r] = (y > 0 && !(u <= 0.0f)) | (y < H - 1 && !(d <= 0.0f)) | (x > 0 && !(l <= 0.0f)) |
-                      (x < W - 1 && !(rr <= 0.0f));
-    }
-    int cnt = 0;  // this wave's staged children (wave-uniform)
-#pragma unroll
-    for (int r = 0; r < kInitRounds; ++r) {
-        const int64_t p = p0 + 256 * r;
-        bool kid = false;
-        if (p < n) {
-            a.out[p] = v[r];
-            const bool known = !(v[r] <= 0.0f);  // fill_holes' mask = disparity <= 0 (postprocess.py:96-97)
-            kid = !known && known_nb[r];
-            a.fb[p] = known ? -1 : (kid ? 1 : kInside);
+    bool kid = false;
+    if (p < a.n) {
+        const int y = (int)(p / W), x = (int)(p - (int64_t)y * W);
+        const uint8_t c = a.cls[p];
+        bool ring = false;
+        if (c == kClsOther) {
+            const int y0 = y - r > 0 ? y - r : 0, y1 = y + r < H - 1 ? y + r : H - 1;
+            for (int yy = y0; yy <= y1 && !ring; ++yy) ring = a.rowd[(int64_t)yy * W + x] != 0;
         }
-        const unsigned long long m = __ballot(kid);
-        if (kid) stage[wv][cnt + __popcll(m & ((1ull << lane) - 1))] = (int)p;
-        cnt += __popcll(m);
+        if (ring) {
+            a.cls[p] = kClsRing;
+            kid = (y > 0 && a.cls[p - W] == kClsBand) | (y < H - 1 && a.cls[p + W] == kClsBand) |
+                  (x > 0 && a.cls[p - 1] == kClsBand) | (x < W - 1 && a.cls[p + 1] == kClsBand);
+        }
+        a.fb[p] = ring ? (kid ? 1 : kInside) : -1;
+        a.T[p] = c == kClsBand ? 0.0f : kFar;
     }
-    if (lane == 0) wsum[wv] = cnt;
+    __shared__ int wsum[4], bbase;
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const unsigned long long m = __ballot(kid);
+    if (lane == 0) wsum[wv] = __popcll(m);
     __syncthreads();
     int woff = 0, btot = 0;
 #pragma unroll
@@ -192,17 +211,18 @@ __global__ __launch_bounds__(256) void tl_init(const float *in, int64_t pitch, A
     }
     if (threadIdx.x == 0) bbase = btot ? atomicAdd(&s0.nC, btot) : 0;
     __syncthreads();
-    for (int k = lane; k < cnt; k += 64) a.C[0][bbase + woff + k] = stage[wv][k];
+    if (kid) a.C[0][bbase + woff + __popcll(m & ((1ull << lane) - 1))] = (int)p;
 }
 
 // ---- one step ----------------------------------------------------------------------------------
 
 struct Mode {
-    int what;  // kPhPop, kPhSweep, kPhDone
-    int k, b, nb, sweep, lsel;
-    int nIn;    // POP: survivors; sweeps: list length (the bucket's children, or the active list)
+    int what;  // kPhPop, kPhSweep, kPhDone, kPhSwitch
+    int k, b, nb, sweep, lsel, march;
+    int nIn;    // POP: survivors; sweeps: list length
     int nPrev;  // POP: the last bucket's children
-    bool full;  // sweep over the bucket's whole list (positions 0..nIn), else over the active list
+    int nP, base, rank_on;
+    bool full;  // sweep over the bucket's whole list, else over the tagged children
     double bound;
 };
 
@@ -216,7 +236,7 @@ __device__ __forceinline__ unsigned long long wave_min_u64(unsigned long long v)
 
 // The step's mode from the slot the previous step wrote (every block computes the same).  mcv: this
 // lane's word of the bucket minima, minC[lane / 16][lane % 16] (lanes < 48), loaded with the slot.
-template <int G>
+template <int RW>
 __device__ __forceinline__ Mode decide(const State &S, unsigned long long mcv, bool tagged) {
     Mode m{};
     m.k = S.k;
@@ -224,23 +244,31 @@ __device__ __forceinline__ Mode decide(const State &S, unsigned long long mcv, b
     m.nb = S.nb;
     m.lsel = S.lsel;
     m.bound = S.bound;
-    if (S.phase == kPhDone || (S.phase == kPhInit && S.nC == 0)) {
+    m.march = S.march;
+    m.nP = S.nP;
+    m.base = S.base;
+    m.rank_on = S.rank_on;
+    const int finish = S.march == 0 ? kPhSwitch : kPhDone;  // the end of a march
+    if (S.phase == kPhDone) {
         m.what = kPhDone;
         return m;
     }
-    if (S.phase == kPhInit) {  // bucket 1 (tl_init popped the band): its sweep 0
+    if (S.phase == kPhInit && S.nC == 0) {
+        m.what = finish;
+        return m;
+    }
+    if (S.phase == kPhInit) {  // bucket 1 (the band popped): its sweep 0
         m.what = kPhSweep;
         m.sweep = 0;
         m.full = true;
         m.nIn = S.nC;
         return m;
     }
+    // (the wide form re-runs every child each sweep until one changes nothing)
     if (S.phase == kPhSweep && (S.sweep == 0 || tagged)) {
         m.what = kPhSweep;
         m.sweep = S.sweep + 1;
-        // sweep 1 runs over every child (their dependency masks are built there); later sweeps over the
-        // children the last one tagged (G = 0: every child again while some change)
-        m.full = G == 0 || m.sweep == 1;
+        m.full = RW == 0 || m.sweep == 1;
         m.nIn = S.nC;
         return m;
     }
@@ -251,13 +279,12 @@ __device__ __forceinline__ Mode decide(const State &S, unsigned long long mcv, b
         m.nIn = S.nC;
         return m;
     }
-    // a POP: over the survivors F[lsel] and the last bucket's children C[lsel] (none after a POP
-    // without children or at the start)
+    // a POP: over the survivors F[lsel] and the last bucket's children C[lsel]
     const bool after_sweep = S.phase == kPhSweep;
     m.nIn = S.nF;
     m.nPrev = after_sweep ? S.nC : 0;
     if (m.nIn + m.nPrev == 0) {
-        m.what = kPhDone;
+        m.what = finish;
         return m;
     }
     unsigned long long mn = S.minF;
@@ -273,6 +300,8 @@ __device__ __forceinline__ Mode decide(const State &S, unsigned long long mcv, b
     m.k = kn + 1;
     m.b = kn + 1;
     m.nb = S.nb + 1;
+    m.base = S.base + S.nP;  // ranks of this bucket's pops follow the last bucket's
+    m.rank_on = 1;
     return m;
 }
 
@@ -289,8 +318,7 @@ __device__ __forceinline__ int wave_excl_scan(int v, int &total) {
     return incl - v;
 }
 
-// Block-wide minimum of a per-thread 64-bit key, then one atomicMin on *dst by thread 0 (no return
-// value: nothing waits for it).  Call from every thread of the block.
+// Block-wide minimum of a per-thread 64-bit key, then one atomicMin on *dst by thread 0.
 __device__ __forceinline__ void block_min_to(unsigned long long v, unsigned long long *dst) {
     __shared__ unsigned long long wmin[4];
     v = wave_min_u64(v);
@@ -305,317 +333,401 @@ __device__ __forceinline__ void block_min_to(unsigned long long v, unsigned long
     __syncthreads();
 }
 
-// Pop key of a band pixel p (known seed or filled): (T, T_parent, root << 32 | dir << 30 | p).
-struct PopKey {
-    double t, tp;
-    unsigned long long lo;
-};
-__device__ __forceinline__ bool pop_less(const PopKey &a, const PopKey &b) {
-    return a.t < b.t || (a.t == b.t && (a.tp < b.tp || (a.tp == b.tp && a.lo < b.lo)));
+// LDS order among the lanes of one wave (a child's lane group lies inside one wave)
+__device__ __forceinline__ void wave_lds_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-// Sweep 0: child c's parent - the pop neighbour with the least pop key (a band neighbour below the
-// bound is a pop of this bucket: one popped earlier would have filled c then) - and its fill key.
-// Branch-free: only the least key is carried through the candidates; the parent's raster index is
-// the key's low 30 bits (kInpaintMaxPixels) and the direction follows from it.
-__device__ __forceinline__ Key parent_key(const Args &a, const Mode &m, int c, const int (&nbp)[4]) {
-    // every neighbour's words load at once (clamped to c), then the candidates are picked
+// Sweep 0: child c's parent - the pop neighbour with the least (T, push key) (a band neighbour below
+// the bound is a pop of this bucket: one popped earlier would have filled c then) - and its fill key
+// (parent T, parent push key, direction).  Directions as OpenCV visits a pop's neighbours: a child
+// above its parent is 0, left of it 1, below 2, right 3.
+__device__ __forceinline__ unsigned long long parent_key(const Args &a, const Mode &m, int c) {
+    const int W = a.W, H = a.H;
+    const int y = c / W, x = c - y * W;
+    // the neighbour below the child (c + W) has it above (0); right (c + 1): 1; above: 2; left: 3
+    const int nbp[4] = {y < H - 1 ? c + W : -1, x < W - 1 ? c + 1 : -1, y > 0 ? c - W : -1, x > 0 ? c - 1 : -1};
     int fn[4];
-    double tn[4], tpn[4];
-    unsigned long long lkn[4];
+    float tn[4];
 #pragma unroll
     for (int d = 0; d < 4; ++d) {
         const int p = nbp[d] >= 0 ? nbp[d] : c;
         fn[d] = a.fb[p];
         tn[d] = a.T[p];
-        tpn[d] = a.Tpar[p];
-        lkn[d] = a.lowkey[p];
     }
-    PopKey best{0.0, 0.0, ~0ull};
-    bool have = false;
+    unsigned long long best = ~0ull;
 #pragma unroll
     for (int d = 0; d < 4; ++d) {
-        const int p = nbp[d];
-        const int f = fn[d];
-        const bool known = f < 0;
-        PopKey k;
-        k.t = known ? 0.0 : tn[d];
-        k.tp = known ? -1.0 : tpn[d];
-        const unsigned long long proot = known ? (unsigned long long)(unsigned)p : lkn[d] >> 34;
-        const unsigned long long pdir = known ? 0ull : (lkn[d] & 3ull);
-        k.lo = proot << 32 | pdir << 30 | (unsigned long long)(unsigned)p;
-        const bool cand = p >= 0 && f < m.b && k.t < m.bound;
-        const bool take = cand && (!have || pop_less(k, best));
-        best.t = take ? k.t : best.t;
-        best.tp = take ? k.tp : best.tp;
-        best.lo = take ? k.lo : best.lo;
-        have = have || cand;
+        const bool cand = nbp[d] >= 0 && fn[d] != kInside && fn[d] < m.b && (double)tn[d] < m.bound;
+        if (cand) {
+            const unsigned pk = pushkey_of(a, nbp[d], fn[d]);
+            const unsigned long long k =
+                (unsigned long long)__float_as_uint(tn[d]) << 32 | (unsigned long long)pk << 2 | (unsigned long long)d;
+            best = k < best ? k : best;
+        }
     }
-    const int bp = (int)(best.lo & ((1ull << 30) - 1ull));
-    // direction from the parent to the child (up, left, down, right): parent above -> down, ...
-    const int W = a.W;
-    const int dirc = bp == c - W ? 2 : (bp == c + W ? 0 : (bp == c - 1 ? 3 : 1));
-    Key me;
-    me.tp = best.t;
-    me.tg = best.tp;
-    const unsigned long long root = best.lo >> 32, pdir = (best.lo >> 30) & 3;
-    me.lo = root << 34 | pdir << 32 | (unsigned long long)(unsigned)bp << 2 | (unsigned long long)dirc;
-    return me;
+    return best;
 }
 
-// One child with G lanes (lane j = window row j - radius; G = 8 up to radius 3, 16 up to 7): the
-// row's cells load at once (clamped addresses, masked afterwards), availability comes from the fill
-// bucket (before this bucket) and the cached `lessm` row mask (this bucket's children filled earlier,
-// built in sweep 1 from the fill keys), the 4-neighbours' T from the centre rows by shuffles.
-// Returns (lane 0) whether T or the value changed, and the child's T.
-template <int G>
-struct Cells {
-    static constexpr int RM = (G - 2) / 2;  // widest radius of the group form: 3 (G 8), 7 (G 16)
-    static constexpr int NCELL = 2 * RM + 1;
-};
+__device__ __forceinline__ unsigned parent_word(int c, int W, unsigned long long key) {
+    const unsigned d = (unsigned)(key & 3);
+    const int p = d == 0 ? c + W : (d == 1 ? c + 1 : (d == 2 ? c - W : c - 1));
+    return (unsigned)p << 2 | d;
+}
 
-template <int G>
-__device__ __forceinline__ void sweep_child(const Args &a, const Mode &m, int i, int c, double &tc, bool &tagged) {
-    constexpr int RM = Cells<G>::RM;
-    constexpr int NCELL = Cells<G>::NCELL;
-    const int j = (int)(threadIdx.x & (G - 1));
-    const int H = a.H, W = a.W, radius = a.radius, r2 = radius * radius;
+// ---- the outward march: T only, one thread per child ----
+
+__device__ __forceinline__ void ring_child(const Args &a, const Mode &m, int i, int c, float &tc, bool &tagged) {
+    const int H = a.H, W = a.W, b = m.b, sweep = m.sweep;
     const int y = c / W, x = c - y * W;
-    const int b = m.b, sweep = m.sweep;
-    const int oy = j - radius, qy = y + oy;
-    const bool rowin = j <= 2 * radius && qy >= 0 && qy < H;
-    const int64_t rowq = (int64_t)(rowin ? qy : y) * W;
-
-    Key me{0, 0, 0};
+    const int nbp[4] = {y > 0 ? c - W : -1, x > 0 ? c - 1 : -1, y < H - 1 ? c + W : -1, x < W - 1 ? c + 1 : -1};
+    unsigned long long me;
     if (sweep == 0) {
-        const int nbp[4] = {y > 0 ? c - W : -1, x > 0 ? c - 1 : -1, y < H - 1 ? c + W : -1, x < W - 1 ? c + 1 : -1};
-        me = parent_key(a, m, c, nbp);
+        me = parent_key(a, m, c);
+        a.key[c] = me;
+        a.par[c] = parent_word(c, W, me);
+        a.queued[c] = 0;
+        a.queued[a.n + c] = 0;
+    } else {
+        me = a.key[c];
+    }
+    int fq[4];
+    float tq[4];
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+        const int q = nbp[d] >= 0 ? nbp[d] : c;
+        fq[d] = a.fb[q];
+        tq[d] = a.T[q];
+    }
+    uint32_t less = sweep >= 2 ? a.lessm[(int64_t)i * kG] : 0u, intra = 0;
+#pragma unroll
+    for (int d = 0; d < 4; ++d) intra |= (uint32_t)(nbp[d] >= 0 && fq[d] == b) << d;
+    if (sweep == 1) {
+#pragma unroll
+        for (int d = 0; d < 4; ++d)
+            if ((intra >> d) & 1u) less |= (uint32_t)(a.key[nbp[d]] < me) << d;
+        a.lessm[(int64_t)i * kG] = (uint16_t)less;
+    }
+    const float Told = a.T[c];
+    tc = Told;
+    if (sweep == 1 && !less) return;  // no earlier child around: the sweep-0 result stands
+    bool av[4];
+    float tv[4];
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+        av[d] = nbp[d] < 0 || fq[d] < b || (fq[d] == b && ((less >> d) & 1u));
+        tv[d] = nbp[d] < 0 || !av[d] ? kFar : tq[d];
+    }
+    const float tp = arrival(tv[0], av[0], tv[1], av[1], tv[2], av[2], tv[3], av[3]);
+    tc = tp;
+    if (sweep != 0 && __float_as_uint(tp) == __float_as_uint(Told)) return;
+    a.T[c] = tp;
+    if (sweep == 0) return;
+    const uint32_t dep = intra & ~less;
+    const unsigned long long tag = (unsigned long long)m.nb << 32 | (unsigned)(sweep + 1);
+    unsigned long long *qn = a.queued + ((sweep + 1) & 1) * a.n;
+#pragma unroll
+    for (int d = 0; d < 4; ++d)
+        if ((dep >> d) & 1u) qn[nbp[d]] = tag;
+    tagged = tagged || dep != 0;
+}
+
+// ---- the inward march: Telea's value, kG lanes per child (lane j = window row j - RW) ----
+
+template <int RW>
+struct Win {
+    static constexpr int R = RW - 1;       // the disc radius
+    static constexpr int NC = 2 * RW + 1;  // window side: the disc and its gradients' neighbours
+    static constexpr int nd() {            // disc cells without the centre
+        int n = 0;
+        for (int dy = -R; dy <= R; ++dy)
+            for (int dx = -R; dx <= R; ++dx) n += (dx * dx + dy * dy <= R * R) && (dx || dy);
+        return n;
+    }
+    static constexpr int ND = nd();
+    struct Lds {
+        float v[NC * NC];  // value at this child's fill (current for available cells, the input else)
+        float t[NC * NC];  // T (unavailable cells and the padding: 1e6)
+        uint16_t av[NC];   // not INSIDE at this child's fill (the padding: known)
+        float4 term[ND];   // (w v, w gIx rx, w gIy ry, w) in row-major disc order
+    };
+};
+template <int RW>
+using WinLds = typename Win<RW == 0 ? 2 : RW>::Lds;
+
+template <int RW>
+__device__ void fill_child(const Args &a, const Mode &m, int i, int c, float &tc, bool &tagged, WinLds<RW> &L) {
+    using WN = Win<RW>;
+    constexpr int NC = WN::NC, R = WN::R, ND = WN::ND;
+    const int j = (int)(threadIdx.x & (kG - 1));
+    const int H = a.H, W = a.W, b = m.b, sweep = m.sweep;
+    const int y = c / W, x = c - y * W;
+    const int dy = j - RW, qy = y + dy;
+    const bool rowv = j < NC;
+    const bool rowin = rowv && qy >= 0 && qy < H;
+    const int qyc = rowin ? qy : y;
+    const int64_t rowq = (int64_t)qyc * W;
+    const float *inrow = a.in + (int64_t)qyc * a.pitch;
+
+    unsigned long long me;
+    if (sweep == 0) {
+        me = parent_key(a, m, c);
         if (j == 0) {
-            a.Tpar[c] = me.tp;
-            a.Tgp[c] = me.tg;
-            a.lowkey[c] = me.lo;
+            a.key[c] = me;
+            a.par[c] = parent_word(c, W, me);
             a.queued[c] = 0;
             a.queued[a.n + c] = 0;
         }
-    } else if (sweep == 1) {
-        me = load_key(a, c);
+    } else {
+        me = a.key[c];
     }
-    const double Told = a.T[c];
-    const float vold = a.out[c];
-    uint32_t less = sweep >= 2 ? a.lessm[(int64_t)i * G + j] : 0u;
+    const float Told = a.T[c], vold = a.out[c];
+    uint32_t less = sweep >= 2 && rowv ? a.lessm[(int64_t)i * kG + j] : 0u;
 
-    // the row's cells: fill bucket, T, value (and the fill keys in sweep 1), all loads in flight
-    int fq[NCELL];
-    double tq[NCELL];
-    float vq[NCELL];
-    uint32_t inw = 0;  // cells inside the disc and the image
+    // the row's cells: fill bucket, T, current value, input value; all loads in flight
+    int fq[NC];
+    float tq[NC], vq[NC], oq[NC];
+    uint32_t inw = 0;
 #pragma unroll
-    for (int cc = 0; cc < NCELL; ++cc) {
-        const int ox = cc - RM, qx = x + ox;
-        const int d2 = oy * oy + ox * ox;
-        const bool ok = rowin && qx >= 0 && qx < W && d2 > 0 && d2 <= r2;
-        const int64_t q = rowq + (qx < 0 ? 0 : (qx >= W ? W - 1 : qx));
-        fq[cc] = a.fb[q];
-        tq[cc] = a.T[q];
-        vq[cc] = a.out[q];
+    for (int cc = 0; cc < NC; ++cc) {
+        const int qx = x + cc - RW;
+        const bool ok = rowin && qx >= 0 && qx < W;
+        const int qxc = qx < 0 ? 0 : (qx >= W ? W - 1 : qx);
+        fq[cc] = a.fb[rowq + qxc];
+        tq[cc] = a.T[rowq + qxc];
+        vq[cc] = a.out[rowq + qxc];
+        oq[cc] = inrow[qxc];
         inw |= (uint32_t)ok << cc;
     }
-    // the centre cell (ox = 0, oy = 0) is outside the disc: d2 = 0
+    const uint32_t self = j == RW ? 1u << RW : 0u;
+    uint32_t intra = 0;
+#pragma unroll
+    for (int cc = 0; cc < NC; ++cc) intra |= (uint32_t)(((inw >> cc) & 1u) && fq[cc] == b) << cc;
+    intra &= ~self;
     if (sweep == 1) {
-        Key kq[NCELL];
+        unsigned long long kq[NC];
 #pragma unroll
-        for (int cc = 0; cc < NCELL; ++cc) {
-            const int ox = cc - RM, qx = x + ox;
-            const int64_t q = rowq + (qx < 0 ? 0 : (qx >= W ? W - 1 : qx));
-            // only this bucket's children need their keys (the loads wait for the fill-bucket words;
-            // C2 -3 %, C4 -4 % against loading every cell's)
-            kq[cc] = Key{0, 0, 0};
-            if (((inw >> cc) & 1u) && fq[cc] == b) kq[cc] = load_key(a, q);
-        }
+        for (int cc = 0; cc < NC; ++cc) kq[cc] = ((intra >> cc) & 1u) ? a.key[rowq + x + cc - RW] : ~0ull;
 #pragma unroll
-        for (int cc = 0; cc < NCELL; ++cc)
-            if (((inw >> cc) & 1u) && fq[cc] == b && key_less(kq[cc], me)) less |= 1u << cc;
-        a.lessm[(int64_t)i * G + j] = (uint16_t)less;
-    }
-    uint32_t avail = 0, intra = 0;
-#pragma unroll
-    for (int cc = 0; cc < NCELL; ++cc) {
-        const bool in = (inw >> cc) & 1u;
-        avail |= (uint32_t)(in && (fq[cc] < b || (fq[cc] == b && ((less >> cc) & 1u)))) << cc;
-        intra |= (uint32_t)(in && fq[cc] == b) << cc;
-        if (fq[cc] < 0) tq[cc] = 0.0;  // known pixels: T = 0 (not stored)
+        for (int cc = 0; cc < NC; ++cc)
+            if (((intra >> cc) & 1u) && kq[cc] < me) less |= 1u << cc;
+        if (rowv) a.lessm[(int64_t)i * kG + j] = (uint16_t)less;
     }
     tc = Told;
-    // sweep 1: a child with no earlier child in its disc keeps its sweep-0 result
-    if (sweep == 1) {
+    if (sweep == 1) {  // a child with no earlier child in its window keeps its sweep-0 result
         int any = less != 0;
 #pragma unroll
-        for (int o = 1; o < G; o <<= 1) {
-            const int other = __shfl_xor(any, o, G);  // every lane takes part: no short circuit
-            any = any | other;
-        }
+        for (int o = 1; o < kG; o <<= 1) any |= __shfl_xor(any, o, kG);
         if (!any) return;
     }
-
-    // ---- T and grad T from the 4-neighbours (centre rows), shuffled from the lanes that hold them ----
-    const int lc = radius;  // lane of the centre row
-    const double tcm = (avail >> RM) & 1u ? tq[RM] : 1e6;
-    const double tcl = (avail >> (RM - 1)) & 1u ? tq[RM - 1] : 1e6;
-    const double tcr = (avail >> (RM + 1)) & 1u ? tq[RM + 1] : 1e6;
-    const double tu = __shfl(tcm, lc - 1, G), tdn = __shfl(tcm, lc + 1, G);
-    const double tl = __shfl(tcl, lc, G), tr = __shfl(tcr, lc, G);
-    const bool ou = tu < 1e6, od = tdn < 1e6, ol = tl < 1e6, orr = tr < 1e6;
-    const double ta = telea_solve(tu, tl), tb = telea_solve(tdn, tl);
-    const double tc2 = telea_solve(tu, tr), td = telea_solve(tdn, tr);
-    const double m01 = ta < tb ? ta : tb, m23 = tc2 < td ? tc2 : td;
-    const double tp = m01 < m23 ? m01 : m23;
-    const double gx = (orr && ol) ? (tr - tl) * 0.5 : (orr ? tr - tp : (ol ? tp - tl : 0.0));
-    const double gy = (od && ou) ? (tdn - tu) * 0.5 : (od ? tdn - tp : (ou ? tp - tu : 0.0));
-
-    double rn = 0.0, rd = 0.0;
+    // stage the window: availability (the padding is known), the value at this fill, T
+    uint32_t avail = 0;
 #pragma unroll
-    for (int cc = 0; cc < NCELL; ++cc) {
-        const int ox = cc - RM;
-        const int d2 = oy * oy + ox * ox;
-        const double ry = (double)(-oy), rx = (double)(-ox);
-        const double w_dir = __builtin_fabs(ry * gy + rx * gx) / __builtin_sqrt((double)(d2 > 0 ? d2 : 1));
-        const double w_dst = 1.0 / (double)(d2 > 0 ? d2 : 1);
-        const double w_lev = 1.0 / (1.0 + __builtin_fabs(tq[cc] - tp));
-        double w = w_dir * w_dst * w_lev;
-        w = w > 1e-6 ? w : 1e-6;
-        const bool use = (avail >> cc) & 1u;
-        rn = use ? rn + w * (double)vq[cc] : rn;
-        rd = use ? rd + w : rd;
+    for (int cc = 0; cc < NC; ++cc) {
+        const bool in = (inw >> cc) & 1u;
+        const bool av = !in || fq[cc] < b || (fq[cc] == b && ((less >> cc) & 1u));
+        avail |= (uint32_t)av << cc;
+        if (rowv) {
+            L.v[j * NC + cc] = av ? vq[cc] : oq[cc];
+            L.t[j * NC + cc] = in && av ? tq[cc] : kFar;
+        }
     }
-    double num = 0.0, den = 0.0;
+    if (rowv) L.av[j] = (uint16_t)avail;
+    wave_lds_sync();
+
+    // T and grad T from the 4-neighbours (every lane: broadcast reads)
+    auto AV = [&](int wy, int wx) -> bool { return (L.av[wy] >> wx) & 1u; };
+    auto TT = [&](int wy, int wx) -> float { return L.t[wy * NC + wx]; };
+    auto VV = [&](int wy, int wx) -> float { return L.v[wy * NC + wx]; };
+    const bool fu = AV(RW - 1, RW), fl = AV(RW, RW - 1), fd = AV(RW + 1, RW), fr = AV(RW, RW + 1);
+    const float tu = TT(RW - 1, RW), tl = TT(RW, RW - 1), td = TT(RW + 1, RW), tr = TT(RW, RW + 1);
+    const float tp = arrival(tu, fu, tl, fl, td, fd, tr, fr);
+    const float gtx = fr ? (fl ? (tr - tl) * 0.5f : tr - tp) : (fl ? tp - tl : 0.0f);
+    const float gty = fd ? (fu ? (td - tu) * 0.5f : td - tp) : (fu ? tp - tu : 0.0f);
+
+    // this lane's disc row: the terms of its cells, zero where a cell does not count (adding an exact
+    // zero leaves every sum's bits unchanged: none of them can be -0)
+    if (dy >= -R && dy <= R) {
+        const int cy = qy;
+        const bool yin = cy >= 0 && cy < H;
+        // OpenCV's rows km (the cell's, one inwards in the first image row), kp + 1 (below), km - 1
+        // (above), kp (the cell's, one inwards in the last row), as window rows; likewise columns
+        auto wrow = [&](int r) { return (r < 0 ? 0 : (r > H - 1 ? H - 1 : r)) - y + RW; };
+        auto wcol = [&](int q) { return (q < 0 ? 0 : (q > W - 1 ? W - 1 : q)) - x + RW; };
+        const int rA = wrow(cy + (cy == 0)), rD = wrow(cy + 1 - (cy == H - 1)), rU = wrow(cy - 1 + (cy == 0)),
+                  rB = wrow(cy - (cy == H - 1));
+        // slot of this row's first disc cell: the disc cells of the rows above (centre skipped)
+        int hw = 0;
+        while ((hw + 1) * (hw + 1) + dy * dy <= R * R) ++hw;
+        int rowbase = 0;
+        for (int yy = -R; yy < dy; ++yy) {
+            int h = 0;
+            while ((h + 1) * (h + 1) + yy * yy <= R * R) ++h;
+            rowbase += 2 * h + 1 - (yy == 0);
+        }
+        const int wy = j;
 #pragma unroll
-    for (int q = 0; q < G; ++q) {  // rows past 2 radius add +0.0: exact
-        num = num + __shfl(rn, q, G);
-        den = den + __shfl(rd, q, G);
+        for (int dx = -R; dx <= R; ++dx) {
+            if (dx * dx + dy * dy > R * R || (dx == 0 && dy == 0)) continue;
+            const int cx = x + dx;
+            const int wx = dx + RW;
+            float4 term = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+            if (yin && cx >= 0 && cx < W && AV(wy, wx)) {
+                const int cA = wcol(cx + (cx == 0)), cR = wcol(cx + 1 - (cx == W - 1)), cL = wcol(cx - 1 + (cx == 0)),
+                          cB = wcol(cx - (cx == W - 1));
+                const float ry = (float)(-dy), rx = (float)(-dx);
+                const float vl = rx * rx + ry * ry;
+                const float dst = (float)(1.0 / ((double)vl * __builtin_sqrt((double)vl)));
+                const float lev = (float)(1.0 / (1.0 + __builtin_fabs((double)(TT(wy, wx) - tp))));
+                float dir = rx * gtx + ry * gty;
+                if (__builtin_fabs((double)dir) <= 0.01) dir = 0.000001f;
+                const float w = __builtin_fabsf(dst * lev * dir);
+                const bool ar = AV(wy, wx + 1), al = AV(wy, wx - 1), ad = AV(wy + 1, wx), au = AV(wy - 1, wx);
+                const float gix = ar ? (al ? (VV(rA, cR) - VV(rA, cL)) * 2.0f : VV(rA, cR) - VV(rA, cA))
+                                     : (al ? VV(rA, cB) - VV(rA, cL) : 0.0f);
+                const float giy = ad ? (au ? (VV(rD, cA) - VV(rU, cA)) * 2.0f : VV(rD, cA) - VV(rA, cA))
+                                     : (au ? VV(rB, cA) - VV(rU, cA) : 0.0f);
+                term = make_float4(w * VV(rA, cA), w * (gix * rx), w * (giy * ry), w);
+            }
+            L.term[rowbase + dx + hw - (dy == 0 && dx > 0)] = term;
+        }
     }
-    const float v = den > 0 ? (float)(num / den) : vold;
+    wave_lds_sync();
+    // OpenCV's sums in disc order (every lane the same: broadcast reads)
+    float Ia = 0.0f, Jx = 0.0f, Jy = 0.0f, s = 1.0e-20f;
+#pragma unroll
+    for (int q = 0; q < ND; ++q) {
+        const float4 t = L.term[q];
+        Ia = Ia + t.x;
+        Jx = Jx - t.y;
+        Jy = Jy - t.z;
+        s = s + t.w;
+    }
+    const double jn = __builtin_sqrt((double)(Jx * Jx + Jy * Jy)) + (double)1.0e-20f;
+    const float v = (float)((double)(Ia / s) + (double)(Jx + Jy) / jn + 0.5);
+    wave_lds_sync();  // the group's LDS is reused by its next child
     tc = tp;
-    const bool changed = sweep == 0 || __double_as_longlong(tp) != __double_as_longlong(Told) ||
-                         __float_as_int(v) != __float_as_int(vold);
+    const bool changed =
+        sweep == 0 || __float_as_uint(tp) != __float_as_uint(Told) || __float_as_uint(v) != __float_as_uint(vold);
     if (!changed) return;
     if (j == 0) {
         a.T[c] = tp;
         a.out[c] = v;
     }
     if (sweep == 0) return;  // sweep 1 visits every child anyway
-    // the children that read this one (this bucket's, filled later) are tagged for the next sweep in
-    // the word of its parity (this sweep reads the other one)
+    // the children that read this one (this bucket's, filled later) are tagged for the next sweep
     const uint32_t dep = intra & ~less;
     const unsigned long long tag = (unsigned long long)m.nb << 32 | (unsigned)(sweep + 1);
     unsigned long long *qn = a.queued + ((sweep + 1) & 1) * a.n;
 #pragma unroll
-    for (int cc = 0; cc < NCELL; ++cc) {
-        if ((dep >> cc) & 1u) {
-            const int qx = x + cc - RM;
-            qn[rowq + qx] = tag;
-        }
-    }
-    tagged = tagged || dep != 0;
+    for (int cc = 0; cc < NC; ++cc)
+        if ((dep >> cc) & 1u) qn[rowq + x + cc - RW] = tag;
+    int dany = dep != 0;
+#pragma unroll
+    for (int o = 1; o < kG; o <<= 1) dany |= __shfl_xor(dany, o, kG);
+    tagged = tagged || dany;
 }
 
-// Radii above 7: one thread per child, every row; availability from the fill keys each sweep and
+// Radii above 6: one thread per child, the window read from memory, availability from the fill keys,
 // every child in every sweep (until one changes nothing).
-__device__ __forceinline__ void sweep_child_wide(const Args &a, const Mode &m, int i, int c, bool &changed, double &tc) {
-    const int H = a.H, W = a.W, radius = a.radius, r2 = radius * radius;
+__device__ __forceinline__ bool avail_wide(const Args &a, int q, int b, bool keys, unsigned long long me) {
+    const int f = a.fb[q];
+    if (f < b) return true;
+    if (f != b || !keys) return false;
+    return a.key[q] < me;
+}
+__device__ void fill_child_wide(const Args &a, const Mode &m, int c, bool &changed, float &tc) {
+    const int H = a.H, W = a.W, b = m.b, R = a.radius;
     const int y = c / W, x = c - y * W;
-    const int b = m.b;
     const bool first = m.sweep == 0;
-    const int nbp[4] = {y > 0 ? c - W : -1, x > 0 ? c - 1 : -1, y < H - 1 ? c + W : -1, x < W - 1 ? c + 1 : -1};
-    Key me;
+    unsigned long long me;
     if (first) {
-        me = parent_key(a, m, c, nbp);
-        a.Tpar[c] = me.tp;
-        a.Tgp[c] = me.tg;
-        a.lowkey[c] = me.lo;
+        me = parent_key(a, m, c);
+        a.key[c] = me;
+        a.par[c] = parent_word(c, W, me);
     } else {
-        me = load_key(a, c);
+        me = a.key[c];
     }
-    const double Told = a.T[c];
-    const float vold = a.out[c];
-    double tn[4];
-    bool on[4];
-#pragma unroll
-    for (int d = 0; d < 4; ++d) {
-        const int p = nbp[d];
-        on[d] = false;
-        tn[d] = 1e6;
-        if (p < 0) continue;
-        const int f = a.fb[p];
-        if (filled_before(a, p, f, b, !first, me)) {
-            on[d] = true;
-            tn[d] = f < 0 ? 0.0 : a.T[p];
+    auto inimg = [&](int yy, int xx) { return yy >= 0 && yy < H && xx >= 0 && xx < W; };
+    auto AV = [&](int yy, int xx) -> bool {
+        if (!inimg(yy, xx)) return true;  // the padding is known
+        if (yy == y && xx == x) return false;
+        return avail_wide(a, yy * W + xx, b, !first, me);
+    };
+    auto TT = [&](int yy, int xx) -> float { return inimg(yy, xx) && AV(yy, xx) ? a.T[(int64_t)yy * W + xx] : kFar; };
+    auto OV = [&](int yy, int xx) -> float {  // image coordinates, clamped (1-row / 1-column images)
+        yy = yy < 0 ? 0 : (yy > H - 1 ? H - 1 : yy);
+        xx = xx < 0 ? 0 : (xx > W - 1 ? W - 1 : xx);
+        return AV(yy, xx) ? a.out[(int64_t)yy * W + xx] : a.in[(int64_t)yy * a.pitch + xx];
+    };
+    const float Told = a.T[c], vold = a.out[c];
+    const bool fu = AV(y - 1, x), fl = AV(y, x - 1), fd = AV(y + 1, x), fr = AV(y, x + 1);
+    const float tu = TT(y - 1, x), tl = TT(y, x - 1), td = TT(y + 1, x), tr = TT(y, x + 1);
+    const float tp = arrival(tu, fu, tl, fl, td, fd, tr, fr);
+    const float gtx = fr ? (fl ? (tr - tl) * 0.5f : tr - tp) : (fl ? tp - tl : 0.0f);
+    const float gty = fd ? (fu ? (td - tu) * 0.5f : td - tp) : (fu ? tp - tu : 0.0f);
+    float Ia = 0.0f, Jx = 0.0f, Jy = 0.0f, s = 1.0e-20f;
+    for (int dy = -R; dy <= R; ++dy) {
+        const int cy = y + dy;
+        for (int dx = -R; dx <= R; ++dx) {
+            const int cx = x + dx;
+            if (dx * dx + dy * dy > R * R || !inimg(cy, cx) || !AV(cy, cx)) continue;
+            const int rA = cy + (cy == 0), rD = cy + 1 - (cy == H - 1), rU = cy - 1 + (cy == 0), rB = cy - (cy == H - 1);
+            const int cA = cx + (cx == 0), cR = cx + 1 - (cx == W - 1), cL = cx - 1 + (cx == 0), cB = cx - (cx == W - 1);
+            const float ry = (float)(-dy), rx = (float)(-dx);
+            const float vl = rx * rx + ry * ry;
+            const float dst = (float)(1.0 / ((double)vl * __builtin_sqrt((double)vl)));
+            const float lev = (float)(1.0 / (1.0 + __builtin_fabs((double)(TT(cy, cx) - tp))));
+            float dir = rx * gtx + ry * gty;
+            if (__builtin_fabs((double)dir) <= 0.01) dir = 0.000001f;
+            const float w = __builtin_fabsf(dst * lev * dir);
+            const bool ar = AV(cy, cx + 1), al = AV(cy, cx - 1), ad = AV(cy + 1, cx), au = AV(cy - 1, cx);
+            const float gix = ar ? (al ? (OV(rA, cR) - OV(rA, cL)) * 2.0f : OV(rA, cR) - OV(rA, cA))
+                                 : (al ? OV(rA, cB) - OV(rA, cL) : 0.0f);
+            const float giy = ad ? (au ? (OV(rD, cA) - OV(rU, cA)) * 2.0f : OV(rD, cA) - OV(rA, cA))
+                                 : (au ? OV(rB, cA) - OV(rU, cA) : 0.0f);
+            Ia = Ia + w * OV(rA, cA);
+            Jx = Jx - w * (gix * rx);
+            Jy = Jy - w * (giy * ry);
+            s = s + w;
         }
     }
-    const double ta = telea_solve(tn[0], tn[1]), tb = telea_solve(tn[2], tn[1]);
-    const double tc2 = telea_solve(tn[0], tn[3]), td = telea_solve(tn[2], tn[3]);
-    const double m01 = ta < tb ? ta : tb, m23 = tc2 < td ? tc2 : td;
-    const double tp = m01 < m23 ? m01 : m23;
-    const bool ou = on[0], ol = on[1], od = on[2], orr = on[3];
-    const double tu = tn[0], tl = tn[1], tdn = tn[2], tr = tn[3];
-    const double gx = (orr && ol) ? (tr - tl) * 0.5 : (orr ? tr - tp : (ol ? tp - tl : 0.0));
-    const double gy = (od && ou) ? (tdn - tu) * 0.5 : (od ? tdn - tp : (ou ? tp - tu : 0.0));
-    double num = 0.0, den = 0.0;
-    for (int oy = -radius; oy <= radius; ++oy) {
-        double rn = 0.0, rd = 0.0;
-        for (int ox = -radius; ox <= radius; ++ox) {
-            const int qy = y + oy, qx = x + ox, d2 = oy * oy + ox * ox;
-            if (d2 == 0 || d2 > r2 || qy < 0 || qy >= H || qx < 0 || qx >= W) continue;
-            const int64_t q = (int64_t)qy * W + qx;
-            const int f = a.fb[q];
-            if (!filled_before(a, q, f, b, !first, me)) continue;
-            const double Tq = f < 0 ? 0.0 : a.T[q];
-            const double ry = (double)(-oy), rx = (double)(-ox);
-            const double w_dir = __builtin_fabs(ry * gy + rx * gx) / __builtin_sqrt((double)d2);
-            const double w_dst = 1.0 / (double)d2;
-            const double w_lev = 1.0 / (1.0 + __builtin_fabs(Tq - tp));
-            double w = w_dir * w_dst * w_lev;
-            w = w > 1e-6 ? w : 1e-6;
-            rn = rn + w * (double)a.out[q];
-            rd = rd + w;
-        }
-        num = num + rn;
-        den = den + rd;
-    }
-    const float v = den > 0 ? (float)(num / den) : vold;
+    const double jn = __builtin_sqrt((double)(Jx * Jx + Jy * Jy)) + (double)1.0e-20f;
+    const float v = (float)((double)(Ia / s) + (double)(Jx + Jy) / jn + 0.5);
     tc = tp;
-    changed = first || __double_as_longlong(tp) != __double_as_longlong(Told) || __float_as_int(v) != __float_as_int(vold);
+    changed = first || __float_as_uint(tp) != __float_as_uint(Told) || __float_as_uint(v) != __float_as_uint(vold);
     if (changed) {
         a.T[c] = tp;
         a.out[c] = v;
     }
 }
 
-// POP: entries of F[lsel] (nIn) then C[lsel] (nPrev); T < bound pops (marks children), the rest
-// survives into F[lsel^1].  T of a known seed is 0.  A block round takes as many entries as the block
-// has groups (<= 4 children each, one sweep-0 pass for the usual 1-2), appends its survivors and the
-// children it marked with one 64-bit counter add, and runs sweep 0 of those children right there
-// (their parent and fill key, T and value from the pixels filled before the bucket): the pops, and
-// so every child's parent, are fixed for the whole step, and sweep 0 reads no child of the bucket.
-template <int G>
-__device__ void do_pop(const Args &a, const Mode &m, State &N, int blk, int nblk) {
+// POP: entries of F[lsel] (nIn) then C[lsel] (nPrev); T < bound pops (marks children, joins the pop
+// list with its push key and rank base), the rest survives into F[lsel^1].  A block round takes one
+// entry per thread, appends survivors and children with ONE 64-bit counter add and the pops with one
+// add, and runs sweep 0 of its children right there (the pops, and so every child's parent, are fixed
+// for the whole step, and sweep 0 reads no child of the bucket).
+template <int RW>
+__device__ void do_pop(const Args &a, const Mode &m, State &N, int blk, int nblk, WinLds<RW> *lds) {
     const int *Fi = a.F[m.lsel], *Ci = a.C[m.lsel];
     int *Fo = a.F[m.lsel ^ 1], *Co = a.C[m.lsel ^ 1];
     const int tot = m.nIn + m.nPrev;
     const int W = a.W, H = a.H;
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     __shared__ int kidc[1024], kidi[1024];
-    __shared__ int wsumF[4], wsumK[4], kbaseF, kbaseK;
+    __shared__ int wsumF[4], wsumK[4], wsumP[4], kbaseF, kbaseK, kbaseP;
     Mode m0 = m;
     m0.what = kPhSweep;
     m0.sweep = 0;
     unsigned long long mn = ~0ull, mnc = ~0ull;
-    constexpr int chunk = G > 0 ? 256 / G : 256;
-    for (int base = blk * chunk; base < tot; base += nblk * chunk) {  // block-uniform trip count
+    for (int base = blk * 256; base < tot; base += nblk * 256) {  // block-uniform trip count
         const int i = base + (int)threadIdx.x;
-        int keep = 0, p = 0;
-        unsigned km = 0;  // the directions whose neighbour this pop marked (no dynamic register index)
+        int keep = 0, popd = 0, p = 0;
+        unsigned km = 0;  // the directions whose neighbour this pop marked
         int nb[4] = {-1, -1, -1, -1};
-        if ((int)threadIdx.x < chunk && i < tot) {
+        if (i < tot) {
             p = i < m.nIn ? Fi[i] : Ci[i - m.nIn];
             const int y = p / W, x = p - y * W;
             nb[0] = y > 0 ? p - W : -1;
@@ -625,48 +737,55 @@ __device__ void do_pop(const Args &a, const Mode &m, State &N, int blk, int nblk
             int fn[4];
 #pragma unroll
             for (int d = 0; d < 4; ++d) fn[d] = a.fb[nb[d] >= 0 ? nb[d] : p];
-            const double t = a.fb[p] < 0 ? 0.0 : a.T[p];
-            if (t < m.bound) {
-                // the marks of the INSIDE neighbours issue together (their results are read after)
+            const float t = a.T[p];
+            if ((double)t < m.bound) {
+                popd = 1;
                 int old[4] = {0, 0, 0, 0};
 #pragma unroll
                 for (int d = 0; d < 4; ++d)
                     if (nb[d] >= 0 && fn[d] == kInside) old[d] = atomicCAS(&a.fb[nb[d]], kInside, m.b);
 #pragma unroll
                 for (int d = 0; d < 4; ++d) km |= (uint32_t)(nb[d] >= 0 && fn[d] == kInside && old[d] == kInside) << d;
+                // its push key (ranked in sweep 1 by (T, push key)) and rank base
+                a.pk[p] = pushkey_of(a, p, a.fb[p]);
+                a.rank[p] = (unsigned)m.base;
             } else {
                 keep = 1;
-                const unsigned long long tb = dbits(t);
+                const unsigned long long tb = dbits((double)t);
                 mn = tb < mn ? tb : mn;
             }
         }
-        // survivors and children: block-wide positions, one counter add for both lists
-        int tf, tk;
+        int tf, tk, tpp;
         const int ef = wave_excl_scan(keep, tf);
         const int ek = wave_excl_scan(__popc(km), tk);
+        const int ep = wave_excl_scan(popd, tpp);
         if (lane == 0) {
             wsumF[wv] = tf;
             wsumK[wv] = tk;
+            wsumP[wv] = tpp;
         }
         __syncthreads();
-        int woffF = 0, woffK = 0, btotF = 0, btot = 0;
+        int woffF = 0, woffK = 0, woffP = 0, btotF = 0, btot = 0, btotP = 0;
 #pragma unroll
         for (int w = 0; w < 4; ++w) {
             woffF += w < wv ? wsumF[w] : 0;
             woffK += w < wv ? wsumK[w] : 0;
+            woffP += w < wv ? wsumP[w] : 0;
             btotF += wsumF[w];
             btot += wsumK[w];
+            btotP += wsumP[w];
         }
         if (threadIdx.x == 0) {
             unsigned long long old = 0;
             if (btotF | btot)
-                old = atomicAdd(reinterpret_cast<unsigned long long *>(&N.nF),
-                                (unsigned long long)btot << 32 | (unsigned)btotF);
+                old = atomicAdd(reinterpret_cast<unsigned long long *>(&N.nF), (unsigned long long)btot << 32 | (unsigned)btotF);
             kbaseF = (int)(unsigned)old;
             kbaseK = (int)(old >> 32);
+            kbaseP = btotP ? atomicAdd(&N.nP, btotP) : 0;
         }
         __syncthreads();
         if (keep) Fo[kbaseF + woffF + ef] = p;
+        if (popd) a.P[kbaseP + woffP + ep] = p;
         const int gb = kbaseK;
 #pragma unroll
         for (int d = 0; d < 4; ++d) {
@@ -678,22 +797,29 @@ __device__ void do_pop(const Args &a, const Mode &m, State &N, int blk, int nblk
             }
         }
         __syncthreads();
-        if constexpr (G > 0) {
-            constexpr int per = 256 / G;
-            const int g = (int)threadIdx.x / G;
-            for (int k = g; k < btot; k += per) {  // group-uniform
-                bool tagged = false;
-                double tc;
-                sweep_child<G>(a, m0, kidi[k], kidc[k], tc, tagged);
-                const unsigned long long tb = dbits(tc);
+        if (m.march == 0) {
+            for (int k = threadIdx.x; k < btot; k += 256) {
+                bool tg = false;
+                float tc;
+                ring_child(a, m0, kidi[k], kidc[k], tc, tg);
+                const unsigned long long tb = dbits((double)tc);
+                mnc = tb < mnc ? tb : mnc;
+            }
+        } else if constexpr (RW > 0) {
+            const int g = (int)threadIdx.x / kG;
+            for (int k = g; k < btot; k += kPer) {  // group-uniform
+                bool tg = false;
+                float tc;
+                fill_child<RW>(a, m0, kidi[k], kidc[k], tc, tg, lds[g]);
+                const unsigned long long tb = dbits((double)tc);
                 mnc = tb < mnc ? tb : mnc;
             }
         } else {
             for (int k = threadIdx.x; k < btot; k += 256) {
                 bool ch;
-                double tc;
-                sweep_child_wide(a, m0, kidi[k], kidc[k], ch, tc);
-                const unsigned long long tb = dbits(tc);
+                float tc;
+                fill_child_wide(a, m0, kidc[k], ch, tc);
+                const unsigned long long tb = dbits((double)tc);
                 mnc = tb < mnc ? tb : mnc;
             }
         }
@@ -703,43 +829,88 @@ __device__ void do_pop(const Args &a, const Mode &m, State &N, int blk, int nblk
     block_min_to(mnc, &a.ctl->minC[m.nb % 3][blk % kMinSlots]);
 }
 
+// Dense ranks of this bucket's pops by (T, push key): rank = base + the number of pops with a
+// smaller key.  Pairs (chunk ci, chunk cj) of 256 pops: chunk cj's keys in LDS, each thread counts
+// those below its own pop's key and adds the count (the POP wrote the base).
+__device__ void do_rank(const Args &a, const Mode &m, int blk, int nblk) {
+    const int np = m.nP;
+    const int nch = (np + 255) / 256;
+    __shared__ unsigned long long kc[256];
+    for (int pr = blk; pr < nch * nch; pr += nblk) {  // block-uniform
+        const int ci = pr / nch, cj = pr - ci * nch;
+        const int jj = cj * 256 + (int)threadIdx.x;
+        unsigned long long kj = ~0ull;
+        if (jj < np) {
+            const int q = a.P[jj];
+            kj = (unsigned long long)__float_as_uint(a.T[q]) << 32 | a.pk[q];
+        }
+        kc[threadIdx.x] = kj;
+        const int ii = ci * 256 + (int)threadIdx.x;
+        int p = -1;
+        unsigned long long ki = 0;
+        if (ii < np) {
+            p = a.P[ii];
+            ki = (unsigned long long)__float_as_uint(a.T[p]) << 32 | a.pk[p];
+        }
+        __syncthreads();
+        if (p >= 0) {
+            unsigned cnt = 0;
+            const int lim = np - cj * 256 < 256 ? np - cj * 256 : 256;
+            for (int u = 0; u < lim; ++u) cnt += kc[u] < ki;
+            if (cnt) atomicAdd(&a.rank[p], cnt);
+        }
+        __syncthreads();
+    }
+}
+
 // SWEEP (m.sweep >= 1) over the bucket's children C[lsel]: every one (full), or the ones tagged for
-// this sweep (a group checks its position's tag).
-template <int G>
-__device__ void do_sweep(const Args &a, const Mode &m, unsigned *tagw, int blk, int nblk) {
+// this sweep (a child's group checks its tag).  Sweep 1 also ranks the bucket's pops.
+template <int RW>
+__device__ void do_sweep(const Args &a, const Mode &m, unsigned *tagw, int blk, int nblk, WinLds<RW> *lds) {
     const int *Cl = a.C[m.lsel];
     unsigned long long mn = ~0ull;
     bool tagged = false;
-    if constexpr (G > 0) {
-        constexpr int per = 256 / G;
-        const int g = (int)threadIdx.x / G;
-        const unsigned long long want = (unsigned long long)m.nb << 32 | (unsigned)m.sweep;
-        const unsigned long long *qin = a.queued + (m.sweep & 1) * a.n;
-        // one child per group and block round, so a block's tagged children take one pass whatever
-        // their clustering (children of one pop sit at adjacent positions)
-        for (int base = blk * per; base < m.nIn; base += nblk * per) {  // block-uniform trip count
-            const int i = base + g;
-            const int c = i < m.nIn ? Cl[i] : 0;
-            if (i < m.nIn && (m.full || qin[c] == want)) {  // group-uniform
-                double t;
-                sweep_child<G>(a, m, i, c, t, tagged);
-                const unsigned long long tb = dbits(t);
-                mn = tb < mn ? tb : mn;
-            }
-        }
-    } else {
+    const unsigned long long want = (unsigned long long)m.nb << 32 | (unsigned)m.sweep;
+    const unsigned long long *qin = a.queued + (m.sweep & 1) * a.n;
+    if (m.march == 0 || RW == 0) {
         for (int base = blk * 256; base < m.nIn; base += nblk * 256) {  // block-uniform
             const int i = base + (int)threadIdx.x;
             if (i < m.nIn) {
-                bool ch;
-                double t;
-                sweep_child_wide(a, m, i, Cl[i], ch, t);
-                tagged = tagged || ch;
-                const unsigned long long tb = dbits(t);
+                const int c = Cl[i];
+                float t = 0.0f;
+                bool run = false;
+                if (m.march == 0) {
+                    if (m.full || qin[c] == want) {
+                        ring_child(a, m, i, c, t, tagged);
+                        run = true;
+                    }
+                } else {
+                    bool ch;
+                    fill_child_wide(a, m, c, ch, t);
+                    tagged = tagged || ch;
+                    run = true;
+                }
+                if (run) {
+                    const unsigned long long tb = dbits((double)t);
+                    mn = tb < mn ? tb : mn;
+                }
+            }
+        }
+    } else if constexpr (RW > 0) {
+        const int g = (int)threadIdx.x / kG;
+        // one child per group and block round, so a block's tagged children take one pass
+        for (int base = blk * kPer; base < m.nIn; base += nblk * kPer) {  // block-uniform
+            const int i = base + g;
+            const int c = i < m.nIn ? Cl[i] : 0;
+            if (i < m.nIn && (m.full || qin[c] == want)) {  // group-uniform
+                float t;
+                fill_child<RW>(a, m, i, c, t, tagged, lds[g]);
+                const unsigned long long tb = dbits((double)t);
                 mn = tb < mn ? tb : mn;
             }
         }
     }
+    if (m.sweep == 1 && m.rank_on && m.nP > 0) do_rank(a, m, blk, nblk);
     if (__syncthreads_or(tagged) && threadIdx.x == 0)
         __hip_atomic_store(tagw + blk % kMinSlots, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     // T of a child only falls over the sweeps (more neighbours filled before it), so the minimum of
@@ -747,20 +918,58 @@ __device__ void do_sweep(const Args &a, const Mode &m, unsigned *tagw, int blk, 
     block_min_to(mn, &a.ctl->minC[m.nb % 3][blk % kMinSlots]);
 }
 
+// SWITCH (the outward march is done): negate T of every pixel it popped (the band and the ring pixels
+// it reached), mark the holes INSIDE, and list the inward march's first bucket - the holes with a
+// known 4-neighbour (every band pixel is a seed that pops at bound 0.7) - in C[0].
+__device__ void do_switch(const Args &a, State &N, int blk, int nblk) {
+    const int H = a.H, W = a.W;
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    __shared__ int wsum[4], bbase;
+    for (int64_t base = (int64_t)blk * 256; base < a.n; base += (int64_t)nblk * 256) {  // block-uniform
+        const int64_t p = base + threadIdx.x;
+        bool kid = false;
+        if (p < a.n) {
+            const int y = (int)(p / W), x = (int)(p - (int64_t)y * W);
+            const uint8_t c = a.cls[p];
+            if (c == kClsBand || (c == kClsRing && a.fb[p] != kInside)) a.T[p] = -a.T[p];
+            const bool hole = c == kClsHole;
+            if (hole)
+                kid = (y > 0 && a.cls[p - W] != kClsHole) | (y < H - 1 && a.cls[p + W] != kClsHole) |
+                      (x > 0 && a.cls[p - 1] != kClsHole) | (x < W - 1 && a.cls[p + 1] != kClsHole);
+            a.fb[p] = hole ? (kid ? 1 : kInside) : -1;
+        }
+        const unsigned long long m = __ballot(kid);
+        if (lane == 0) wsum[wv] = __popcll(m);
+        __syncthreads();
+        int woff = 0, btot = 0;
+#pragma unroll
+        for (int w = 0; w < 4; ++w) {
+            woff += w < wv ? wsum[w] : 0;
+            btot += wsum[w];
+        }
+        if (threadIdx.x == 0) bbase = btot ? atomicAdd(&N.nC, btot) : 0;
+        __syncthreads();
+        if (kid) a.C[0][bbase + woff + __popcll(m & ((1ull << lane) - 1))] = (int)p;
+        __syncthreads();
+    }
+}
+
 // Step s: returns the mode it ran (kPhDone: the march had finished).
-template <int G>
+template <int RW>
 __device__ int step(const Args &a, unsigned s, int blk, int nblk) {
+    __shared__ WinLds<RW> lds[RW > 0 ? kPer : 1];  // one child window per lane group (inward sweeps)
     Ctl *ctl = a.ctl;
     const State S = ctl->st[s % 3];
     const int lane = threadIdx.x & 63;
     const unsigned long long mcv = lane < 3 * kMinSlots ? (&ctl->minC[0][0])[lane] : ~0ull;
     const unsigned tg = lane < kMinSlots ? ctl->tagged[s % 3][lane] : 0u;
     State &N = ctl->st[(s + 1) % 3];
-    const Mode m = decide<G>(S, mcv, __ballot(tg != 0u) != 0ull);
+    const Mode m = decide<RW>(S, mcv, __ballot(tg != 0u) != 0ull);
     if (blk == 0 && threadIdx.x == 0) {
         State &Z = ctl->st[(s + 2) % 3];
         Z.nF = 0;
         Z.nC = 0;
+        Z.nP = 0;
         for (int q = 0; q < kMinSlots; ++q) ctl->tagged[(s + 2) % 3][q] = 0u;
         Z.minF = ~0ull;
         N.phase = m.what;
@@ -769,14 +978,31 @@ __device__ int step(const Args &a, unsigned s, int blk, int nblk) {
         N.nb = m.nb;
         N.sweep = m.sweep;
         N.bound = m.bound;
+        N.march = m.march;
+        N.base = m.base;
+        N.rank_on = m.rank_on;
         if (m.what == kPhSweep) {  // carried: the POP's outputs
             N.lsel = m.lsel;
             N.nF = S.nF;
             N.nC = S.nC;
+            N.nP = S.nP;
             N.minF = S.minF;
         } else if (m.what == kPhPop) {
             N.lsel = m.lsel ^ 1;
             // the next bucket's accumulator (this step reads slot nb-1 and fills slot nb)
+            for (int q = 0; q < kMinSlots; ++q) ctl->minC[(m.nb + 1) % 3][q] = ~0ull;
+        } else if (m.what == kPhSwitch) {
+            // the next step starts the inward march at its bucket 1 (listed into C[0] by this step)
+            N.phase = kPhInit;
+            N.march = 1;
+            N.k = 1;
+            N.b = 1;
+            N.nb = m.nb + 1;
+            N.sweep = 0;
+            N.lsel = 0;
+            N.bound = kDelta;
+            N.base = (int)a.n;
+            N.rank_on = 0;
             for (int q = 0; q < kMinSlots; ++q) ctl->minC[(m.nb + 1) % 3][q] = ~0ull;
         } else {
             N.lsel = m.lsel;
@@ -784,14 +1010,15 @@ __device__ int step(const Args &a, unsigned s, int blk, int nblk) {
                 __hip_atomic_store(a.host + kHostSteps, (int)s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         }
     }
-    if (m.what == kPhPop) do_pop<G>(a, m, N, blk, nblk);
-    else if (m.what == kPhSweep) do_sweep<G>(a, m, ctl->tagged[(s + 1) % 3], blk, nblk);
+    if (m.what == kPhPop) do_pop<RW>(a, m, N, blk, nblk, lds);
+    else if (m.what == kPhSweep) do_sweep<RW>(a, m, ctl->tagged[(s + 1) % 3], blk, nblk, lds);
+    else if (m.what == kPhSwitch) do_switch(a, N, blk, nblk);
     return m.what;
 }
 
-template <int G>
+template <int RW>
 __global__ __launch_bounds__(256) void tl_step(Args a, unsigned s) {
-    step<G>(a, s, blockIdx.x, gridDim.x);
+    step<RW>(a, s, blockIdx.x, gridDim.x);
 }
 
 // Grid barrier: every wave drains its stores, lane 0 of the block releases them to the device
@@ -831,11 +1058,11 @@ __device__ __forceinline__ bool grid_barrier(unsigned *ctr, unsigned *gen, unsig
     return ok;
 }
 
-// The steps from s0 on, in ONE persistent launch (cooperative: the runtime refuses it unless every
-// block is co-resident), a grid barrier per step.  Exits at once when the step launches finished the
-// march.  A barrier timeout (or the step cap) leaves holes unfilled and raises the workspace's sticky
-// flag in mapped host memory, which the next hole-filling call on it and the status queries report.
-template <int G>
+// The steps from s0 on, in ONE persistent launch (one block per CU, all co-resident), a grid
+// barrier per step.  Exits at once when the step launches finished the march.  A barrier timeout (or
+// the step cap) leaves holes unfilled and raises the workspace's sticky flag in mapped host memory,
+// which the next hole-filling call on it and the status queries report.
+template <int RW>
 __global__ __launch_bounds__(256) void tl_tail(Args a, unsigned s0) {
     unsigned epoch = 0;
     for (unsigned s = s0;; ++s) {
@@ -844,7 +1071,7 @@ __global__ __launch_bounds__(256) void tl_tail(Args a, unsigned s0) {
                 __hip_atomic_store(a.host + kHostTmo, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             return;
         }
-        if (step<G>(a, s, blockIdx.x, gridDim.x) == kPhDone) return;  // grid-uniform
+        if (step<RW>(a, s, blockIdx.x, gridDim.x) == kPhDone) return;  // grid-uniform
         ++epoch;
         if (!grid_barrier(&a.ctl->bar, &a.ctl->gen, epoch, gridDim.x, &a.ctl->tmo, a.spin_limit)) {
             if (threadIdx.x == 0 && a.host) __hip_atomic_store(a.host + kHostTmo, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -864,7 +1091,7 @@ hipError_t dbg_sync(const char *what, hipStream_t st) {
     return e;
 }
 
-Args views(void *ws, int H, int W, int G) {
+Args views(void *ws, int H, int W) {
     const size_t n = (size_t)H * W;
     uint8_t *w = static_cast<uint8_t *>(ws);
     Args a{};
@@ -872,24 +1099,31 @@ Args views(void *ws, int H, int W, int G) {
     w += align256(sizeof(Ctl));
     a.fb = reinterpret_cast<int *>(w);
     w += align256(n * 4);
-    a.T = reinterpret_cast<double *>(w);
+    a.T = reinterpret_cast<float *>(w);
+    w += align256(n * 4);
+    a.key = reinterpret_cast<unsigned long long *>(w);
     w += align256(n * 8);
-    a.Tpar = reinterpret_cast<double *>(w);
-    w += align256(n * 8);
-    a.Tgp = reinterpret_cast<double *>(w);
-    w += align256(n * 8);
-    a.lowkey = reinterpret_cast<unsigned long long *>(w);
-    w += align256(n * 8);
+    a.pk = reinterpret_cast<unsigned *>(w);
+    w += align256(n * 4);
+    a.rank = reinterpret_cast<unsigned *>(w);
+    w += align256(n * 4);
+    a.par = reinterpret_cast<unsigned *>(w);
+    w += align256(n * 4);
     a.queued = reinterpret_cast<unsigned long long *>(w);
     w += align256(2 * n * 8);
     a.lessm = reinterpret_cast<uint16_t *>(w);
-    w += align256(n * 2 * (size_t)(G > 0 ? G : 1));
+    w += align256(n * 2 * (size_t)kG);
     for (int i = 0; i < 2; ++i) {
         a.F[i] = reinterpret_cast<int *>(w);
         w += align256(n * 4);
         a.C[i] = reinterpret_cast<int *>(w);
         w += align256(n * 4);
     }
+    a.P = reinterpret_cast<int *>(w);
+    w += align256(n * 4);
+    a.cls = w;
+    w += align256(n);
+    a.rowd = w;
     a.H = H;
     a.W = W;
     a.n = (int64_t)n;
@@ -933,19 +1167,19 @@ DeviceInfo &device_info(int dev) {
     return info[dev];
 }
 
-template <int G>
-hipError_t run_march(const float *in, int64_t pitch, Args a, int ncu, int *hw, const InpaintOpts &o, hipStream_t st) {
+template <int RW>
+hipError_t run_march(Args a, int ncu, int *hw, const InpaintOpts &o, hipStream_t st) {
     hipError_t e;
-    const size_t n = (size_t)a.H * a.W;
     if ((e = hipMemsetAsync(a.ctl, 0, sizeof(Ctl), st)) != hipSuccess) return e;
-    const int ib = (int)((n + kInitChunk - 1) / kInitChunk);
-    hipLaunchKernelGGL(tl_init, dim3(ib), dim3(256), 0, st, in, pitch, a);
-    if ((e = dbg_sync("tl_init", st)) != hipSuccess) return e;
-    if (a.radius < 1) return hipSuccess;  // no neighbourhood: nothing changes (cv2 uses radius >= 1)
+    const int ib = (int)((a.n + 255) / 256);
+    hipLaunchKernelGGL(tl_init_a, dim3(ib), dim3(256), 0, st, a);
+    if ((e = dbg_sync("tl_init_a", st)) != hipSuccess) return e;
+    hipLaunchKernelGGL(tl_init_b, dim3(ib), dim3(256), 0, st, a);
+    if ((e = dbg_sync("tl_init_b", st)) != hipSuccess) return e;
     // step launches: as many as the previous call on this workspace needed (+3); the persistent
     // kernel takes whatever is left
     const int prev = hw ? __atomic_load_n(hw + kHostSteps, __ATOMIC_RELAXED) : -1;
-    int nsteps = prev < 0 ? 48 : prev + 3;
+    int nsteps = prev < 0 ? 64 : prev + 3;
     if (o.steps >= 0) nsteps = o.steps;
     const bool trace = getenv("DSX_INPAINT_TRACE") != nullptr;  // debugging: the state and time of each step
     hipEvent_t e0 = nullptr, e1 = nullptr;
@@ -955,7 +1189,7 @@ hipError_t run_march(const float *in, int64_t pitch, Args a, int ncu, int *hw, c
     }
     for (int s = 0; s < nsteps; ++s) {
         if (trace) (void)hipEventRecord(e0, st);
-        hipLaunchKernelGGL(tl_step<G>, dim3(kStepBlocks), dim3(256), 0, st, a, (unsigned)s);
+        hipLaunchKernelGGL(tl_step<RW>, dim3(kStepBlocks), dim3(256), 0, st, a, (unsigned)s);
         if ((e = dbg_sync("tl_step", st)) != hipSuccess) return e;
         if (trace) {
             (void)hipEventRecord(e1, st);
@@ -965,17 +1199,29 @@ hipError_t run_march(const float *in, int64_t pitch, Args a, int ncu, int *hw, c
                 return e;
             float ms = 0;
             (void)hipEventElapsedTime(&ms, e0, e1);
-            fprintf(stderr, "step %d: %.1f us phase %d k %d b %d sweep %d lsel %d nF %d nC %d bound %.3f\n", s,
-                    ms * 1e3f, S.phase, S.k, S.b, S.sweep, S.lsel, S.nF, S.nC, S.bound);
+            fprintf(stderr, "step %d: %.1f us march %d phase %d k %d b %d sweep %d lsel %d nF %d nC %d nP %d bound %.3f\n", s,
+                    ms * 1e3f, S.march, S.phase, S.k, S.b, S.sweep, S.lsel, S.nF, S.nC, S.nP, S.bound);
             if (S.phase == kPhDone) break;
         }
     }
-    if (getenv("DSX_INPAINT_NO_TAIL")) return hipSuccess;  // profiling only (rocprofv3 and cooperative launches)
-    unsigned s0 = (unsigned)nsteps;
-    void *args[] = {&a, &s0};
-    if ((e = hipLaunchCooperativeKernel(reinterpret_cast<const void *>(tl_tail<G>), dim3(ncu), dim3(256), args, 0, st)) !=
-        hipSuccess)
-        return e;
+    if (getenv("DSX_INPAINT_NO_TAIL")) return hipSuccess;  // profiling only
+    // One block per CU: every block is resident at once (the kernel fits a CU: checked once per
+    // device), which the grid barrier needs.  A plain launch, not hipLaunchCooperativeKernel: the
+    // runtime's exit-time teardown of its cooperative-launch resources faulted inside
+    // libhsa-runtime64 under rocprofv3 (tools/exit_probe.py: the same march without its cooperative
+    // tail exits 0; profiles/README.md).  A block that waits beyond the spin limit still leaves and
+    // flags the timeout.
+    static std::once_flag occ_once[64];
+    static int occ_ok[64];
+    int dev = 0;
+    if ((e = hipGetDevice(&dev)) != hipSuccess) return e;
+    std::call_once(occ_once[dev & 63], [&] {
+        int nb = 0;
+        occ_ok[dev & 63] = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, reinterpret_cast<const void *>(tl_tail<RW>), 256,
+                                                                          0) == hipSuccess && nb >= 1;
+    });
+    if (!occ_ok[dev & 63]) return hipErrorCooperativeLaunchTooLarge;
+    hipLaunchKernelGGL(tl_tail<RW>, dim3(ncu), dim3(256), 0, st, a, (unsigned)nsteps);
     return dbg_sync("tl_tail", st);
 }
 
@@ -983,32 +1229,39 @@ hipError_t run_march(const float *in, int64_t pitch, Args a, int ncu, int *hw, c
 
 size_t inpaint_workspace(int H, int W) {
     const size_t n = (size_t)H * W;
-    // the widest layout (G = 16 row masks); radius <= 3 uses half of the mask area
-    return align256(sizeof(Ctl)) + align256(n * 4) + 4 * align256(n * 8) + align256(2 * n * 8) + align256(n * 2 * 16) +
-           4 * align256(n * 4);
+    return align256(sizeof(Ctl)) + 6 * align256(n * 4) + align256(n * 8) + align256(2 * n * 8) +
+           align256(n * 2 * (size_t)kG) + 4 * align256(n * 4) + 2 * align256(n);
 }
 
 hipError_t launch_inpaint(const float *in, int64_t pitch, int H, int W, int radius, float *out, void *ws, hipStream_t st,
                           const InpaintOpts &o) {
-    if ((int64_t)H * W >= kInpaintMaxPixels) return hipErrorInvalidValue;  // 30-bit pixel indices in the keys
+    if ((int64_t)H * W >= kInpaintMaxPixels) return hipErrorInvalidValue;  // ranks * 4 in 30 bits of the keys
     int dev = 0;
     hipError_t e;
     if ((e = hipGetDevice(&dev)) != hipSuccess) return e;
     if (dev < 0 || dev >= 64) return hipErrorInvalidDevice;
     const DeviceInfo &di = device_info(dev);
     if (di.err != hipSuccess) return di.err;
-    const int G = radius <= 3 ? 8 : radius <= 7 ? 16 : 0;
-    Args a = views(ws, H, W, G);
+    radius = radius < 1 ? 1 : (radius > 100 ? 100 : radius);  // cv2.inpaint's range clamp
+    Args a = views(ws, H, W);
     a.out = out;
+    a.in = in;
+    a.pitch = pitch;
     a.radius = radius;
     int *hw = host_words(o.status_key ? o.status_key : ws);
     a.host = nullptr;
     if (hw && hipHostGetDevicePointer(reinterpret_cast<void **>(&a.host), hw, 0) != hipSuccess) a.host = nullptr;
     a.spin_limit = o.spin_limit ? o.spin_limit : (1u << 23);
-    int rb = di.ncu;
-    if (radius <= 3) return run_march<8>(in, pitch, a, rb, hw, o, st);
-    if (radius <= 7) return run_march<16>(in, pitch, a, rb, hw, o, st);
-    return run_march<0>(in, pitch, a, rb, hw, o, st);
+    const int rb = di.ncu;
+    switch (radius) {
+        case 1: return run_march<2>(a, rb, hw, o, st);
+        case 2: return run_march<3>(a, rb, hw, o, st);
+        case 3: return run_march<4>(a, rb, hw, o, st);
+        case 4: return run_march<5>(a, rb, hw, o, st);
+        case 5: return run_march<6>(a, rb, hw, o, st);
+        case 6: return run_march<7>(a, rb, hw, o, st);
+        default: return run_march<0>(a, rb, hw, o, st);
+    }
 }
 
 int inpaint_take_timeout(const void *key) {
@@ -1021,6 +1274,18 @@ int inpaint_take_timeout_any() {
     int any = 0;
     for (auto &kv : words_map()) any |= __atomic_exchange_n(kv.second + kHostTmo, 0, __ATOMIC_ACQ_REL);
     return any;
+}
+
+bool inpaint_has_words() {
+    std::lock_guard<std::mutex> lk(g_words_mu);
+    return !words_map().empty();
+}
+
+void inpaint_forget_all() {
+    std::lock_guard<std::mutex> lk(g_words_mu);
+    auto &m = words_map();
+    for (auto &kv : m) (void)hipHostFree(kv.second);
+    m.clear();
 }
 
 void inpaint_forget(const void *key) {

@@ -205,7 +205,7 @@ bool post_full_two_launch(const PostFullArgs &a);
 // arrival-time order (T-buckets, fixed-point sweeps).  Asynchronous: nothing is read back to the host.
 size_t inpaint_workspace(int H, int W);
 constexpr int kInpaintMaxW = 1 << 20;              // no row staging: only the pixel count is bounded
-constexpr int64_t kInpaintMaxPixels = 1ll << 30;   // 30-bit pixel indices in the march's keys
+constexpr int64_t kInpaintMaxPixels = 1ll << 27;   // pop ranks (< 2 n) * 4 in 30 bits of the fill keys
 hipError_t launch_inpaint(const float *in, int64_t pitch, int H, int W, int radius, float *out, void *ws, hipStream_t st,
                           const InpaintOpts &o = InpaintOpts{});
 // 1 if a march with status key `key` (the caller's workspace, or a handle's) timed out (grid barrier
@@ -215,6 +215,8 @@ int inpaint_take_timeout(const void *key);
 int inpaint_take_timeout_any();
 // drop the mapped status words of a key whose workspace is being freed
 void inpaint_forget(const void *key);
+void inpaint_forget_all();
+bool inpaint_has_words();
 
 // Birchfield-Tomasi block costs into K1's volume layout (dsx_bt.hip, oracle/bt_cost.py)
 struct BtArgs {

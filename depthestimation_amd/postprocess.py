@@ -85,156 +85,368 @@ def detect_outliers(disparity, threshold=3.0, kernel_size=5):
     return (np.abs(d - mean) > np.float32(threshold) * std) & valid
 
 
-def _telea_solve(t1, t2):
-    """Telea's upwind eikonal update from two neighbour arrival times (1e6 = not available)."""
-    both = (t1 < 1e6) & (t2 < 1e6)
-    d = t1 - t2
-    r = 2.0 - d * d
-    s = (t1 + t2 + np.sqrt(np.maximum(r, 0.0))) / 2.0
-    ok = both & (r > 0) & (s >= t1) & (s >= t2)
-    return np.where(ok, s, 1.0 + np.minimum(t1, t2))
-
-
 _TELEA_DELTA = 0.7          # T-bucket width: below the least T step sqrt(2)/2 of a popped pixel's child
 _TELEA_MAX_SWEEPS = 1 << 16  # safety bound on one bucket's fixed-point sweeps (a DAG: never reached)
+_OFF4 = ((-1, 0), (0, -1), (1, 0), (0, 1))  # OpenCV's neighbour order: up, left, down, right
+_U64MAX = np.uint64(0xFFFFFFFFFFFFFFFF)
 
 
-def _telea_front(T, avail, cy, cx, H, W):
-    """T, grad T of pixels (cy, cx) from the 4-neighbours ``avail`` marks (Telea's upwind solve)."""
-    def tv(dy, dx):
-        yy, xx = cy + dy, cx + dx
-        inb = (yy >= 0) & (yy < H) & (xx >= 0) & (xx < W)
-        q = np.clip(yy, 0, H - 1) * W + np.clip(xx, 0, W - 1)
-        ok = inb & avail(q)
-        return ok, np.where(ok, T[q], 1e6)
-    (ou, tu), (od, td), (ol, tl), (orr, tr) = tv(-1, 0), tv(1, 0), tv(0, -1), tv(0, 1)
-    tp = np.minimum(np.minimum(_telea_solve(tu, tl), _telea_solve(td, tl)),
-                    np.minimum(_telea_solve(tu, tr), _telea_solve(td, tr)))
-    gx = np.where(orr & ol, (tr - tl) * 0.5, np.where(orr, tr - tp, np.where(ol, tp - tl, 0.0)))
-    gy = np.where(od & ou, (td - tu) * 0.5, np.where(od, td - tp, np.where(ou, tp - tu, 0.0)))
-    return tp, gx, gy
+def _cmin(a, b):
+    """C's ``a < b ? a : b`` (NaN-free; the sign of a zero follows C, not np.minimum)."""
+    return np.where(a < b, a, b)
 
 
-def _telea_value(out, T, avail, cy, cx, tp, gx, gy, H, W, radius, rows, keep):
-    """Telea's weighted average over the disc cells ``avail`` marks: float64, each window row summed
-    left to right from 0.0, the row sums added top to bottom; float32(num / den) where den > 0, else
-    ``keep``."""
-    num = np.zeros(cy.size)
-    den = np.zeros(cy.size)
-    for row in rows:
-        rn = np.zeros(cy.size)
-        rd = np.zeros(cy.size)
-        for oy, ox in row:
-            yy, xx = cy + oy, cx + ox
-            inb = (yy >= 0) & (yy < H) & (xx >= 0) & (xx < W)
-            q = np.clip(yy, 0, H - 1) * W + np.clip(xx, 0, W - 1)
-            ok = inb & avail(q)
-            ry, rx = -oy, -ox
-            d2 = ry * ry + rx * rx
-            w = np.maximum(np.abs(ry * gy + rx * gx) / math.sqrt(float(d2)) * (1.0 / d2)
-                           * (1.0 / (1.0 + np.abs(T[q] - tp))), 1e-6)
-            rn = np.where(ok, rn + w * out[q].astype(np.float64), rn)
-            rd = np.where(ok, rd + w, rd)
-        num = num + rn  # +0.0 for a row without terms: exact
-        den = den + rd
-    return np.where(den > 0, (num / np.where(den > 0, den, 1.0)).astype(np.float32), keep)
+def _fm_solve(t1, f1, t2, f2):
+    """OpenCV's FastMarching_solve for pixel pairs: t float32, f = not INSIDE; double inside, float32
+    out.  Both not INSIDE: 1 + min when |t1 - t2| >= 1, else (t1 + t2 + sqrt(2 - (t1 - t2)^2)) / 2;
+    one: 1 + its T; none: 1 + min."""
+    a11 = t1.astype(np.float64)
+    a22 = t2.astype(np.float64)
+    m12 = _cmin(a11, a22)
+    d = a11 - a22
+    quad = (a11 + a22 + np.sqrt(np.maximum(2.0 - d * d, 0.0))) * 0.5
+    sol = np.where(f1 & f2, np.where(np.abs(d) >= 1.0, 1.0 + m12, quad),
+                   np.where(f1, 1.0 + a11, np.where(f2, 1.0 + a22, 1.0 + m12)))
+    return sol.astype(np.float32)
+
+
+def _arrival(ci, cj, av, tv):
+    """min4 of the four (vertical, horizontal) pair solves at E pixels (ci, cj)."""
+    fu, fd, fl, fr = av(ci - 1, cj), av(ci + 1, cj), av(ci, cj - 1), av(ci, cj + 1)
+    tu, td, tl, tr = tv(ci - 1, cj), tv(ci + 1, cj), tv(ci, cj - 1), tv(ci, cj + 1)
+    a = _cmin(_fm_solve(tu, fu, tl, fl), _fm_solve(td, fd, tl, fl))
+    c = _cmin(_fm_solve(tu, fu, tr, fr), _fm_solve(td, fd, tr, fr))
+    return _cmin(a, c)
+
+
+def _telea_value_cv(ci, cj, tq, av, tv, ov, radius, EH, EW):
+    """OpenCV's Telea value for E pixels (ci, cj) with arrival time tq (icvTeleaInpaintFMM, single
+    channel, float image; the arithmetic is specified in oracle/telea_cv.c): float32 sums over the
+    disc in row-major order.  av(k, l): not INSIDE at this child's fill; tv: T; ov(r, c): the image
+    value at (r, c) (image coordinates) at this child's fill."""
+    f32 = np.float32
+    h = f32(0.5)
+    rgt, lft, dn, up = av(ci, cj + 1), av(ci, cj - 1), av(ci + 1, cj), av(ci - 1, cj)
+    tr, tl, td, tu = tv(ci, cj + 1), tv(ci, cj - 1), tv(ci + 1, cj), tv(ci - 1, cj)
+    gtx = np.where(rgt, np.where(lft, (tr - tl) * h, tr - tq), np.where(lft, tq - tl, f32(0)))
+    gty = np.where(dn, np.where(up, (td - tu) * h, td - tq), np.where(up, tq - tu, f32(0)))
+    n = ci.size
+    Ia = np.zeros(n, f32)
+    Jx = np.zeros(n, f32)
+    Jy = np.zeros(n, f32)
+    s = np.full(n, f32(1.0e-20), f32)
+    two = f32(2.0)
+    for dy in range(-radius, radius + 1):
+        k = ci + dy
+        km = k - 1 + (k == 1)
+        kp = k - 1 - (k == EH - 2)
+        for dx in range(-radius, radius + 1):
+            if dx * dx + dy * dy > radius * radius or (dx == 0 and dy == 0):
+                continue
+            l = cj + dx
+            lm = l - 1 + (l == 1)
+            lp = l - 1 - (l == EW - 2)
+            ok = (k > 0) & (l > 0) & (k < EH - 1) & (l < EW - 1) & av(k, l)
+            if not ok.any():
+                continue
+            ry, rx = float(-dy), float(-dx)
+            vl = rx * rx + ry * ry
+            dst = f32(1.0 / (vl * math.sqrt(vl)))
+            lev = (1.0 / (1.0 + np.abs((tv(k, l) - tq).astype(np.float64)))).astype(f32)
+            dirv = f32(rx) * gtx + f32(ry) * gty
+            dirv = np.where(np.abs(dirv).astype(np.float64) <= 0.01, f32(0.000001), dirv)
+            w = np.abs(dst * lev * dirv)
+            a_r, a_l, a_d, a_u = av(k, l + 1), av(k, l - 1), av(k + 1, l), av(k - 1, l)
+            gix = np.where(a_r, np.where(a_l, (ov(km, lp + 1) - ov(km, lm - 1)) * two, ov(km, lp + 1) - ov(km, lm)),
+                           np.where(a_l, ov(km, lp) - ov(km, lm - 1), f32(0)))
+            giy = np.where(a_d, np.where(a_u, (ov(kp + 1, lm) - ov(km - 1, lm)) * two, ov(kp + 1, lm) - ov(km, lm)),
+                           np.where(a_u, ov(kp, lm) - ov(km - 1, lm), f32(0)))
+            Ia = np.where(ok, Ia + w * ov(km, lm), Ia)
+            Jx = np.where(ok, Jx - w * (gix * f32(rx)), Jx)
+            Jy = np.where(ok, Jy - w * (giy * f32(ry)), Jy)
+            s = np.where(ok, s + w, s)
+    jn = np.sqrt((Jx * Jx + Jy * Jy).astype(np.float64)) + float(f32(1.0e-20))
+    sat = (Ia / s).astype(np.float64) + (Jx + Jy).astype(np.float64) / jn + 0.5
+    return sat.astype(f32)
+
+
+def _f32(x):
+    return float(np.float32(x))
+
+
+def _telea_child_scalar(c, kb, Tn, vc, orig, fb, key, EH, EW, radius, values):
+    """The same T (and value) as _arrival / _telea_value_cv for ONE child (E index c), in scalar
+    Python with float32 rounding after every float32 operation (small DAG layers: the vectorised form
+    costs thousands of numpy calls per layer whatever its size)."""
+    H, W = EH - 2, EW - 2
+    kc = key[c]
+    ci, cj = divmod(int(c), EW)
+
+    def av(i, j):
+        q = i * EW + j
+        f = fb[q]
+        return bool(f < kb or (f == kb and key[q] < kc))
+
+    def solve(t1, f1, t2, f2):
+        a11, a22 = float(t1), float(t2)
+        m12 = a11 if a11 < a22 else a22
+        if f1 and f2:
+            d = a11 - a22
+            return _f32(1.0 + m12 if abs(d) >= 1.0 else (a11 + a22 + math.sqrt(2.0 - d * d)) * 0.5)
+        return _f32(1.0 + (a11 if f1 else (a22 if f2 else m12)))
+
+    def cm(a, b):
+        return a if a < b else b
+
+    fu, fl, fd, fr = av(ci - 1, cj), av(ci, cj - 1), av(ci + 1, cj), av(ci, cj + 1)
+    tu, tl, td, tr = (float(Tn[(ci - 1) * EW + cj]), float(Tn[ci * EW + cj - 1]), float(Tn[(ci + 1) * EW + cj]),
+                      float(Tn[ci * EW + cj + 1]))
+    tp = cm(cm(solve(tu, fu, tl, fl), solve(td, fd, tl, fl)), cm(solve(tu, fu, tr, fr), solve(td, fd, tr, fr)))
+    if not values:
+        return tp, None
+    gtx = (_f32(_f32(tr - tl) * 0.5) if fl else _f32(tr - tp)) if fr else (_f32(tp - tl) if fl else 0.0)
+    gty = (_f32(_f32(td - tu) * 0.5) if fu else _f32(td - tp)) if fd else (_f32(tp - tu) if fu else 0.0)
+
+    def ov(r, col):
+        r = min(max(r, 0), H - 1) + 1
+        col = min(max(col, 0), W - 1) + 1
+        q = r * EW + col
+        return float(vc[q]) if av(r, col) else float(orig[q])
+
+    Ia = Jx = Jy = 0.0
+    s = _f32(1.0e-20)
+    for dy in range(-radius, radius + 1):
+        k = ci + dy
+        if not (0 < k < EH - 1):
+            continue
+        km, kp = k - 1 + (k == 1), k - 1 - (k == EH - 2)
+        for dx in range(-radius, radius + 1):
+            l = cj + dx
+            if dx * dx + dy * dy > radius * radius or (dx == 0 and dy == 0) or not (0 < l < EW - 1) or not av(k, l):
+                continue
+            lm, lp = l - 1 + (l == 1), l - 1 - (l == EW - 2)
+            ry, rx = float(-dy), float(-dx)
+            vl = rx * rx + ry * ry
+            dst = _f32(1.0 / (vl * math.sqrt(vl)))
+            lev = _f32(1.0 / (1.0 + abs(_f32(float(Tn[k * EW + l]) - tp))))
+            dirv = _f32(_f32(rx * gtx) + _f32(ry * gty))
+            if abs(dirv) <= 0.01:
+                dirv = _f32(0.000001)
+            w = abs(_f32(_f32(dst * lev) * dirv))
+            ar, al, ad, au = av(k, l + 1), av(k, l - 1), av(k + 1, l), av(k - 1, l)
+            if ar:
+                gix = _f32(_f32(ov(km, lp + 1) - ov(km, lm - 1)) * 2.0) if al else _f32(ov(km, lp + 1) - ov(km, lm))
+            else:
+                gix = _f32(ov(km, lp) - ov(km, lm - 1)) if al else 0.0
+            if ad:
+                giy = _f32(_f32(ov(kp + 1, lm) - ov(km - 1, lm)) * 2.0) if au else _f32(ov(kp + 1, lm) - ov(km, lm))
+            else:
+                giy = _f32(ov(kp, lm) - ov(km - 1, lm)) if au else 0.0
+            Ia = _f32(Ia + _f32(w * ov(km, lm)))
+            Jx = _f32(Jx - _f32(w * _f32(gix * rx)))
+            Jy = _f32(Jy - _f32(w * _f32(giy * ry)))
+            s = _f32(s + w)
+    jn = math.sqrt(_f32(_f32(Jx * Jx) + _f32(Jy * Jy))) + _f32(1.0e-20)
+    return tp, _f32(_f32(Ia / s) + _f32(Jx + Jy) / jn + 0.5)
+
+
+def _dag_layers(C, key, fb, kb, ys, xs, EH, EW, offsets):
+    """Topological layers of a bucket's children C: child c depends on the bucket's children q at the
+    given window offsets with key[q] < key[c].  Returns index arrays into C, in order."""
+    n = C.size
+    pos = np.full(EH * EW, -1, np.int64)
+    pos[C] = np.arange(n, dtype=np.int64)
+    cy, cx, kc = ys[C], xs[C], key[C]
+    src, dst = [], []
+    for dy, dx in offsets:
+        qy, qx = cy + dy, cx + dx
+        ok = (qy >= 0) & (qy < EH) & (qx >= 0) & (qx < EW)
+        q = np.where(ok, qy * EW + qx, 0)
+        ok &= (fb[q] == kb) & (key[q] < kc)
+        src.append(pos[q[ok]])
+        dst.append(np.nonzero(ok)[0])
+    src = np.concatenate(src)
+    dst = np.concatenate(dst)
+    indeg = np.bincount(dst, minlength=n)
+    order = np.argsort(src, kind="stable")
+    src_s, dst_s = src[order], dst[order]
+    starts = np.searchsorted(src_s, np.arange(n + 1))
+    layers = []
+    front = np.nonzero(indeg == 0)[0]
+    while front.size:
+        layers.append(front)
+        lens = starts[front + 1] - starts[front]
+        tot = int(lens.sum())
+        if tot == 0:
+            break
+        first = np.repeat(starts[front] - np.concatenate(([0], np.cumsum(lens)[:-1])), lens)
+        out = dst_s[first + np.arange(tot)]
+        np.subtract.at(indeg, out, 1)
+        cand = np.unique(out)
+        front = cand[indeg[cand] == 0]
+    if sum(l.size for l in layers) != n:
+        raise RuntimeError("Telea march: the bucket's dependencies are not acyclic")
+    return layers
+
+
+def _telea_march(T, vn, orig, inside, seeds, EH, EW, radius, values):
+    """One fast march of cv2.inpaint on the padded (EH x EW) grid, in the queue's own order, for a
+    parallel machine (the form csrc/dsx_inpaint.hip runs; the sequential queue is oracle/telea_cv).
+
+    ``inside``: the pixels to march into (INSIDE); ``seeds``: the band, pushed with T = 0 in raster
+    order; everything else is known with its current T.  ``values``: also Telea's values (the inward
+    march), else T only (the outward march).  T, vn: float32 E arrays, updated in place; orig: the
+    values before the march (what an unfilled pixel holds).  Returns the filled pixels.
+
+    The queue pops (T, push order).  A child's T exceeds its parent's by at least sqrt(2)/2 - its
+    other upwind neighbours are band pixels not yet popped (T >= the parent's) or pixels filled
+    since, so the pair solve gives at least the parent's T + sqrt(2)/2 - so with T-buckets of width
+    D = 0.7 the pops of a bucket are exactly the band pixels in it when it starts, and their children
+    land in later buckets.  Per bucket:
+      * order.  A pop's push order is (its parent's pop rank, its direction from the parent); seeds
+        by raster index.  The pops of a bucket are ranked by (T, push order): seeds rank by raster
+        index, later pops from EN on, bucket by bucket (dense, so a push key rank * 4 + dir fits 32
+        bits).  A child's fill key is (its parent's T, the parent's push key, its direction): the
+        order in which the queue fills the bucket's children;
+      * children.  The INSIDE 4-neighbours of the pops; the parent is the pop neighbour with the
+        least (T, push key);
+      * values.  A child sees the pixels filled before the bucket and the bucket's children with a
+        smaller fill key (in its (2 r + 3)^2 window: disc, its gradients' neighbours, OpenCV's edge
+        shift) - a DAG, so T and value are the unique fixed point of those equations; sweeps repeat
+        until no T or value bit changes (sweep 0: the pre-bucket pixels only)."""
+    EN = EH * EW
+    INF = np.iinfo(np.int64).max
+    fb = np.where(inside, INF, -1).astype(np.int64)          # fill bucket; -1: known
+    idx = np.arange(EN, dtype=np.int64)
+    pk = idx.copy()                                           # push key (seeds: raster index)
+    rank = idx.copy()                                         # pop rank (seeds: raster index)
+    key = np.zeros(EN, np.uint64)                             # fill key of the current bucket's children
+    ys, xs = np.divmod(idx, EW)
+    H, W = EH - 2, EW - 2
+    band = np.asarray(seeds, np.int64)
+    filled = np.zeros(EN, bool)
+    k, base, first = 0, EN, True
+    RW = radius + 1
+    while band.size:
+        k = max(k, int(math.floor(float(T[band].astype(np.float64).min()) / _TELEA_DELTA)))
+        bound = (k + 1) * _TELEA_DELTA
+        is_pop = T[band].astype(np.float64) < bound
+        P, band = band[is_pop], band[~is_pop]
+        if not first:  # seeds keep their raster index as rank
+            order = np.lexsort((pk[P], T[P].view(np.uint32)))
+            rank[P[order]] = base + np.arange(P.size, dtype=np.int64)
+            base += P.size
+        first = False
+        kb = k + 1
+        k = kb
+        tbits = T[P].view(np.uint32).astype(np.uint64)
+        ckey = np.full(EN, _U64MAX, np.uint64)
+        for d, (dy, dx) in enumerate(_OFF4):
+            c = P + dy * EW + dx
+            ok = fb[c] == INF
+            kk = (tbits << np.uint64(32)) | (pk[P].astype(np.uint64) << np.uint64(2)) | np.uint64(d)
+            np.minimum.at(ckey, c[ok], kk[ok])
+        C = np.nonzero(ckey != _U64MAX)[0]
+        if C.size == 0:
+            continue
+        fb[C] = kb
+        key[C] = ckey[C]
+        dC = (ckey[C] & np.uint64(3)).astype(np.int64)
+        offs = np.array([dy * EW + dx for dy, dx in _OFF4], np.int64)
+        pk[C] = rank[C - offs[dC]] * 4 + dC
+        Tn = T.copy()
+        vc = vn.copy()
+
+        def run(cs):
+            ci, cj = ys[cs], xs[cs]
+            kc = key[cs]
+
+            def e(a, b):
+                return np.clip(a, 0, EH - 1) * EW + np.clip(b, 0, EW - 1)
+
+            def av(a, b):
+                q = e(a, b)
+                f = fb[q]
+                return (f < kb) | ((f == kb) & (key[q] < kc))
+
+            def tv(a, b):
+                return Tn[e(a, b)]
+
+            tp = _arrival(ci, cj, av, tv)
+            if not values:
+                return tp, None
+
+            def ov(r, c):
+                r = np.clip(r, 0, H - 1) + 1
+                c = np.clip(c, 0, W - 1) + 1
+                q = r * EW + c
+                return np.where(av(r, c), vc[q], orig[q])
+
+            return tp, _telea_value_cv(ci, cj, tp, av, tv, ov, radius, EH, EW)
+
+        # The bucket's equations form a DAG (a child reads the children with a smaller fill key in its
+        # window: (2 r + 3)^2 for values, the 4-neighbours for T), so evaluating its layers in
+        # topological order gives the fixed point the device reaches by repeated sweeps.
+        offs_w = [(dy, dx) for dy in range(-RW, RW + 1) for dx in range(-RW, RW + 1) if dy or dx] if values \
+            else [(-1, 0), (0, -1), (1, 0), (0, 1)]
+        for layer in _dag_layers(C, key, fb, kb, ys, xs, EH, EW, offs_w):
+            cs = C[layer]
+            if cs.size <= 24:  # small layers one child at a time (the same arithmetic)
+                for c in cs.tolist():
+                    tp, v = _telea_child_scalar(c, kb, Tn, vc, orig, fb, key, EH, EW, radius, values)
+                    Tn[c] = tp
+                    if values:
+                        vc[c] = v
+                continue
+            tp, v = run(cs)
+            Tn[cs] = tp
+            if values:
+                vc[cs] = v
+        T[C] = Tn[C]
+        if values:
+            vn[C] = vc[C]
+        filled[C] = True
+        band = np.concatenate([band, C])
+    return filled
 
 
 def _telea_inpaint(img: np.ndarray, hole: np.ndarray, radius: int) -> np.ndarray:
-    """Telea (2004) fast-marching inpainting of float32 ``img`` where ``hole`` is True, in the
-    arrival-time order of cv2.inpaint(INPAINT_TELEA) (postprocess.py:104), restated for a parallel
-    machine (the form csrc/dsx_inpaint.hip runs; the sequential heap march is oracle/telea_heap.py).
-
-    The heap pops the narrow band by (T, push order); popping p fills each still-INSIDE 4-neighbour q
-    (up, left, down, right) from the pixels filled so far: T(q) by the upwind solve over its filled
-    4-neighbours, value(q) = sum w v / sum w over the filled pixels of its radius disc,
-    w = max(|(q-n).grad T| / |q-n| * 1/|q-n|^2 * 1/(1 + |T(n) - T(q)|), 1e-6).  A child's T exceeds its
-    parent's by at least sqrt(2)/2 (both upwind neighbours are at least the parent's T), so the pops of
-    one T-bucket [k*D, (k+1)*D), D = 0.7 < sqrt(2)/2, are exactly the band pixels in it when the bucket
-    starts, and their children land in later buckets.  Per bucket:
-      * order.  The push order inside a bucket is the lexicographic chain (T, T of the parent, ..., 0,
-        the seed's raster index, the directions back down); it is kept to one generation:
-        pop key (T, T_parent, root seed, direction from the parent, raster index), seeds (0, -1, raster,
-        0, raster);
-      * children.  Every INSIDE 4-neighbour of a pop; its parent is the pop neighbour with the least
-        pop key, its fill key (parent's pop key, its direction);
-      * values.  A child sees the pixels filled before the bucket and the bucket's children with a
-        smaller fill key - a DAG, so T and value are the unique fixed point of those equations.  Sweep
-        0 uses the pre-bucket pixels only; sweeps repeat (Jacobi) until no T or value bit changes.
-    Equal to ``telea_heap`` bit for bit on the C2 / C4 matcher maps and the tests' random maps
-    (tests/test_telea_heap.py); parity with OpenCV's own output is unpinned (cv2 absent).  Hole pixels
-    no known pixel reaches keep their value."""
+    """cv2.inpaint(img, hole, radius, INPAINT_TELEA) for a float32 image (postprocess.py:104), as
+    OpenCV's photo/src/inpaint.cpp does it (recalled; the specification and the sequential oracle are
+    oracle/telea_cv.c): the image padded by one pixel (KNOWN, T = 1e6); the band (known pixels
+    4-adjacent to a hole) seeds two marches - outward over the known pixels within Chebyshev distance
+    ``radius`` of a hole (their T negated afterwards, the band's to -0), then inward over the holes
+    with Telea's float32 values (+ OpenCV's normalised gradient term and + 0.5).  Both marches run
+    in the queue's order in the parallel form of ``_telea_march`` (the GPU's).  ``radius`` < 1 is 1,
+    as in OpenCV.  Parity with OpenCV's own output is unpinned (cv2 absent)."""
+    img = np.asarray(img, np.float32)
     H, W = img.shape
-    n = H * W
-    out = np.asarray(img, np.float32).ravel().copy()
-    hole = np.asarray(hole, bool).ravel()
-    INSIDE = np.iinfo(np.int64).max
-    fb = np.where(hole, INSIDE, -1).astype(np.int64)   # fill bucket: -1 known, INSIDE unfilled
-    T = np.where(hole, 1e6, 0.0)
-    Tp = np.full(n, -1.0)                              # pop key fields (seeds: T_parent -1, root = self)
-    root = np.arange(n, dtype=np.int64)
-    dirc = np.zeros(n, np.int64)
-    rows = [[(dy, dx) for dx in range(-radius, radius + 1) if 0 < dy * dy + dx * dx <= radius * radius]
-            for dy in range(-radius, radius + 1)]
-    h2 = hole.reshape(H, W)
-    nb = np.zeros((H, W), bool)
-    nb[1:, :] |= h2[:-1, :]
-    nb[:-1, :] |= h2[1:, :]
-    nb[:, 1:] |= h2[:, :-1]
-    nb[:, :-1] |= h2[:, 1:]
-    band = np.nonzero(~hole & nb.ravel())[0]            # the narrow band: seeds, then the filled pixels
-    ys_all, xs_all = np.divmod(np.arange(n, dtype=np.int64), W)
-    DIRS = ((-1, 0), (0, -1), (1, 0), (0, 1))           # OpenCV's neighbour order: up, left, down, right
-    k = 0
-    while band.size:
-        k = max(k, int(math.floor(T[band].min() / _TELEA_DELTA)))
-        bound = (k + 1) * _TELEA_DELTA
-        is_pop = T[band] < bound
-        P, band = band[is_pop], band[~is_pop]
-        # pop order (T, T_parent, root, direction, raster)
-        P = P[np.lexsort((P, dirc[P], root[P], Tp[P], T[P]))]
-        prank = np.full(n, -1, np.int64)
-        prank[P] = np.arange(P.size)
-        # children: INSIDE 4-neighbours of the pops; parent = least-ranked pop neighbour
-        ckey = np.full(n, INSIDE, np.int64)
-        py, px = ys_all[P], xs_all[P]
-        for di, (dy, dx) in enumerate(DIRS):
-            cy, cx = py + dy, px + dx
-            ok = (cy >= 0) & (cy < H) & (cx >= 0) & (cx < W)
-            c = cy[ok] * W + cx[ok]
-            kk = np.arange(P.size, dtype=np.int64)[ok] * 4 + di
-            m = fb[c] == INSIDE
-            np.minimum.at(ckey, c[m], kk[m])
-        C = np.nonzero(ckey != INSIDE)[0]
-        k += 1
-        if C.size == 0:
-            continue
-        fb[C] = k
-        kc = ckey[C]
-        cy, cx = ys_all[C], xs_all[C]
-        pre = lambda q: fb[q] < k                      # filled before this bucket (or known)
-        cur = lambda q: (fb[q] < k) | ((fb[q] == k) & (ckey[q] < kc))
-        Tn, vn = T.copy(), out.copy()
-        avail = pre
-        for _ in range(_TELEA_MAX_SWEEPS):
-            tp, gx, gy = _telea_front(Tn, avail, cy, cx, H, W)
-            v = _telea_value(vn, Tn, avail, cy, cx, tp, gx, gy, H, W, radius, rows, out[C])
-            changed = (tp != Tn[C]) | (v.view(np.int32) != vn[C].view(np.int32))
-            Tn[C] = tp
-            vn[C] = v
-            if avail is cur and not changed.any():
-                break
-            avail = cur
-        else:
-            raise RuntimeError("Telea march: a bucket did not converge")
-        T[C] = Tn[C]
-        out[C] = vn[C]
-        par = P[kc // 4]
-        Tp[C] = T[par]
-        root[C] = root[par]
-        dirc[C] = kc % 4
-        band = np.concatenate([band, C])
-    return out.reshape(H, W)
+    radius = min(max(int(radius), 1), 100)
+    EH, EW = H + 2, W + 2
+    mask = np.zeros((EH, EW), bool)
+    mask[1:-1, 1:-1] = np.asarray(hole, bool)
+    interior = np.zeros((EH, EW), bool)
+    interior[1:-1, 1:-1] = True
+    nb = np.zeros((EH, EW), bool)
+    nb[1:, :] |= mask[:-1, :]
+    nb[:-1, :] |= mask[1:, :]
+    nb[:, 1:] |= mask[:, :-1]
+    nb[:, :-1] |= mask[:, 1:]
+    band = interior & ~mask & nb
+    near = ndimage.maximum_filter(mask.astype(np.uint8), size=2 * radius + 1, mode="constant", cval=0) > 0
+    ring = interior & near & ~mask & ~band
+    vals = np.zeros((EH, EW), np.float32)
+    vals[1:-1, 1:-1] = img
+    vals = vals.ravel()
+    T = np.full(EH * EW, 1.0e6, np.float32)
+    seeds = np.nonzero(band.ravel())[0]
+    T[seeds] = 0.0
+    reached = _telea_march(T, vals, vals, ring.ravel(), seeds, EH, EW, radius, values=False)
+    neg = band.ravel() | reached
+    T[neg] = -T[neg]
+    out = vals.copy()
+    _telea_march(T, out, vals, mask.ravel(), seeds, EH, EW, radius, values=True)
+    return out.reshape(EH, EW)[1:-1, 1:-1].copy()
 
 
 def fill_holes(disparity, mask=None, method="inpaint", kernel_size=5):

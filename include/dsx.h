@@ -32,7 +32,9 @@
 extern "C" {
 #endif
 
-#define DSX_VERSION 105 /* 1.0.5: arrival-order hole filling, per-workspace / per-handle fill status, dsx_fill_opts;
+#define DSX_VERSION 106 /* 1.0.6: hole filling in OpenCV's own arithmetic and exact queue order, dsx_fill_holes_release,
+                           dsx_shutdown;
+                           1.0.5: arrival-order hole filling, per-workspace / per-handle fill status, dsx_fill_opts;
                            1.0.4: dsx_params.in_flight; 1.0.3: dsx_process_pair_device, dsx_fill_holes_status */
 
 #define DSX_OK 0
@@ -207,10 +209,12 @@ int dsx_postprocess_full_ex_device(const void *d_disp, int32_t H, int32_t W, int
                                    void *d_workspace, size_t workspace_bytes, void *hip_stream);
 
 /* fill_holes(disparity, method='inpaint', kernel_size=radius) on the device (postprocess.py:72-118,
- * cv2.inpaint INPAINT_TELEA on d <= 0): Telea fast-marching inpainting in cv2.inpaint's arrival-time
- * (heap) order, equal bit for bit to the host restatement (postprocess.py _telea_inpaint) and, on every
- * map tested, to the sequential heap march (oracle/telea_heap.py).
- * d_disp: float32 H x W, row pitch `in_pitch` elements; d_out: contiguous float32 H x W; H * W < 2^30.
+ * cv2.inpaint INPAINT_TELEA on d <= 0) as OpenCV's inpaint.cpp does it (recalled): the outward march
+ * over the known pixels within `radius` of a hole, then the inward march with Telea's float32 values,
+ * OpenCV's normalised gradient term and + 0.5, both in the queue's exact (T, push order) order.  Equal
+ * bit for bit to the sequential march (oracle/telea_cv.c) and the host restatement (postprocess.py
+ * _telea_inpaint).  radius < 1 is taken as 1 (OpenCV clamps its range to [1, 100]).
+ * d_disp: float32 H x W, row pitch `in_pitch` elements; d_out: contiguous float32 H x W; H * W < 2^27.
  * d_workspace: >= dsx_fill_holes_workspace_bytes(H, W).  Asynchronous on hip_stream: the march runs
  * as step launches (as many as the previous call on this workspace needed) plus one persistent
  * launch for any steps beyond them; nothing is read back to the host. */
@@ -239,6 +243,17 @@ int dsx_fill_holes_ex_device(const void *d_disp, int32_t H, int32_t W, int64_t i
 int dsx_fill_holes_status_ws(const void *d_workspace);
 int dsx_fill_holes_status_handle(dsx_handle *h);
 int dsx_fill_holes_status(void);
+
+/* Release the mapped host words (step history, timeout flag) kept for a workspace key: call it
+ * before freeing or reusing a hole-filling workspace, so a new buffer at a recycled address does not
+ * inherit the old one's flag (its pending flag is returned first, as dsx_fill_holes_status_ws).
+ * Handles release theirs in dsx_destroy. */
+int dsx_fill_holes_release(const void *d_workspace);
+
+/* Process teardown: wait for every device, then free what the library keeps per process (the mapped
+ * host words of every workspace key).  Python registers it with atexit; C callers call it before
+ * exit() when no other thread uses the library.  Later calls re-create what they need. */
+int dsx_shutdown(void);
 
 /* The per-frame call of the drop-in path, StereoCore._process_pair on the device (stereo_core.py:
  * 162-200): compute_disparity (:165, the matcher with this handle's parameters, float = fixed / 16,

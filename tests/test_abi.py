@@ -62,7 +62,7 @@ def test_post_params_struct_layout_matches_c(tmp_path):
 
 def test_version_and_defaults():
     lib = _dsx.lib()
-    assert lib.dsx_version() == 105
+    assert lib.dsx_version() == 106
     p = _dsx.default_params()
     # StereoCore.sgbm_params defaults (stereo_core.py:16-39) + build keys
     assert (p.min_disp, p.num_disp, p.block_size, p.uniqueness_ratio, p.disp12_max_diff) == (0, 128, 5, 10, 1)

@@ -204,7 +204,9 @@ def test_fill_holes_inpaint_and_nearest():
     holes[8:12, 12:16] = 0
     f = pp.fill_holes(holes, method="inpaint", kernel_size=3)
     assert np.all(f[8:12, 12:16] > 10) and np.all(f[8:12, 12:16] < 20)
-    assert np.max(np.abs(f - d)) < 1.5
+    # cv2.inpaint's Telea on a float map adds its normalised gradient term (|.| <= sqrt 2) and + 0.5
+    # (oracle/telea_cv.c): within 2 levels of the ramp here
+    assert np.max(np.abs(f - d)) < 2.0
     g = pp.fill_holes(holes, method="nearest", kernel_size=5)
     assert np.all(g[8:12, 12:16] > 0)
 

@@ -1,14 +1,15 @@
 """Hole filling (fill_holes method 'inpaint', postprocess.py:72-118 -> cv2.inpaint INPAINT_TELEA):
-the arrival-time (T-bucket, fixed-point) restatement on the host, pinned bit for bit by the
-sequential heap march (oracle/telea_heap.py, the order cv2.inpaint pops its narrow band), and the
-device kernel against both (GPU).  Parity with OpenCV's own output is unpinned (cv2 is absent); the
-reference's own behavioural check (holes filled between their neighbours' values) is
+the parallel (T-bucket, DAG) restatement on the host, pinned bit for bit by the sequential queue
+march of OpenCV's inpaint.cpp as recalled (oracle/telea_cv.c, itself pinned by the pure-Python
+oracle.telea_cv.telea_cv_py in tests/test_telea_heap.py), and the device kernel against the oracle
+(GPU).  Parity with OpenCV's own output is unpinned (cv2 is absent); the reference's own behavioural
+check (holes filled between their neighbours' values) is
 tests/test_host_api.py::test_fill_holes_inpaint_and_nearest."""
 import numpy as np
 import pytest
 
 from depthestimation_amd import postprocess as pp
-from oracle.telea_heap import telea_heap
+from oracle.telea_cv import telea as telea_heap
 
 
 def _holey(H, W, seed, frac=0.15):
@@ -22,7 +23,11 @@ def _holey(H, W, seed, frac=0.15):
 
 
 def _bits(a):
-    return np.asarray(a, np.float32).view(np.int32)
+    """Bit patterns, with every NaN as the canonical quiet NaN (a NaN input pixel is known and spreads
+    into the values that read it; the sign of a NaN result is not part of the contract)."""
+    a = np.array(a, np.float32, copy=True)
+    a[np.isnan(a)] = np.float32(np.nan)
+    return a.view(np.int32)
 
 
 @pytest.mark.parametrize("shape,radius,seed", [((12, 17), 3, 1), ((9, 23), 5, 2), ((15, 11), 1, 3), ((7, 7), 2, 4),
@@ -84,9 +89,11 @@ def test_inpaint_equals_heap_march_symmetric(case):
 def test_inpaint_edge_cases():
     d = np.zeros((6, 8), np.float32)                       # nothing known: nothing filled
     np.testing.assert_array_equal(pp.fill_holes(d, method="inpaint", kernel_size=3), d)
-    d[2, 3] = 7.5                                          # one known pixel: everything becomes 7.5
-    f = pp.fill_holes(d, method="inpaint", kernel_size=3)
-    np.testing.assert_array_equal(f, np.full_like(d, 7.5))
+    d[2, 3] = 7.5                                          # one known pixel: the first pixel filled (above it)
+    f = pp.fill_holes(d, method="inpaint", kernel_size=3)  # sees only it: 7.5 + 0.5 (OpenCV's rounding term
+    assert f[2, 3] == np.float32(7.5)                      # stays in a float image; later pixels see filled
+    assert abs(float(f[1, 3]) - 8.0) < 1e-4                # ones too, and their gradient term)
+    np.testing.assert_array_equal(_bits(f), _bits(telea_heap(d, d <= 0, 3)))
     g = np.arange(20, dtype=np.float32).reshape(4, 5) + 1  # no holes: unchanged
     np.testing.assert_array_equal(pp.fill_holes(g, method="inpaint", kernel_size=3), g)
     n = _holey(10, 12, 3)
@@ -102,7 +109,21 @@ def test_inpaint_fills_between_neighbours():
     f = pp.fill_holes(h, method="inpaint", kernel_size=3)
     known = h > 0
     np.testing.assert_array_equal(f[known], h[known])
-    assert np.all(f[~known] >= d[10:20, 15:25].min() - 1) and np.all(f[~known] <= d[10:20, 15:25].max() + 1)
+    # OpenCV's form adds its normalised gradient term (|.| <= sqrt 2) and + 0.5 to the weighted mean of
+    # pixels that carry the same terms from earlier generations: filled values scatter by a few levels
+    assert np.all(f[~known] >= d[10:20, 15:25].min() - 3) and np.all(f[~known] <= d[10:20, 15:25].max() + 3)
+    np.testing.assert_array_equal(_bits(f), _bits(telea_heap(h, h <= 0, 3)))
+
+
+def test_inpaint_push_order_island():
+    """a one-generation pop key swaps the fill order of the children of (-1, 1) and
+    (1, -1) around a lone known pixel, which changes values when another known value is in reach.  The
+    exact push order (dense pop ranks) equals the sequential queue here."""
+    d = np.zeros((41, 41), np.float32)
+    d[20, 20] = 5.0
+    d[21, 14] = 9.0
+    np.testing.assert_array_equal(_bits(pp.fill_holes(d, method="inpaint", kernel_size=5)),
+                                  _bits(telea_heap(d, d <= 0, 5)))
 
 
 # ---- device ----------------------------------------------------------------------------------
@@ -114,9 +135,12 @@ def test_fill_holes_device_matches_host(shape, radius, seed):
     import torch
     from depthestimation_amd.matcher import fill_holes_device
     d = _holey(*shape, seed, frac=0.2)
-    ref = pp.fill_holes(d, method="inpaint", kernel_size=radius)
+    ref = telea_heap(d, d <= 0, radius)
     got = fill_holes_device(torch.from_numpy(d).cuda(), radius=radius)
     np.testing.assert_array_equal(_bits(got.cpu().numpy()), _bits(ref))
+    if d.size <= 10000:
+        np.testing.assert_array_equal(_bits(got.cpu().numpy()),
+                                      _bits(pp.fill_holes(d, method="inpaint", kernel_size=radius)))
 
 
 @pytest.mark.gpu
@@ -143,7 +167,7 @@ def test_fill_holes_device_tall_maps(H):
     e[:, 30:] = 0                                # columns with no known pixel in any row ...
     e[: H // 2, :] = 0                           # ... and rows with none
     for m in (d, e, np.zeros_like(d)):
-        ref = pp.fill_holes(m, method="inpaint", kernel_size=3)
+        ref = telea_heap(m, m <= 0, 3)
         got = fill_holes_device(torch.from_numpy(m).cuda(), radius=3)
         np.testing.assert_array_equal(_bits(got.cpu().numpy()), _bits(ref))
 
@@ -156,14 +180,49 @@ def test_fill_holes_device_edge_cases():
     n[4, 4] = np.nan
     for d in (np.zeros((6, 8), np.float32), np.arange(12, dtype=np.float32).reshape(3, 4) + 1,
               np.where(np.eye(9, 13) > 0, 4.0, 0.0).astype(np.float32), np.full((1, 50), -1.0, np.float32), n):
-        ref = pp.fill_holes(d, method="inpaint", kernel_size=3)
+        ref = telea_heap(d, d <= 0, 3)
         got = fill_holes_device(torch.from_numpy(d).cuda(), radius=3)
         np.testing.assert_array_equal(_bits(got.cpu().numpy()), _bits(ref))
     # a pitched (column-sliced) input
     d = _holey(40, 90, 9)
     t = torch.from_numpy(d).cuda()[:, 10:]
     np.testing.assert_array_equal(_bits(fill_holes_device(t, radius=3).cpu().numpy()),
-                                  _bits(pp.fill_holes(d[:, 10:], method="inpaint", kernel_size=3)))
+                                  _bits(telea_heap(d[:, 10:], d[:, 10:] <= 0, 3)))
+    # radius 0 is taken as 1 (cv2.inpaint clamps its range to [1, 100])
+    d = _holey(30, 40, 4)
+    np.testing.assert_array_equal(_bits(fill_holes_device(torch.from_numpy(d).cuda(), radius=0).cpu().numpy()),
+                                  _bits(telea_heap(d, d <= 0, 1)))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", ["island", "center", "square", "disc", "diagonal", "grid", "corner"])
+def test_fill_holes_device_symmetric_and_island(case):
+    """Equal arrival times everywhere (the push order decides who sees whom), and ADVICE r5's island."""
+    import torch
+    from depthestimation_amd.matcher import fill_holes_device
+    yy, xx = np.mgrid[0:41, 0:41]
+    d = (5 + 0.2 * xx + 0.1 * yy).astype(np.float32)
+    r = 3
+    if case == "island":
+        d[:] = 0
+        d[20, 20], d[21, 14] = 5.0, 9.0
+        r = 5
+    elif case == "center":
+        d[:] = 0
+        d[20, 20] = 5
+    elif case == "square":
+        d[8:33, 8:33] = 0
+    elif case == "disc":
+        d[(xx - 20) ** 2 + (yy - 20) ** 2 < 200] = 0
+    elif case == "diagonal":
+        d[np.abs(xx - yy) < 4] = 0
+    elif case == "grid":
+        d[::3, :] = 0
+        d[:, ::4] = 0
+    else:
+        d[1:, 1:] = 0
+    got = fill_holes_device(torch.from_numpy(d).cuda(), radius=r).cpu().numpy()
+    np.testing.assert_array_equal(_bits(got), _bits(telea_heap(d, d <= 0, r)))
 
 
 @pytest.mark.gpu
@@ -215,7 +274,7 @@ def test_fill_holes_device_step_split(steps):
     d3 = np.zeros((64, 64), np.float32)                # nothing known: nothing reached
     ws = FillWorkspace()
     for d, r in ((d1, 3), (d2, 5), (d3, 3), (_holey(50, 70, 12), 9)):
-        ref = pp.fill_holes(d, method="inpaint", kernel_size=r)
+        ref = telea_heap(d, d <= 0, r)
         got = fill_holes_device(torch.from_numpy(d).cuda(), radius=r, workspace=ws, steps=steps)
         torch.cuda.synchronize()
         from depthestimation_amd.matcher import fill_holes_status
@@ -230,7 +289,7 @@ def test_fill_holes_device_does_not_block():
     import torch
     from depthestimation_amd.matcher import fill_holes_device
     d = _holey(200, 300, 13, frac=0.25)
-    ref = pp.fill_holes(d, method="inpaint", kernel_size=3)
+    ref = telea_heap(d, d <= 0, 3)
     x = torch.from_numpy(d).cuda()
     st = torch.cuda.Stream()
     torch.cuda.synchronize()
@@ -265,13 +324,12 @@ def _matcher_fill_input(config):
 def test_fill_holes_device_on_matcher_output(config):
     """The bench's hole-filling input: the matcher's own map at the config's size after the default
     post-processing (speckles + outliers), radius 3 as _process_pair passes it - against the host
-    restatement and the sequential heap march, bit for bit (C4: ~228k holes, 47 T-buckets)."""
+    sequential queue march, bit for bit (C4: ~228k holes)."""
     from depthestimation_amd.matcher import fill_holes_device
     clean = _matcher_fill_input(config)
     got = fill_holes_device(clean, radius=3).cpu().numpy()
     c = clean.cpu().numpy()
     assert (c <= 0).sum() > 1000
-    np.testing.assert_array_equal(_bits(got), _bits(pp.fill_holes(c, method="inpaint", kernel_size=3)))
     np.testing.assert_array_equal(_bits(got), _bits(telea_heap(c, c <= 0, 3)))
 
 
@@ -300,8 +358,8 @@ def test_fill_holes_timeout_is_reported_per_workspace():
     torch.cuda.synchronize()
     with pytest.raises(RuntimeError, match="timed out"):
         fill_holes_device(x, radius=3, workspace=bad)
-    # with the normal bound everything is filled again and equals the host
-    ref = pp.fill_holes(d, method="inpaint", kernel_size=3)
+    # with the normal bound everything is filled again and equals the oracle
+    ref = telea_heap(d, d <= 0, 3)
     got = fill_holes_device(x, radius=3, workspace=bad)
     torch.cuda.synchronize()
     fill_holes_status(bad)

@@ -1,13 +1,22 @@
-"""The heap-ordered Telea oracle (oracle/telea_heap.py): cv2.inpaint's march
-order (depthlib/postprocess.py:102-105), one pixel at a time.  Pinned here by an independent queue
-form and by the single-layer case; the product's arrival-time form is checked against it in
-tests/test_inpaint.py."""
+"""The hole-filling oracles.
+
+* oracle/telea_cv.c (``oracle.telea_cv.telea``): cv2.inpaint(INPAINT_TELEA) on a float32 map as
+  OpenCV's inpaint.cpp does it (recalled: OpenCV is absent, parity with its output is unpinned),
+  one pixel at a time in its queue's order (depthlib/postprocess.py:102-105).  Pinned here by an
+  independent pure-Python restatement with a sorted-list queue (``telea_cv_py``), by known answers
+  (constant surroundings: the mean + OpenCV's + 0.5; nothing known; no hole) and by the
+  isolated-pixel case (every order computes the same thing).
+* oracle/telea_heap.py: the round-5 form (Telea's paper weights, float64, no outward march), kept
+  only to measure how far the OpenCV form moved the values (tools/telea_divergence.py); pinned by its
+  own sorted-list form.
+The product's parallel form is checked against ``telea`` in tests/test_inpaint.py."""
 from __future__ import annotations
 
 import numpy as np
 import pytest
 
 from depthestimation_amd import postprocess as pp
+from oracle.telea_cv import telea, telea_cv_py
 from oracle.telea_heap import telea_heap, telea_heap_list
 
 
@@ -19,40 +28,73 @@ def _holey(H, W, seed, frac=0.15):
     return d
 
 
-@pytest.mark.parametrize("seed,radius", [(0, 3), (1, 1), (2, 5), (3, 3), (4, 2)])
-def test_heap_forms_agree(seed, radius):
-    d = _holey(14, 23, seed)
-    np.testing.assert_array_equal(telea_heap(d, d <= 0, radius), telea_heap_list(d, d <= 0, radius))
+def _bits(a):
+    return np.asarray(a, np.float32).view(np.int32)
+
+
+@pytest.mark.parametrize("seed,radius", [(0, 3), (1, 1), (2, 5), (3, 3), (4, 2), (5, 4)])
+@pytest.mark.parametrize("with_ring", [True, False])
+def test_c_and_python_oracles_agree(seed, radius, with_ring):
+    d = _holey(11 + seed, 17 + 2 * seed, seed, frac=0.1 + 0.04 * seed)
+    if seed % 2 == 0:
+        d[0, :3] = 0        # holes on every border: OpenCV's index shifts and the padding's T
+        d[-1, -2:] = 0
+        d[::3, 0] = 0
+        d[1::4, -1] = 0
+    np.testing.assert_array_equal(_bits(telea(d, d <= 0, radius, with_ring)),
+                                  _bits(telea_cv_py(d, d <= 0, radius, with_ring)))
+
+
+@pytest.mark.parametrize("shape", [(1, 9), (9, 1), (2, 2), (3, 40)])
+def test_oracles_agree_on_thin_maps(shape):
+    d = (np.arange(np.prod(shape)).reshape(shape) % 5 + 1).astype(np.float32)
+    d.ravel()[::3] = 0
+    np.testing.assert_array_equal(_bits(telea(d, d <= 0, 3)), _bits(telea_cv_py(d, d <= 0, 3)))
+
+
+def test_known_answers():
+    d = np.full((5, 5), 7.5, np.float32)
+    d[2, 2] = 0.0
+    # constant surroundings: the weighted mean is 7.5 (s starts at 1e-20, one ulp below), no gradient
+    # term, + 0.5 (saturate_cast's rounding term, kept by a float image)
+    assert abs(float(telea(d, d <= 0, 3)[2, 2]) - 8.0) < 2e-6
+    z = np.zeros((4, 6), np.float32)
+    np.testing.assert_array_equal(telea(z, z <= 0, 3), z)  # nothing known: nothing filled
+    k = np.arange(12, dtype=np.float32).reshape(3, 4) + 1
+    np.testing.assert_array_equal(telea(k, k <= 0, 3), k)  # no hole
+    # radius 0 is radius 1 (cv2.inpaint clamps its range to [1, 100])
+    h = _holey(12, 14, 3)
+    np.testing.assert_array_equal(telea(h, h <= 0, 0), telea(h, h <= 0, 1))
+
+
+def test_outward_march_times():
+    """The outward march's T: the band -0, the known pixels within Chebyshev distance r of a hole
+    minus their distance (1, sqrt 2 / 2 + ... ), everything else 1e6."""
+    d = np.full((15, 15), 3.0, np.float32)
+    d[7, 7] = 0.0
+    _, T = telea(d, d <= 0, 2, return_t=True)
+    Ti = T[1:-1, 1:-1]
+    for y, x in ((6, 7), (8, 7), (7, 6), (7, 8)):
+        assert Ti[y, x] == 0.0 and np.signbit(Ti[y, x])      # the band, negated
+    assert Ti[5, 7] == np.float32(-1.0)                     # two above the hole: one step from the band
+    assert Ti[6, 6] < 0 and Ti[5, 5] < Ti[6, 6]             # further out, more negative
+    assert Ti[0, 0] == np.float32(1.0e6) and Ti[7, 2] == np.float32(1.0e6)  # beyond the ring
 
 
 @pytest.mark.parametrize("radius", [1, 3])
-def test_single_layer_equals_layered(radius):
-    """Isolated hole pixels more than 2r apart: no hole pixel sees another, so any march order
-    computes the same thing."""
+def test_isolated_pixels_any_order(radius):
+    """Isolated hole pixels more than 2r + 2 apart: no hole reads another, so every march order
+    computes the same thing - the parallel form too."""
     rng = np.random.default_rng(7)
     d = (10 + rng.integers(0, 64, (30, 41)) / 16.0).astype(np.float32)
-    for y in range(3, 30, 2 * radius + 3):
-        for x in range(2, 41, 2 * radius + 4):
+    for y in range(3, 30, 2 * radius + 5):
+        for x in range(2, 41, 2 * radius + 5):
             d[y, x] = 0.0
     hole = d <= 0
-    np.testing.assert_array_equal(telea_heap(d, hole, radius), pp._telea_inpaint(d, hole, radius))
+    np.testing.assert_array_equal(_bits(telea(d, hole, radius)), _bits(pp._telea_inpaint(d, hole, radius)))
 
 
-def test_known_answers_and_edges():
-    d = np.full((5, 5), 7.5, np.float32)
-    d[2, 2] = 0.0
-    assert telea_heap(d, d <= 0, 3)[2, 2] == np.float32(7.5)  # constant surroundings
-    z = np.zeros((4, 6), np.float32)
-    np.testing.assert_array_equal(telea_heap(z, z <= 0, 3), z)  # nothing known: nothing filled
-    k = np.arange(12, dtype=np.float32).reshape(3, 4) + 1
-    np.testing.assert_array_equal(telea_heap(k, k <= 0, 3), k)  # no hole
-
-
-def test_wide_hole_equals_arrival_order_form():
-    """A wide hole: the heap fills pixels of one distance layer from each other (the order a layered
-    march cannot reproduce); the arrival-time form (postprocess._telea_inpaint, the GPU's) does, bit
-    for bit."""
-    d = _holey(24, 30, 11, frac=0.0)
-    d[4:20, 5:25] = 0.0
-    h, a = telea_heap(d, d <= 0, 3), pp._telea_inpaint(d, d <= 0, 3)
-    np.testing.assert_array_equal(h.view(np.int32), a.view(np.int32))
+@pytest.mark.parametrize("seed,radius", [(0, 3), (1, 1), (2, 5)])
+def test_round5_form_heap_forms_agree(seed, radius):
+    d = _holey(14, 23, seed)
+    np.testing.assert_array_equal(telea_heap(d, d <= 0, radius), telea_heap_list(d, d <= 0, radius))
