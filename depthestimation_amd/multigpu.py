@@ -351,21 +351,25 @@ class DepthPipeline:
         # keys) orders its calls across streams, so a shared handle would run one frame at a time.  The
         # other streams use shallow copies of ``core`` (same parameters and rectification cache) with
         # a handle of their own.
-        # With several streams every stream gets a copy with its own in-flight handle (dsx_params.in_flight:
-        # the balance for a lone frame is dropped) on the pipeline's device; the caller's core keeps its
-        # own handle untouched.  The copies freeze the core's parameters as they are now: a later
+        # With several streams every ring SLOT gets a copy with its own in-flight handle
+        # (dsx_params.in_flight: the balance for a lone frame is dropped) on the pipeline's device; the
+        # caller's core keeps its own handle untouched.  One handle per slot, not per stream: a
+        # handle's hole-filling timeout flag then belongs to exactly one frame in flight (frame i + depth
+        # reuses it only after frame i was finished and checked), so a timeout is reported by the frame
+        # that timed out.  The copies freeze the core's parameters as they are now: a later
         # core.configure_sgbm does not reach them (build a new pipeline after reconfiguring).
         self.cores = [core]
         self._own = []
         if len(self.streams) > 1 and getattr(core, "sgbm", None) is not None and hasattr(core.sgbm, "params"):
             self.cores = []
-            for _ in self.streams:
+            for _ in range(self.depth):
                 c = copy.copy(core)
                 c.sgbm = HipBlockMatcher(**dict(core.sgbm.params, in_flight=True, device=self.dev.index))
                 self._own.append(c.sgbm)
                 self.cores.append(c)
         self.shape = None
         self.pending: List[Optional[Tuple[int, object, object]]] = [None] * self.depth
+        self._ready: List[Tuple[int, Optional[np.ndarray]]] = []  # finished before a later frame raised
 
     def _alloc(self, shape) -> None:
         torch = self.torch
@@ -381,27 +385,42 @@ class DepthPipeline:
         core.check_fill_status()  # a frame whose hole filling timed out raises instead of being yielded
         return i, (None if z is None else self.hout[slot][: z[0], : z[1]].numpy().copy())
 
+    def _collect(self, slots) -> List[Tuple[int, Optional[np.ndarray]]]:
+        """Finish ``slots`` in order; a frame that raises keeps the ones finished before it for the
+        next call (nothing is dropped) and leaves the later ones in flight."""
+        out, self._ready = self._ready, []
+        for s in slots:
+            try:
+                out.append(self._finish(s))
+            except Exception:
+                self._ready = out
+                raise
+        return out
+
     def push(self, i: int, pair) -> List[Tuple[int, Optional[np.ndarray]]]:
         torch = self.torch
         L, R = (np.asarray(pair[0]), np.asarray(pair[1]))
         if L.dtype != np.uint8 or L.shape != R.shape or L.ndim not in (2, 3):
             raise ValueError("frames must be uint8 arrays of one shape (H x W x 3 BGR or H x W)")
-        done = []
+        done = self._collect([])
         if self.shape != L.shape:
+            self._ready = done
             done = self.drain_all()
             self._alloc(L.shape)
         slot = i % self.depth
         if self.pending[slot] is not None:
-            done.append(self._finish(slot))
+            self._ready = done
+            done = self._collect([slot])
         hl, hr = self.hin[slot]
         np.copyto(hl.numpy(), L)
         np.copyto(hr.numpy(), R)
         k = i % len(self.streams)
         st = self.streams[k]
+        core = self.cores[slot % len(self.cores)]
         with torch.cuda.stream(st):
             dl = hl.to(self.dev, non_blocking=True)
             dr = hr.to(self.dev, non_blocking=True)
-            _, z = self.cores[k].estimate_depth_device(dl, dr, stream=st)
+            _, z = core.estimate_depth_device(dl, dr, stream=st)
             zshape = None
             if z is not None:
                 if self.hout[slot] is None or self.hout[slot].shape != z.shape:
@@ -410,23 +429,23 @@ class DepthPipeline:
                 zshape = tuple(z.shape)
             ev = torch.cuda.Event()
             ev.record(st)
-        self.pending[slot] = (i, ev, zshape, self.cores[k])
-        done.extend(self.poll(keep=i))
-        return done
+        self.pending[slot] = (i, ev, zshape, core)
+        self._ready = done
+        return self.poll(keep=i)
 
     def poll(self, keep: int = -1) -> List[Tuple[int, Optional[np.ndarray]]]:
         """The oldest frames in flight whose GPU work has already finished (no waiting), in frame
         order up to the first unfinished one; frame ``keep`` stays in flight."""
-        out = []
+        slots = []
         for j, s in sorted((p[0], s) for s, p in enumerate(self.pending) if p is not None):
             if j == keep or not self.pending[s][1].query():
                 break
-            out.append(self._finish(s))
-        return out
+            slots.append(s)
+        return self._collect(slots)
 
     def drain_all(self) -> List[Tuple[int, Optional[np.ndarray]]]:
         live = sorted((p[0], s) for s, p in enumerate(self.pending) if p is not None)
-        return [self._finish(s) for _, s in live]
+        return self._collect([s for _, s in live])
 
     def close(self) -> None:
         """Finish the frames in flight and release the per-stream handles this pipeline created."""

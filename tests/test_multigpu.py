@@ -263,3 +263,121 @@ def test_banded_single_frame_is_bit_exact(nb, bs, lr):
     got = b.compute(L, R)
     b.close()
     np.testing.assert_array_equal(got, stereo_bm(L, R, **kw)["fixed"])
+
+
+# ---- device placement and per-frame status without a GPU -----------
+
+class _StubMatcher:
+    """Records the device every handle is created on (multigpu.HipBlockMatcher stand-in)."""
+    made = []
+
+    def __init__(self, **kw):
+        _StubMatcher.made.append(kw.get("device"))
+        self.params = dict(kw)
+
+    def close(self):
+        pass
+
+
+class _StubStream:
+    def __init__(self, device=None):
+        self.device = device
+
+
+def _no_cuda(monkeypatch):
+    import torch
+    from depthestimation_amd import multigpu
+    monkeypatch.setattr(multigpu, "HipBlockMatcher", _StubMatcher)
+    monkeypatch.setattr(torch.cuda, "set_device", lambda d: None)
+    monkeypatch.setattr(torch.cuda, "Stream", _StubStream)
+    _StubMatcher.made = []
+    return multigpu
+
+
+def test_pipelines_put_every_handle_on_their_device(monkeypatch):
+    """threaded_stereo.py:49-80 / SURVEY 8e: a regression to device 0 would pass the 1-GPU box's GPU
+    tests (devices=[0, 0]); here every handle a pipeline creates must name the pipeline's device."""
+    multigpu = _no_cuda(monkeypatch)
+
+    class Core:
+        pass
+
+    core = Core()
+    core.sgbm = _StubMatcher(device=0, num_disp=64)
+    _StubMatcher.made = []
+    p = multigpu.DepthPipeline(core, 3, depth=3, streams=2)
+    assert _StubMatcher.made == [3, 3, 3]                      # one in-flight handle per ring slot
+    assert all(c.sgbm.params["device"] == 3 and c.sgbm.params["in_flight"] for c in p.cores)
+    assert core.sgbm.params["device"] == 0                     # the caller's handle is untouched
+    _StubMatcher.made = []
+    multigpu.HostPipeline(5, depth=3, streams=2, num_disp=64)
+    assert _StubMatcher.made == [5, 5]
+    _StubMatcher.made = []
+    monkeypatch.setattr(multigpu._dsx, "device_count", lambda: 4)
+    multigpu.BandedStereo(devices=[0, 1, 2], block_size=5).close()
+    assert _StubMatcher.made == [0, 1, 2]
+
+
+def test_multidevice_map_builds_each_worker_on_its_device(monkeypatch):
+    multigpu = _no_cuda(monkeypatch)
+    monkeypatch.setattr(multigpu._dsx, "device_count", lambda: 4)
+    built = []
+
+    class StubHP:
+        def __init__(self, dev, **kw):
+            built.append((dev, kw.get("device")))
+            self.dev = dev
+
+        def push(self, i, pair):
+            return [(i, np.full((2, 2), self.dev, np.int16))]
+
+        def drain_all(self):
+            return []
+
+    monkeypatch.setattr(multigpu, "HostPipeline", StubHP)
+    m = multigpu.MultiDeviceStereo(devices=[0, 1, 2], num_disp=64, device=7)
+    frames = [(np.zeros((2, 2), np.uint8), np.zeros((2, 2), np.uint8))] * 7
+    outs = list(m.map(frames))
+    assert sorted(d for d, _ in built) == [0, 1, 2] and all(k is None for _, k in built)
+    assert [int(o[0, 0]) for o in outs] == [0, 1, 2, 0, 1, 2, 0]
+
+
+def test_depth_pipeline_reports_the_frame_that_timed_out(monkeypatch):
+    """a frame whose hole filling timed out raises when THAT frame is finished, frames
+    finished before it in the same call are not dropped, and later frames stay in flight."""
+    import torch
+    multigpu = _no_cuda(monkeypatch)
+    calls = []
+
+    class Ev:
+        def synchronize(self):
+            pass
+
+        def query(self):
+            return True
+
+    class Core:
+        def __init__(self, bad=False):
+            self.bad = bad
+
+        def check_fill_status(self):
+            if self.bad:
+                self.bad = False
+                raise RuntimeError("hole filling: the persistent march timed out")
+
+    class Slot:
+        def __init__(self, i):
+            self.i = i
+
+    p = multigpu.DepthPipeline(Core(), 0, depth=3, streams=1)
+    p.shape = (2, 2)
+    p.hout = [None] * 3
+    good, bad = Core(), Core(bad=True)
+    p.pending = [(0, Ev(), None, good), (1, Ev(), None, bad), (2, Ev(), None, good)]
+    with pytest.raises(RuntimeError, match="timed out"):
+        p.drain_all()                              # frame 0 finishes, frame 1 raises
+    assert [i for i, _ in p._ready] == [0]         # kept for the next call
+    assert p.pending[0] is None and p.pending[1] is None and p.pending[2] is not None
+    out = p.drain_all()
+    assert [i for i, _ in out] == [0, 2]           # nothing dropped
+    calls.append(torch)
