@@ -21,9 +21,10 @@
 //            which the queue fills the bucket) and computes T / value from the pre-bucket pixels;
 //   SWEEP 1  each child recomputes from the pre-bucket pixels and the bucket's children with a
 //            smaller fill key - a DAG, so the fixed point is unique - and caches which cells of its
-//            window those are (a bit mask per window row).  The same step ranks the bucket's pops
-//            (dense ranks by (T, push key): pairs of 256-pop chunks compared in LDS, counts added to
-//            the base) - the children's push keys, needed from the next bucket on;
+//            window those are (a bit mask per window row).  The same step sorts the bucket's pop keys
+//            (T, push key) per chunk of 2048 (bitonic, in LDS);
+//   RANK     each pop's dense rank = base + the number of smaller pop keys, by binary searches in the
+//            sorted chunks - the children's push keys, needed from the next bucket on;
 //   SWEEP i  only the children queued by the last sweep recompute: a child whose T or value changed
 //            tags the bucket's children that read it (a per-pixel word per sweep parity).  A sweep
 //            that tags nothing ends the bucket.
@@ -53,13 +54,15 @@ namespace {
 constexpr int kInside = 0x7FFFFFFF;  // fill-bucket word of an unfilled pixel of the march (known: -1)
 constexpr double kDelta = 0.7;       // T-bucket width (postprocess._TELEA_DELTA)
 constexpr float kFar = 1.0e6f;       // T of the padding and of pixels no march reaches
-constexpr int kStepBlocks = 1024;    // grid of the step launches: one block round for most steps
+constexpr int kStepBlocks = 1024;    // at most this grid for the step launches (see run_march)
 constexpr unsigned kMaxSteps = 1u << 24;
 constexpr int kMinSlots = 16;
 constexpr int kG = 16;               // lanes per child (window rows) of the grouped sweep
 constexpr int kPer = 256 / kG;       // children per block round of the grouped sweep
+constexpr int kRankChunk = 4096;     // pop keys sorted per block (registers) for the ranks
+constexpr int kRankILP = 16;         // chunks searched at once per thread
 
-enum Phase : int { kPhInit = 0, kPhPop = 1, kPhSweep = 2, kPhDone = 3, kPhSwitch = 4 };
+enum Phase : int { kPhInit = 0, kPhPop = 1, kPhSweep = 2, kPhDone = 3, kPhSwitch = 4, kPhRank = 5 };
 enum : uint8_t { kClsOther = 0, kClsHole = 1, kClsBand = 2, kClsRing = 3 };
 
 // One state slot (written by step s-1, read by step s).  Counters and minima are accumulated by the
@@ -69,6 +72,7 @@ struct alignas(128) State {
     int nF, nC;         // adjacent, 8-aligned: one 64-bit add appends to both lists (nF low word)
     int nP, march;      // pops of this bucket; 0: the outward march, 1: the inward one
     int base, rank_on;  // rank base of this bucket's pops; whether they need ranks (not the seeds)
+    int ranked, pad;    // the bucket's ranks are written (the RANK step ran)
     double bound;
     unsigned long long minF;  // bit patterns of non-negative doubles (monotone as integers)
 };
@@ -90,6 +94,7 @@ struct Args {
     unsigned long long *key;  // fill key of the current bucket's children
     unsigned *pk, *rank, *par;   // push key and pop rank of pops; parent * 4 + direction of filled pixels
     unsigned long long *queued;  // [sweep & 1][pixel]: (bucket ordinal << 32 | sweep) it was tagged for
+    unsigned long long *sk;   // this bucket's pop keys (T, push key), sorted per chunk of kRankChunk
     uint16_t *lessm;          // [list position][window row]: cells that are children filled earlier
     int *F[2], *C[2], *P;     // frontier, children (ping-pong), this bucket's pops
     uint8_t *cls, *rowd;      // pixel class; a hole within `radius` along the row
@@ -217,8 +222,8 @@ __global__ __launch_bounds__(256) void tl_init_b(Args a) {
 // ---- one step ----------------------------------------------------------------------------------
 
 struct Mode {
-    int what;  // kPhPop, kPhSweep, kPhDone, kPhSwitch
-    int k, b, nb, sweep, lsel, march;
+    int what;  // kPhPop, kPhSweep, kPhDone, kPhSwitch, kPhRank
+    int k, b, nb, sweep, lsel, march, ranked;
     int nIn;    // POP: survivors; sweeps: list length
     int nPrev;  // POP: the last bucket's children
     int nP, base, rank_on;
@@ -248,6 +253,7 @@ __device__ __forceinline__ Mode decide(const State &S, unsigned long long mcv, b
     m.nP = S.nP;
     m.base = S.base;
     m.rank_on = S.rank_on;
+    m.ranked = S.ranked;
     const int finish = S.march == 0 ? kPhSwitch : kPhDone;  // the end of a march
     if (S.phase == kPhDone) {
         m.what = kPhDone;
@@ -261,6 +267,13 @@ __device__ __forceinline__ Mode decide(const State &S, unsigned long long mcv, b
         m.what = kPhSweep;
         m.sweep = 0;
         m.full = true;
+        m.nIn = S.nC;
+        return m;
+    }
+    // after sweep 1 (which sorted the pop keys per chunk) the bucket's pops get their ranks
+    if (S.phase == kPhSweep && S.sweep == 1 && S.rank_on && S.nP > 0 && !S.ranked) {
+        m.what = kPhRank;
+        m.sweep = 1;
         m.nIn = S.nC;
         return m;
     }
@@ -302,6 +315,7 @@ __device__ __forceinline__ Mode decide(const State &S, unsigned long long mcv, b
     m.nb = S.nb + 1;
     m.base = S.base + S.nP;  // ranks of this bucket's pops follow the last bucket's
     m.rank_on = 1;
+    m.ranked = 0;
     return m;
 }
 
@@ -568,7 +582,7 @@ __device__ void fill_child(const Args &a, const Mode &m, int i, int c, float &tc
             rowbase += 2 * h + 1 - (yy == 0);
         }
         const int wy = j;
-#pragma unroll
+#pragma unroll 1
         for (int dx = -R; dx <= R; ++dx) {
             if (dx * dx + dy * dy > R * R || (dx == 0 && dy == 0)) continue;
             const int cx = x + dx;
@@ -746,9 +760,8 @@ __device__ void do_pop(const Args &a, const Mode &m, State &N, int blk, int nblk
                     if (nb[d] >= 0 && fn[d] == kInside) old[d] = atomicCAS(&a.fb[nb[d]], kInside, m.b);
 #pragma unroll
                 for (int d = 0; d < 4; ++d) km |= (uint32_t)(nb[d] >= 0 && fn[d] == kInside && old[d] == kInside) << d;
-                // its push key (ranked in sweep 1 by (T, push key)) and rank base
+                // its push key (ranked after sweep 1 by (T, push key))
                 a.pk[p] = pushkey_of(a, p, a.fb[p]);
-                a.rank[p] = (unsigned)m.base;
             } else {
                 keep = 1;
                 const unsigned long long tb = dbits((double)t);
@@ -829,44 +842,120 @@ __device__ void do_pop(const Args &a, const Mode &m, State &N, int blk, int nblk
     block_min_to(mnc, &a.ctl->minC[m.nb % 3][blk % kMinSlots]);
 }
 
-// Dense ranks of this bucket's pops by (T, push key): rank = base + the number of pops with a
-// smaller key.  Pairs (chunk ci, chunk cj) of 256 pops: chunk cj's keys in LDS, each thread counts
-// those below its own pop's key and adds the count (the POP wrote the base).
+__device__ __forceinline__ unsigned long long pop_key(const Args &a, int p) {
+    return (unsigned long long)__float_as_uint(a.T[p]) << 32 | a.pk[p];
+}
+
+// Sweep 1's side task: this bucket's pop keys (T, push key; unique) sorted per chunk of kRankChunk,
+// one chunk per block, into sk.  Bitonic network with the chunk in registers (thread t holds elements
+// 16 t .. 16 t + 15): partners 1-8 apart inside a thread, 16-512 apart across the wave by shuffles,
+// 1024 and more apart through LDS (three stages of the 4096 network).
+__device__ __forceinline__ unsigned long long shfl_xor_u64(unsigned long long v, int m) {
+    const unsigned lo = (unsigned)__shfl_xor((int)(unsigned)v, m), hi = (unsigned)__shfl_xor((int)(unsigned)(v >> 32), m);
+    return (unsigned long long)hi << 32 | lo;
+}
+__device__ void do_sort_chunks(const Args &a, const Mode &m, int blk, int nblk, unsigned long long *buf) {
+    constexpr int E = kRankChunk / 256;  // elements per thread
+    const int np = m.nP;
+    const int nch = (np + kRankChunk - 1) / kRankChunk;
+    const int t = threadIdx.x;
+    for (int c = blk; c < nch; c += nblk) {  // block-uniform
+        const int c0 = c * kRankChunk;
+        const int len = np - c0 < kRankChunk ? np - c0 : kRankChunk;
+        unsigned long long v[E];
+        int pi[E];
+#pragma unroll
+        for (int i = 0; i < E; ++i) pi[i] = t * E + i < len ? a.P[c0 + t * E + i] : -1;
+#pragma unroll
+        for (int i = 0; i < E; ++i) v[i] = pi[i] >= 0 ? pop_key(a, pi[i]) : ~0ull;
+        for (int k = 2; k <= kRankChunk; k <<= 1) {
+            for (int j = k >> 1; j > 0; j >>= 1) {  // block-uniform
+                if (j < E) {
+#pragma unroll
+                    for (int i = 0; i < E; ++i) {
+                        if (i & j) continue;
+                        const int l = i | j;
+                        const bool up = ((t * E + i) & k) == 0;
+                        const unsigned long long x = v[i], y = v[l];
+                        const bool sw = (x > y) == up;
+                        v[i] = sw ? y : x;
+                        v[l] = sw ? x : y;
+                    }
+                } else if (j < E * 64) {
+                    const int tm = j / E;
+                    const bool lower = (t & tm) == 0;
+                    const bool up = ((t * E) & k) == 0;
+#pragma unroll
+                    for (int i = 0; i < E; ++i) {
+                        const unsigned long long o = shfl_xor_u64(v[i], tm);
+                        const bool keep_min = lower == up;
+                        v[i] = keep_min ? (o < v[i] ? o : v[i]) : (o > v[i] ? o : v[i]);
+                    }
+                } else {
+#pragma unroll
+                    for (int i = 0; i < E; ++i) buf[t * E + i] = v[i];
+                    __syncthreads();
+                    const int tm = j / E;
+                    const bool lower = (t & tm) == 0;
+                    const bool up = ((t * E) & k) == 0;
+#pragma unroll
+                    for (int i = 0; i < E; ++i) {
+                        const unsigned long long o = buf[(t ^ tm) * E + i];
+                        const bool keep_min = lower == up;
+                        v[i] = keep_min ? (o < v[i] ? o : v[i]) : (o > v[i] ? o : v[i]);
+                    }
+                    __syncthreads();
+                }
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < E; ++i)
+            if (t * E + i < len) a.sk[c0 + t * E + i] = v[i];
+    }
+}
+
+// RANK: dense ranks of this bucket's pops by (T, push key) - base + the number of pop keys below
+// its own, summed over the sorted chunks by binary searches (kRankILP chunks in flight per thread).
+// The children's push keys read them from the next bucket on.
 __device__ void do_rank(const Args &a, const Mode &m, int blk, int nblk) {
     const int np = m.nP;
-    const int nch = (np + 255) / 256;
-    __shared__ unsigned long long kc[256];
-    for (int pr = blk; pr < nch * nch; pr += nblk) {  // block-uniform
-        const int ci = pr / nch, cj = pr - ci * nch;
-        const int jj = cj * 256 + (int)threadIdx.x;
-        unsigned long long kj = ~0ull;
-        if (jj < np) {
-            const int q = a.P[jj];
-            kj = (unsigned long long)__float_as_uint(a.T[q]) << 32 | a.pk[q];
+    const int nch = (np + kRankChunk - 1) / kRankChunk;
+    for (int i = blk * 256 + (int)threadIdx.x; i < np; i += nblk * 256) {
+        const int p = a.P[i];
+        const unsigned long long key = pop_key(a, p);
+        unsigned cnt = 0;
+        for (int c0 = 0; c0 < nch; c0 += kRankILP) {
+            int lo[kRankILP], len[kRankILP];
+#pragma unroll
+            for (int u = 0; u < kRankILP; ++u) {
+                const int c = c0 + u;
+                lo[u] = 0;
+                len[u] = c < nch ? (np - c * kRankChunk < kRankChunk ? np - c * kRankChunk : kRankChunk) : 0;
+            }
+            // lower_bound in each chunk: first position whose key is not below `key`
+            for (int step = kRankChunk; step > 0; step >>= 1) {
+                unsigned long long v[kRankILP];
+#pragma unroll
+                for (int u = 0; u < kRankILP; ++u) {
+                    const int q = lo[u] + step - 1;
+                    v[u] = q < len[u] ? a.sk[(int64_t)(c0 + u) * kRankChunk + q] : ~0ull;
+                }
+#pragma unroll
+                for (int u = 0; u < kRankILP; ++u)
+                    if (lo[u] + step - 1 < len[u] && v[u] < key) lo[u] += step;
+            }
+#pragma unroll
+            for (int u = 0; u < kRankILP; ++u) cnt += (unsigned)lo[u];
         }
-        kc[threadIdx.x] = kj;
-        const int ii = ci * 256 + (int)threadIdx.x;
-        int p = -1;
-        unsigned long long ki = 0;
-        if (ii < np) {
-            p = a.P[ii];
-            ki = (unsigned long long)__float_as_uint(a.T[p]) << 32 | a.pk[p];
-        }
-        __syncthreads();
-        if (p >= 0) {
-            unsigned cnt = 0;
-            const int lim = np - cj * 256 < 256 ? np - cj * 256 : 256;
-            for (int u = 0; u < lim; ++u) cnt += kc[u] < ki;
-            if (cnt) atomicAdd(&a.rank[p], cnt);
-        }
-        __syncthreads();
+        a.rank[p] = (unsigned)m.base + cnt;
     }
 }
 
 // SWEEP (m.sweep >= 1) over the bucket's children C[lsel]: every one (full), or the ones tagged for
-// this sweep (a child's group checks its tag).  Sweep 1 also ranks the bucket's pops.
+// this sweep (a child's group checks its tag).  Sweep 1 also sorts the bucket's pop keys per chunk.
 template <int RW>
-__device__ void do_sweep(const Args &a, const Mode &m, unsigned *tagw, int blk, int nblk, WinLds<RW> *lds) {
+__device__ void do_sweep(const Args &a, const Mode &m, unsigned *tagw, int blk, int nblk, WinLds<RW> *lds,
+                         unsigned long long *sortbuf) {
     const int *Cl = a.C[m.lsel];
     unsigned long long mn = ~0ull;
     bool tagged = false;
@@ -910,7 +999,10 @@ __device__ void do_sweep(const Args &a, const Mode &m, unsigned *tagw, int blk, 
             }
         }
     }
-    if (m.sweep == 1 && m.rank_on && m.nP > 0) do_rank(a, m, blk, nblk);
+    if (m.sweep == 1 && m.rank_on && m.nP > 0) {
+        __syncthreads();  // the sort buffer aliases the lane groups' windows
+        do_sort_chunks(a, m, blk, nblk, sortbuf);
+    }
     if (__syncthreads_or(tagged) && threadIdx.x == 0)
         __hip_atomic_store(tagw + blk % kMinSlots, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     // T of a child only falls over the sweeps (more neighbours filled before it), so the minimum of
@@ -957,7 +1049,11 @@ __device__ void do_switch(const Args &a, State &N, int blk, int nblk) {
 // Step s: returns the mode it ran (kPhDone: the march had finished).
 template <int RW>
 __device__ int step(const Args &a, unsigned s, int blk, int nblk) {
-    __shared__ WinLds<RW> lds[RW > 0 ? kPer : 1];  // one child window per lane group (inward sweeps)
+    // one child window per lane group (inward sweeps), or the pop keys of one chunk (the sort)
+    constexpr size_t kWin = sizeof(WinLds<RW>) * (RW > 0 ? kPer : 1), kSort = sizeof(unsigned long long) * kRankChunk;
+    __shared__ __attribute__((aligned(16))) unsigned char smem[kWin > kSort ? kWin : kSort];
+    WinLds<RW> *lds = reinterpret_cast<WinLds<RW> *>(smem);
+    unsigned long long *sortbuf = reinterpret_cast<unsigned long long *>(smem);
     Ctl *ctl = a.ctl;
     const State S = ctl->st[s % 3];
     const int lane = threadIdx.x & 63;
@@ -981,7 +1077,17 @@ __device__ int step(const Args &a, unsigned s, int blk, int nblk) {
         N.march = m.march;
         N.base = m.base;
         N.rank_on = m.rank_on;
-        if (m.what == kPhSweep) {  // carried: the POP's outputs
+        N.ranked = m.ranked;
+        if (m.what == kPhRank) {  // carried like a sweep; the next step decides as after sweep 1
+            N.phase = kPhSweep;
+            N.ranked = 1;
+            N.lsel = m.lsel;
+            N.nF = S.nF;
+            N.nC = S.nC;
+            N.nP = S.nP;
+            N.minF = S.minF;
+            for (int q = 0; q < kMinSlots; ++q) ctl->tagged[(s + 1) % 3][q] = ctl->tagged[s % 3][q];
+        } else if (m.what == kPhSweep) {  // carried: the POP's outputs
             N.lsel = m.lsel;
             N.nF = S.nF;
             N.nC = S.nC;
@@ -1011,8 +1117,9 @@ __device__ int step(const Args &a, unsigned s, int blk, int nblk) {
         }
     }
     if (m.what == kPhPop) do_pop<RW>(a, m, N, blk, nblk, lds);
-    else if (m.what == kPhSweep) do_sweep<RW>(a, m, ctl->tagged[(s + 1) % 3], blk, nblk, lds);
+    else if (m.what == kPhSweep) do_sweep<RW>(a, m, ctl->tagged[(s + 1) % 3], blk, nblk, lds, sortbuf);
     else if (m.what == kPhSwitch) do_switch(a, N, blk, nblk);
+    else if (m.what == kPhRank) do_rank(a, m, blk, nblk);
     return m.what;
 }
 
@@ -1111,6 +1218,8 @@ Args views(void *ws, int H, int W) {
     w += align256(n * 4);
     a.queued = reinterpret_cast<unsigned long long *>(w);
     w += align256(2 * n * 8);
+    a.sk = reinterpret_cast<unsigned long long *>(w);
+    w += align256(n * 8);
     a.lessm = reinterpret_cast<uint16_t *>(w);
     w += align256(n * 2 * (size_t)kG);
     for (int i = 0; i < 2; ++i) {
@@ -1187,9 +1296,10 @@ hipError_t run_march(Args a, int ncu, int *hw, const InpaintOpts &o, hipStream_t
         (void)hipEventCreate(&e0);
         (void)hipEventCreate(&e1);
     }
+    const int sgrid = kStepBlocks;
     for (int s = 0; s < nsteps; ++s) {
         if (trace) (void)hipEventRecord(e0, st);
-        hipLaunchKernelGGL(tl_step<RW>, dim3(kStepBlocks), dim3(256), 0, st, a, (unsigned)s);
+        hipLaunchKernelGGL(tl_step<RW>, dim3(sgrid), dim3(256), 0, st, a, (unsigned)s);
         if ((e = dbg_sync("tl_step", st)) != hipSuccess) return e;
         if (trace) {
             (void)hipEventRecord(e1, st);
@@ -1199,8 +1309,8 @@ hipError_t run_march(Args a, int ncu, int *hw, const InpaintOpts &o, hipStream_t
                 return e;
             float ms = 0;
             (void)hipEventElapsedTime(&ms, e0, e1);
-            fprintf(stderr, "step %d: %.1f us march %d phase %d k %d b %d sweep %d lsel %d nF %d nC %d nP %d bound %.3f\n", s,
-                    ms * 1e3f, S.march, S.phase, S.k, S.b, S.sweep, S.lsel, S.nF, S.nC, S.nP, S.bound);
+            fprintf(stderr, "step %d: %.1f us march %d phase %d k %d b %d sweep %d lsel %d nF %d nC %d nP %d ranked %d bound %.3f\n",
+                    s, ms * 1e3f, S.march, S.phase, S.k, S.b, S.sweep, S.lsel, S.nF, S.nC, S.nP, S.ranked, S.bound);
             if (S.phase == kPhDone) break;
         }
     }
@@ -1229,7 +1339,7 @@ hipError_t run_march(Args a, int ncu, int *hw, const InpaintOpts &o, hipStream_t
 
 size_t inpaint_workspace(int H, int W) {
     const size_t n = (size_t)H * W;
-    return align256(sizeof(Ctl)) + 6 * align256(n * 4) + align256(n * 8) + align256(2 * n * 8) +
+    return align256(sizeof(Ctl)) + 6 * align256(n * 4) + 2 * align256(n * 8) + align256(2 * n * 8) +
            align256(n * 2 * (size_t)kG) + 4 * align256(n * 4) + 2 * align256(n);
 }
 
