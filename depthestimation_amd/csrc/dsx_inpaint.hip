@@ -43,6 +43,7 @@
 #include <cmath>
 #include <cstdlib>
 #include <mutex>
+#include <type_traits>
 #include <unordered_map>
 
 namespace dsx {
@@ -448,6 +449,10 @@ __device__ __forceinline__ void ring_child(const Args &a, const Mode &m, int i, 
     tagged = tagged || dep != 0;
 }
 
+// OpenCV's distance weight (float)(1 / (|r|^2 sqrt(|r|^2))) by |r|^2 (<= 36: radius <= 6), computed in
+// double and rounded to float offline (the same bits as the expression)
+__constant__ float kDst[37] = {0.0f, 0x1.0000000000000p+0f, 0x1.6a09e60000000p-2f, 0x1.8a23460000000p-3f, 0x1.0000000000000p-3f, 0x1.6e5b7e0000000p-4f, 0x1.16b2900000000p-4f, 0x1.ba53900000000p-5f, 0x1.6a09e60000000p-5f, 0x1.2f684c0000000p-5f, 0x1.030dc40000000p-5f, 0x1.c116620000000p-6f, 0x1.8a23460000000p-6f, 0x1.5d8be40000000p-6f, 0x1.38c5a20000000p-6f, 0x1.1a05a40000000p-6f, 0x1.0000000000000p-6f, 0x1.d37e9a0000000p-7f, 0x1.ad15360000000p-7f, 0x1.8ba85a0000000p-7f, 0x1.6e5b7e0000000p-7f, 0x1.5480c80000000p-7f, 0x1.3d8d820000000p-7f, 0x1.2911d00000000p-7f, 0x1.16b2900000000p-7f, 0x1.0624de0000000p-7f, 0x1.ee55560000000p-8f, 0x1.d320520000000p-8f, 0x1.ba53900000000p-8f, 0x1.a3a5560000000p-8f, 0x1.8ed6e20000000p-8f, 0x1.7bb27c0000000p-8f, 0x1.6a09e60000000p-8f, 0x1.59b52a0000000p-8f, 0x1.4a918e0000000p-8f, 0x1.3c80c60000000p-8f, 0x1.2f684c0000000p-8f};
+
 // ---- the inward march: Telea's value, kG lanes per child (lane j = window row j - RW) ----
 
 template <int RW>
@@ -472,7 +477,7 @@ template <int RW>
 using WinLds = typename Win<RW == 0 ? 2 : RW>::Lds;
 
 template <int RW>
-__device__ void fill_child(const Args &a, const Mode &m, int i, int c, float &tc, bool &tagged, WinLds<RW> &L) {
+__device__ __forceinline__ void fill_child(const Args &a, const Mode &m, int i, int c, float &tc, bool &tagged, WinLds<RW> &L) {
     using WN = Win<RW>;
     constexpr int NC = WN::NC, R = WN::R, ND = WN::ND;
     const int j = (int)(threadIdx.x & (kG - 1));
@@ -592,8 +597,7 @@ __device__ void fill_child(const Args &a, const Mode &m, int i, int c, float &tc
                 const int cA = wcol(cx + (cx == 0)), cR = wcol(cx + 1 - (cx == W - 1)), cL = wcol(cx - 1 + (cx == 0)),
                           cB = wcol(cx - (cx == W - 1));
                 const float ry = (float)(-dy), rx = (float)(-dx);
-                const float vl = rx * rx + ry * ry;
-                const float dst = (float)(1.0 / ((double)vl * __builtin_sqrt((double)vl)));
+                const float dst = kDst[dx * dx + dy * dy];
                 const float lev = (float)(1.0 / (1.0 + __builtin_fabs((double)(TT(wy, wx) - tp))));
                 float dir = rx * gtx + ry * gty;
                 if (__builtin_fabs((double)dir) <= 0.01) dir = 0.000001f;
@@ -652,7 +656,7 @@ __device__ __forceinline__ bool avail_wide(const Args &a, int q, int b, bool key
     if (f != b || !keys) return false;
     return a.key[q] < me;
 }
-__device__ void fill_child_wide(const Args &a, const Mode &m, int c, bool &changed, float &tc) {
+__device__ __forceinline__ void fill_child_wide(const Args &a, const Mode &m, int c, bool &changed, float &tc) {
     const int H = a.H, W = a.W, b = m.b, R = a.radius;
     const int y = c / W, x = c - y * W;
     const bool first = m.sweep == 0;
@@ -724,7 +728,7 @@ __device__ void fill_child_wide(const Args &a, const Mode &m, int c, bool &chang
 // add, and runs sweep 0 of its children right there (the pops, and so every child's parent, are fixed
 // for the whole step, and sweep 0 reads no child of the bucket).
 template <int RW>
-__device__ void do_pop(const Args &a, const Mode &m, State &N, int blk, int nblk, WinLds<RW> *lds) {
+__device__ __forceinline__ void do_pop(const Args &a, const Mode &m, State &N, int blk, int nblk, WinLds<RW> *lds) {
     const int *Fi = a.F[m.lsel], *Ci = a.C[m.lsel];
     int *Fo = a.F[m.lsel ^ 1], *Co = a.C[m.lsel ^ 1];
     const int tot = m.nIn + m.nPrev;
@@ -854,7 +858,7 @@ __device__ __forceinline__ unsigned long long shfl_xor_u64(unsigned long long v,
     const unsigned lo = (unsigned)__shfl_xor((int)(unsigned)v, m), hi = (unsigned)__shfl_xor((int)(unsigned)(v >> 32), m);
     return (unsigned long long)hi << 32 | lo;
 }
-__device__ void do_sort_chunks(const Args &a, const Mode &m, int blk, int nblk, unsigned long long *buf) {
+__device__ __forceinline__ void do_sort_chunks(const Args &a, const Mode &m, int blk, int nblk, unsigned long long *buf) {
     constexpr int E = kRankChunk / 256;  // elements per thread
     const int np = m.nP;
     const int nch = (np + kRankChunk - 1) / kRankChunk;
@@ -871,16 +875,26 @@ __device__ void do_sort_chunks(const Args &a, const Mode &m, int blk, int nblk, 
         for (int k = 2; k <= kRankChunk; k <<= 1) {
             for (int j = k >> 1; j > 0; j >>= 1) {  // block-uniform
                 if (j < E) {
+                    // partners inside the thread: j is one of E/2 ... 1, made a constant so every
+                    // register index is static
+                    auto cx = [&](auto jc) __attribute__((always_inline)) {
+                        constexpr int J = decltype(jc)::value;
 #pragma unroll
-                    for (int i = 0; i < E; ++i) {
-                        if (i & j) continue;
-                        const int l = i | j;
-                        const bool up = ((t * E + i) & k) == 0;
-                        const unsigned long long x = v[i], y = v[l];
-                        const bool sw = (x > y) == up;
-                        v[i] = sw ? y : x;
-                        v[l] = sw ? x : y;
-                    }
+                        for (int i = 0; i < E; ++i) {
+                            if (i & J) continue;
+                            const int l = i | J;
+                            const bool up = ((t * E + i) & k) == 0;
+                            const unsigned long long x = v[i], y = v[l];
+                            const bool sw = (x > y) == up;
+                            v[i] = sw ? y : x;
+                            v[l] = sw ? x : y;
+                        }
+                    };
+                    static_assert(E == 16, "in-thread stages below are written for 16 elements per thread");
+                    if (j == 8) cx(std::integral_constant<int, 8>{});
+                    else if (j == 4) cx(std::integral_constant<int, 4>{});
+                    else if (j == 2) cx(std::integral_constant<int, 2>{});
+                    else cx(std::integral_constant<int, 1>{});
                 } else if (j < E * 64) {
                     const int tm = j / E;
                     const bool lower = (t & tm) == 0;
@@ -917,7 +931,7 @@ __device__ void do_sort_chunks(const Args &a, const Mode &m, int blk, int nblk, 
 // RANK: dense ranks of this bucket's pops by (T, push key) - base + the number of pop keys below
 // its own, summed over the sorted chunks by binary searches (kRankILP chunks in flight per thread).
 // The children's push keys read them from the next bucket on.
-__device__ void do_rank(const Args &a, const Mode &m, int blk, int nblk) {
+__device__ __forceinline__ void do_rank(const Args &a, const Mode &m, int blk, int nblk) {
     const int np = m.nP;
     const int nch = (np + kRankChunk - 1) / kRankChunk;
     for (int i = blk * 256 + (int)threadIdx.x; i < np; i += nblk * 256) {
@@ -954,7 +968,7 @@ __device__ void do_rank(const Args &a, const Mode &m, int blk, int nblk) {
 // SWEEP (m.sweep >= 1) over the bucket's children C[lsel]: every one (full), or the ones tagged for
 // this sweep (a child's group checks its tag).  Sweep 1 also sorts the bucket's pop keys per chunk.
 template <int RW>
-__device__ void do_sweep(const Args &a, const Mode &m, unsigned *tagw, int blk, int nblk, WinLds<RW> *lds,
+__device__ __forceinline__ void do_sweep(const Args &a, const Mode &m, unsigned *tagw, int blk, int nblk, WinLds<RW> *lds,
                          unsigned long long *sortbuf) {
     const int *Cl = a.C[m.lsel];
     unsigned long long mn = ~0ull;
@@ -1013,7 +1027,7 @@ __device__ void do_sweep(const Args &a, const Mode &m, unsigned *tagw, int blk, 
 // SWITCH (the outward march is done): negate T of every pixel it popped (the band and the ring pixels
 // it reached), mark the holes INSIDE, and list the inward march's first bucket - the holes with a
 // known 4-neighbour (every band pixel is a seed that pops at bound 0.7) - in C[0].
-__device__ void do_switch(const Args &a, State &N, int blk, int nblk) {
+__device__ __forceinline__ void do_switch(const Args &a, State &N, int blk, int nblk) {
     const int H = a.H, W = a.W;
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     __shared__ int wsum[4], bbase;
@@ -1048,7 +1062,7 @@ __device__ void do_switch(const Args &a, State &N, int blk, int nblk) {
 
 // Step s: returns the mode it ran (kPhDone: the march had finished).
 template <int RW>
-__device__ int step(const Args &a, unsigned s, int blk, int nblk) {
+__device__ __forceinline__ int step(const Args &a, unsigned s, int blk, int nblk) {
     // one child window per lane group (inward sweeps), or the pop keys of one chunk (the sort)
     constexpr size_t kWin = sizeof(WinLds<RW>) * (RW > 0 ? kPer : 1), kSort = sizeof(unsigned long long) * kRankChunk;
     __shared__ __attribute__((aligned(16))) unsigned char smem[kWin > kSort ? kWin : kSort];
