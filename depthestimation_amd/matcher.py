@@ -423,6 +423,9 @@ def fill_holes_status(workspace=None):
     holes were left unfilled); the condition is cleared.  ``workspace``: a ``FillWorkspace`` (its
     own flag, dsx_fill_holes_status_ws); None: every flag of the process (dsx_fill_holes_status)."""
     L = _dsx.lib()
+    if workspace is not None and workspace.take_pending():
+        _dsx.check(_dsx.DSX_EHIP, "hole filling: the persistent march timed out (on this workspace's previous "
+                                  "buffer); the holes of that call were left unfilled")
     rc = L.dsx_fill_holes_status() if workspace is None else L.dsx_fill_holes_status_ws(workspace.ptr)
     _dsx.check(rc, "hole filling")
 
@@ -430,19 +433,42 @@ def fill_holes_status(workspace=None):
 class FillWorkspace:
     """Device workspace of the hole-filling march on one device, grown on demand.  It carries the
     march's timeout flag and step history (both keyed by the workspace in the library), so calls
-    that share one report to it: ``fill_holes_status(ws)``.  One stream at a time."""
+    that share one report to it: ``fill_holes_status(ws)``.  One stream at a time.
+
+    When the buffer is replaced (a larger frame, another device) the old key is released in the
+    library (``dsx_fill_holes_release``, after the device has finished with it) and a timeout it still
+    held is kept here, so ``fill_holes_status(ws)`` reports it (a new buffer at a recycled
+    address must not inherit the old flag, and the old flag must not be lost)."""
 
     def __init__(self, device=None):
         self.device = device
         self.buf = None
+        self._pending = False
+
+    def _release(self):
+        if self.buf is None:
+            return
+        import torch
+        torch.cuda.synchronize(self.buf.device)  # the device may still write the key's mapped words
+        if _dsx.lib().dsx_fill_holes_release(self.buf.data_ptr()) != _dsx.DSX_OK:
+            self._pending = True
 
     def get(self, nbytes, device, stream=None):
         import torch
         if self.buf is None or self.buf.numel() < nbytes or self.buf.device != device:
             if self.buf is not None:
-                _keep_until_done(self.buf, stream)
+                self._release()
             self.buf = torch.empty(nbytes, dtype=torch.uint8, device=device)
         return self.buf
+
+    def take_pending(self) -> bool:
+        p, self._pending = self._pending, False
+        return p
+
+    def close(self):
+        """Release the buffer and its key in the library (a pending timeout stays reportable)."""
+        self._release()
+        self.buf = None
 
     @property
     def ptr(self):
@@ -450,6 +476,7 @@ class FillWorkspace:
 
 
 _fill_ws = {}
+_FILL_WS_MAX = 8  # default workspaces kept (per (kind, device, stream)); the least recently used is closed
 
 
 def _stream_ptr(stream):
@@ -459,12 +486,16 @@ def _stream_ptr(stream):
 def default_workspace(device, stream, kind="fill"):
     """The workspace shared by the ``kind`` calls ("fill": fill_holes_device, "post":
     postprocess_full_device) on one (device, stream): a stable key for the library's step history
-    and timeout flag."""
+    and timeout flag.  At most ``_FILL_WS_MAX`` are kept (hundreds of MB each at 1080p); callers that use
+    many streams should pass their own ``FillWorkspace``."""
     import torch
     key = (kind, device.index, _stream_ptr(stream) or torch.cuda.current_stream(device).cuda_stream)
-    ws = _fill_ws.get(key)
+    ws = _fill_ws.pop(key, None)
     if ws is None:
-        ws = _fill_ws[key] = FillWorkspace(device)
+        ws = FillWorkspace(device)
+        while len(_fill_ws) >= _FILL_WS_MAX:  # bounded (ADVICE r5): callers cycling through many streams
+            _fill_ws.pop(next(iter(_fill_ws))).close()
+    _fill_ws[key] = ws  # most recently used last
     return ws
 
 

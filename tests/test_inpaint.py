@@ -394,3 +394,24 @@ def test_fill_timeout_is_per_handle():
     np.testing.assert_array_equal(da.cpu().numpy(), db.cpu().numpy())
     a.close()
     b.close()
+
+
+@pytest.mark.gpu
+def test_fill_workspace_growth_keeps_and_releases_the_flag():
+    """when a FillWorkspace grows, its old buffer's key is released in the library
+    (a new buffer at a recycled address starts clean) and a timeout the old key held is still reported."""
+    import torch
+    from depthestimation_amd.matcher import FillWorkspace, fill_holes_device, fill_holes_status
+    ws = FillWorkspace()
+    d = np.zeros((160, 240), np.float32)
+    d[7, 200] = 5.0
+    fill_holes_device(torch.from_numpy(d).cuda(), radius=3, workspace=ws, spin_limit=1, steps=-1)  # times out
+    torch.cuda.synchronize()
+    big = _holey(300, 400, 5)
+    got = fill_holes_device(torch.from_numpy(big).cuda(), radius=3, workspace=ws)  # grows the buffer
+    torch.cuda.synchronize()
+    with pytest.raises(RuntimeError, match="timed out"):
+        fill_holes_status(ws)
+    fill_holes_status(ws)  # reported once
+    np.testing.assert_array_equal(_bits(got.cpu().numpy()), _bits(telea_heap(big, big <= 0, 3)))
+    ws.close()

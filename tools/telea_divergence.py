@@ -1,9 +1,11 @@
-"""How far the product's Telea march (the GPU's form, postprocess._telea_inpaint: the layered march
-until round 4, the arrival-time bucket march since round 5) departs from the heap-ordered march of
-cv2.inpaint (oracle/telea_heap.py) on the reference pipeline's real input: the
-C oracle's matcher map at a BASELINE config, cropped and passed through the speckle filter and the
-outlier removal exactly as _process_pair does before fill_holes (stereo_core.py:175-184,
-postprocess.py:120-171, radius 3).  Writes one JSON line per config.  CPU only.
+"""How far cv2.inpaint's own arithmetic (oracle/telea_cv.c: the outward march's negative T, the
+normalised gradient term, + 0.5, float32 sums; the product's form since round 6) moves the filled
+disparities away from the round-5 form (oracle/telea_heap.py: Telea's paper weights in float64, known
+pixels at T = 0, the same queue order), on the reference pipeline's real input: the C oracle's
+matcher map at a BASELINE config, cropped and passed through the speckle filter and the outlier
+removal exactly as _process_pair does before fill_holes (stereo_core.py:175-184, postprocess.py:
+120-171, radius 3).  Also the share of that distance due to the outward march alone (the OpenCV form
+without it: telea_cv with_ring=False).  One JSON line per config.  CPU only.
 
 usage: python tools/telea_divergence.py [c4 c2 ...]
 """
@@ -19,7 +21,19 @@ from depthestimation_amd import postprocess as pp  # noqa: E402
 from depthestimation_amd.configs import CONFIGS, matcher_kwargs  # noqa: E402
 from depthestimation_amd.synthetic import stereo_pair  # noqa: E402
 from oracle.cref import CRef  # noqa: E402
+from oracle.telea_cv import telea  # noqa: E402
 from oracle.telea_heap import telea_heap  # noqa: E402
+
+
+def stats(a, b, hole):
+    d = np.abs(a.astype(np.float64) - b.astype(np.float64))[hole]
+    if d.size == 0:
+        return {}
+    return {"max_abs_diff_px": round(float(d.max()), 4), "mean_abs_diff_px": round(float(d.mean()), 4),
+            "p99_abs_diff_px": round(float(np.percentile(d, 99)), 4),
+            "frac_holes_diff_gt_0.25px": round(float((d > 0.25).mean()), 4),
+            "frac_holes_diff_gt_1px": round(float((d > 1.0).mean()), 4),
+            "after_median_frac_pixels_differ": round(float((pp.median_blur3(a) != pp.median_blur3(b)).mean()), 4)}
 
 
 def main():
@@ -32,26 +46,16 @@ def main():
         d[pp.detect_outliers(d, threshold=2.5, kernel_size=5)] = 0
         hole = d <= 0
         t0 = time.time()
-        lay = pp._telea_inpaint(d, hole, 3)
+        cv = telea(d, hole, 3)
         t1 = time.time()
-        heap = telea_heap(d, hole, 3)
+        cv_noring = telea(d, hole, 3, with_ring=False)
+        r5 = telea_heap(d, hole, 3)
         t2 = time.time()
-        filled = hole & (lay != d)  # pixels the march reached
-        diff = np.abs(heap.astype(np.float64) - lay.astype(np.float64))[hole]
-        fin = np.median(pp.median_blur3(heap)[...] != pp.median_blur3(lay))
-        out = {"config": c, "H": H, "W_cropped": W - D, "matcher": matcher_kwargs(cfg), "hole_pixels": int(hole.sum()),
-               "reached": int(filled.sum()),
-               "max_abs_diff_px": float(diff.max()) if diff.size else 0.0,
-               "mean_abs_diff_px": float(diff.mean()) if diff.size else 0.0,
-               "frac_holes_differ": float((diff > 0).mean()) if diff.size else 0.0,
-               "frac_holes_diff_gt_1e-3": float((diff > 1e-3).mean()) if diff.size else 0.0,
-               "frac_holes_diff_gt_0.25px": float((diff > 0.25).mean()) if diff.size else 0.0,
-               "frac_holes_diff_gt_1px": float((diff > 1.0).mean()) if diff.size else 0.0,
-               "p99_abs_diff_px": float(np.percentile(diff, 99)) if diff.size else 0.0,
-               "after_median_frac_pixels_differ": float((pp.median_blur3(heap) != pp.median_blur3(lay)).mean()),
-               "known_pixels_identical": bool((heap[~hole] == lay[~hole]).all()),
-               "seconds": {"product_form": round(t1 - t0, 2), "heap": round(t2 - t1, 2)}}
-        del fin
+        out = {"config": c, "H": H, "W_cropped": W - D, "hole_pixels": int(hole.sum()),
+               "opencv_form_vs_round5_form": stats(cv, r5, hole),
+               "opencv_form_vs_without_outward_march": stats(cv, cv_noring, hole),
+               "known_pixels_identical": bool((cv[~hole] == r5[~hole]).all()),
+               "seconds": {"opencv_form_c": round(t1 - t0, 2), "others": round(t2 - t1, 2)}}
         print(json.dumps(out), flush=True)
 
 
