@@ -43,7 +43,9 @@ def main(src, tag, config, path):
     os.makedirs(prof, exist_ok=True)
     stats = glob.glob(os.path.join(src, "trace", "*kernel_stats.csv"))[0]
     shutil.copy(stats, os.path.join(prof, f"{tag}_kernel_stats.csv"))
-    avg_ns = {r["Name"]: float(r["AverageNs"]) for r in csv.DictReader(open(stats))}
+    rows = list(csv.DictReader(open(stats)))
+    avg_ns = {r["Name"]: float(r["AverageNs"]) for r in rows}
+    calls = {r["Name"]: int(r["Calls"]) for r in rows}
     acc = defaultdict(lambda: defaultdict(list))
     for f in sorted(glob.glob(os.path.join(src, "pmc*", "*counter_collection.csv"))):
         for r in csv.DictReader(open(f)):
@@ -54,7 +56,9 @@ def main(src, tag, config, path):
     traffic = json.load(open(tp)) if os.path.exists(tp) else {}
     vp = os.path.join(prof, "valu_counts.json")
     valu = json.load(open(vp)) if os.path.exists(vp) else {}
-    for k, cs in acc.items():
+    # kernels that share a short name (e.g. a secondary leg's matcher next to the config's own) are
+    # listed each, and the entry of traffic.json / valu_counts.json is the most dispatched one's
+    for k, cs in sorted(acc.items(), key=lambda kv: calls.get(kv[0], 0)):
         if "rocclr" in k or "dsx::" not in k:  # torch fill kernels of the bench harness
             continue
         lines.append(f"{k}  [{short(k)}]  avg_ns={avg_ns.get(k)}")

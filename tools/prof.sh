@@ -7,7 +7,7 @@ REPO=$PWD
 OUT=$PWD/gpurun_out/prof_$TAG
 mkdir -p $OUT
 cd /tmp && export TMPDIR=/tmp
-BENCH="python3 $REPO/bench.py --steps ${PSTEPS:-1000} --warmup ${PWARM:-500} --streams 1 --no-cpu-baseline --no-volume-roofline --no-batched --no-e2e --no-parity --no-ref-defaults --no-post --no-dropin $@"
+BENCH="python3 $REPO/bench.py --steps ${PSTEPS:-1000} --warmup ${PWARM:-500} --streams 1 --no-cpu-baseline --no-volume-roofline --no-batched --no-e2e --no-parity --no-ref-defaults --no-post --no-dropin --video-frames 0 $@"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o run -- $BENCH > $OUT/trace.log 2>&1 || { echo "trace failed"; tail -20 $OUT/trace.log; exit 1; }
 i=0
 for pmc in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_SMEM SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_BRANCH" \
