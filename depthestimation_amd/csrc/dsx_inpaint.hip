@@ -16,7 +16,7 @@
 //   POP      band pixels below the bound pop: each marks its INSIDE 4-neighbours (atomic CAS on the
 //            fill-bucket word; the first one appends the child), joins the bucket's pop list with its
 //            push key (its parent's pop rank * 4 + its direction; seeds: raster index) and rank base;
-//   SWEEP 0  (fused with the POP) each child picks its parent - the pop neighbour with the least
+//   SWEEP 0  (the step after the POP) each child picks its parent - the pop neighbour with the least
 //            (T, push key) - stores its fill key (parent T, parent push key, direction: the order in
 //            which the queue fills the bucket) and computes T / value from the pre-bucket pixels;
 //   SWEEP 1  each child recomputes from the pre-bucket pixels and the bucket's children with a
@@ -45,6 +45,7 @@
 #include <mutex>
 #include <type_traits>
 #include <unordered_map>
+#include <vector>
 
 namespace dsx {
 
@@ -104,6 +105,9 @@ struct Args {
     int *host;                // mapped host words of this workspace (nullable)
     int H, W, radius;
     unsigned spin_limit;
+    unsigned long long *stamps;  // DSX_INPAINT_STAMPS diagnostics: per step {start, mode, list length, bucket,
+                                 // block 0's end, the last block's end, ~the first block's end, -}
+    unsigned nstamps;
 };
 
 constexpr int kHostSteps = 0, kHostTmo = 16;
@@ -286,9 +290,9 @@ __device__ __forceinline__ Mode decide(const State &S, unsigned long long mcv, b
         m.nIn = S.nC;
         return m;
     }
-    if (S.phase == kPhPop && S.nC > 0) {  // the POP ran sweep 0 of its children
+    if (S.phase == kPhPop && S.nC > 0) {  // the POP listed the children: their sweep 0
         m.what = kPhSweep;
-        m.sweep = 1;
+        m.sweep = 0;
         m.full = true;
         m.nIn = S.nC;
         return m;
@@ -725,21 +729,18 @@ __device__ __forceinline__ void fill_child_wide(const Args &a, const Mode &m, in
 // POP: entries of F[lsel] (nIn) then C[lsel] (nPrev); T < bound pops (marks children, joins the pop
 // list with its push key and rank base), the rest survives into F[lsel^1].  A block round takes one
 // entry per thread, appends survivors and children with ONE 64-bit counter add and the pops with one
-// add, and runs sweep 0 of its children right there (the pops, and so every child's parent, are fixed
-// for the whole step, and sweep 0 reads no child of the bucket).
-template <int RW>
-__device__ __forceinline__ void do_pop(const Args &a, const Mode &m, State &N, int blk, int nblk, WinLds<RW> *lds) {
+// add.  The children's sweep 0 is the next step: run here (as through round 6's first builds), its
+// window code doubled the step kernel's registers to 170 VGPRs (2 waves per SIMD); without it the
+// step kernel takes 111 (4 waves), and C2 / C4 fill in 2.13 / 65 ms against 2.27 / 73
+// (profiles/r06_inpaint_lib_ab.txt).
+__device__ __forceinline__ void do_pop(const Args &a, const Mode &m, State &N, int blk, int nblk) {
     const int *Fi = a.F[m.lsel], *Ci = a.C[m.lsel];
     int *Fo = a.F[m.lsel ^ 1], *Co = a.C[m.lsel ^ 1];
     const int tot = m.nIn + m.nPrev;
     const int W = a.W, H = a.H;
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    __shared__ int kidc[1024], kidi[1024];
     __shared__ int wsumF[4], wsumK[4], wsumP[4], kbaseF, kbaseK, kbaseP;
-    Mode m0 = m;
-    m0.what = kPhSweep;
-    m0.sweep = 0;
-    unsigned long long mn = ~0ull, mnc = ~0ull;
+    unsigned long long mn = ~0ull;
     for (int base = blk * 256; base < tot; base += nblk * 256) {  // block-uniform trip count
         const int i = base + (int)threadIdx.x;
         int keep = 0, popd = 0, p = 0;
@@ -809,41 +810,11 @@ __device__ __forceinline__ void do_pop(const Args &a, const Mode &m, State &N, i
             if ((km >> d) & 1u) {
                 const int li = woffK + ek + __popc(km & ((1u << d) - 1u));
                 Co[gb + li] = nb[d];
-                kidc[li] = nb[d];
-                kidi[li] = gb + li;
             }
         }
-        __syncthreads();
-        if (m.march == 0) {
-            for (int k = threadIdx.x; k < btot; k += 256) {
-                bool tg = false;
-                float tc;
-                ring_child(a, m0, kidi[k], kidc[k], tc, tg);
-                const unsigned long long tb = dbits((double)tc);
-                mnc = tb < mnc ? tb : mnc;
-            }
-        } else if constexpr (RW > 0) {
-            const int g = (int)threadIdx.x / kG;
-            for (int k = g; k < btot; k += kPer) {  // group-uniform
-                bool tg = false;
-                float tc;
-                fill_child<RW>(a, m0, kidi[k], kidc[k], tc, tg, lds[g]);
-                const unsigned long long tb = dbits((double)tc);
-                mnc = tb < mnc ? tb : mnc;
-            }
-        } else {
-            for (int k = threadIdx.x; k < btot; k += 256) {
-                bool ch;
-                float tc;
-                fill_child_wide(a, m0, kidc[k], ch, tc);
-                const unsigned long long tb = dbits((double)tc);
-                mnc = tb < mnc ? tb : mnc;
-            }
-        }
-        __syncthreads();  // LDS lists and sums reused by the next round
+        __syncthreads();  // the sums are reused by the next round
     }
     block_min_to(mn, &N.minF);
-    block_min_to(mnc, &a.ctl->minC[m.nb % 3][blk % kMinSlots]);
 }
 
 __device__ __forceinline__ unsigned long long pop_key(const Args &a, int p) {
@@ -1075,6 +1046,13 @@ __device__ __forceinline__ int step(const Args &a, unsigned s, int blk, int nblk
     const unsigned tg = lane < kMinSlots ? ctl->tagged[s % 3][lane] : 0u;
     State &N = ctl->st[(s + 1) % 3];
     const Mode m = decide<RW>(S, mcv, __ballot(tg != 0u) != 0ull);
+    if (a.stamps && blk == 0 && threadIdx.x == 0 && s < a.nstamps) {
+        unsigned long long *e = a.stamps + 8 * (size_t)s;
+        e[0] = __builtin_amdgcn_s_memrealtime();
+        e[1] = (unsigned)m.what | (unsigned)m.sweep << 8 | (unsigned)m.march << 24;
+        e[2] = (unsigned long long)(unsigned)m.nIn | (unsigned long long)(unsigned)m.nPrev << 32;
+        e[3] = (unsigned long long)(unsigned)m.b | (unsigned long long)(unsigned)m.nP << 32;
+    }
     if (blk == 0 && threadIdx.x == 0) {
         State &Z = ctl->st[(s + 2) % 3];
         Z.nF = 0;
@@ -1130,10 +1108,17 @@ __device__ __forceinline__ int step(const Args &a, unsigned s, int blk, int nblk
                 __hip_atomic_store(a.host + kHostSteps, (int)s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         }
     }
-    if (m.what == kPhPop) do_pop<RW>(a, m, N, blk, nblk, lds);
+    if (m.what == kPhPop) do_pop(a, m, N, blk, nblk);
     else if (m.what == kPhSweep) do_sweep<RW>(a, m, ctl->tagged[(s + 1) % 3], blk, nblk, lds, sortbuf);
     else if (m.what == kPhSwitch) do_switch(a, N, blk, nblk);
     else if (m.what == kPhRank) do_rank(a, m, blk, nblk);
+    if (a.stamps && threadIdx.x == 0 && s < a.nstamps) {  // diagnostics: when each block finished the step
+        unsigned long long *e = a.stamps + 8 * (size_t)s;
+        const unsigned long long t = __builtin_amdgcn_s_memrealtime();
+        if (blk == 0) e[4] = t;
+        atomicMax(e + 5, t);
+        atomicMax(e + 6, ~t);
+    }
     return m.what;
 }
 
@@ -1310,6 +1295,13 @@ hipError_t run_march(Args a, int ncu, int *hw, const InpaintOpts &o, hipStream_t
         (void)hipEventCreate(&e0);
         (void)hipEventCreate(&e1);
     }
+    const char *stp = getenv("DSX_INPAINT_STAMPS");  // diagnostics: per-step device timestamps to a file
+    constexpr unsigned kStamps = 1u << 17;
+    if (stp && *stp && !a.stamps) {
+        if (hipMalloc(&a.stamps, (size_t)kStamps * 64) != hipSuccess) return hipErrorOutOfMemory;
+        a.nstamps = kStamps;
+        if ((e = hipMemsetAsync(a.stamps, 0, (size_t)kStamps * 64, st)) != hipSuccess) return e;
+    }
     const int sgrid = kStepBlocks;
     for (int s = 0; s < nsteps; ++s) {
         if (trace) (void)hipEventRecord(e0, st);
@@ -1346,7 +1338,30 @@ hipError_t run_march(Args a, int ncu, int *hw, const InpaintOpts &o, hipStream_t
     });
     if (!occ_ok[dev & 63]) return hipErrorCooperativeLaunchTooLarge;
     hipLaunchKernelGGL(tl_tail<RW>, dim3(ncu), dim3(256), 0, st, a, (unsigned)nsteps);
-    return dbg_sync("tl_tail", st);
+    e = dbg_sync("tl_tail", st);
+    if (a.stamps) {  // one line per step: index, start (us from the first stamp), mode, sweep, march, list, prev, bucket, pops
+        std::vector<unsigned long long> h((size_t)kStamps * 8);
+        if (e == hipSuccess && (e = hipStreamSynchronize(st)) == hipSuccess &&
+            (e = hipMemcpy(h.data(), a.stamps, h.size() * 8, hipMemcpyDeviceToHost)) == hipSuccess) {
+            if (FILE *f = fopen(stp, "a")) {
+                unsigned long long t0 = 0;
+                for (unsigned i = 0; i < kStamps; ++i) {
+                    const unsigned long long *r = &h[8 * (size_t)i];
+                    if (!r[0]) continue;
+                    if (!t0) t0 = r[0];
+                    // + block 0's, the first and the last block's end, us after the step's start
+                    auto rel = [&](unsigned long long t) { return t ? (double)((long long)(t - r[0])) / 100.0 : -1.0; };
+                    fprintf(f, "%u %.2f %u %u %u %u %u %u %u %.2f %.2f %.2f\n", i, (double)(r[0] - t0) / 100.0,
+                            (unsigned)(r[1] & 255), (unsigned)((r[1] >> 8) & 0xFFFF), (unsigned)(r[1] >> 24), (unsigned)r[2],
+                            (unsigned)(r[2] >> 32), (unsigned)r[3], (unsigned)(r[3] >> 32), rel(r[4]), rel(~r[6]), rel(r[5]));
+                }
+                fprintf(f, "end\n");
+                fclose(f);
+            }
+        }
+        (void)hipFree(a.stamps);
+    }
+    return e;
 }
 
 }  // namespace
