@@ -61,10 +61,10 @@ constexpr unsigned kMaxSteps = 1u << 24;
 constexpr int kMinSlots = 16;
 constexpr int kG = 16;               // lanes per child (window rows) of the grouped sweep
 constexpr int kPer = 256 / kG;       // children per block round of the grouped sweep
-constexpr int kRankChunk = 4096;     // pop keys sorted per block (registers) for the ranks
-constexpr int kRankILP = 16;         // chunks searched at once per thread
+constexpr int kRankChunk = 1024;     // pop keys sorted per block (registers) for the ranks
+constexpr int kRankBatch = 8;        // sorted chunks one rank task counts against (through LDS)
 
-enum Phase : int { kPhInit = 0, kPhPop = 1, kPhSweep = 2, kPhDone = 3, kPhSwitch = 4, kPhRank = 5 };
+enum Phase : int { kPhInit = 0, kPhPop = 1, kPhSweep = 2, kPhDone = 3, kPhSwitch = 4 };
 enum : uint8_t { kClsOther = 0, kClsHole = 1, kClsBand = 2, kClsRing = 3 };
 
 // One state slot (written by step s-1, read by step s).  Counters and minima are accumulated by the
@@ -227,7 +227,7 @@ __global__ __launch_bounds__(256) void tl_init_b(Args a) {
 // ---- one step ----------------------------------------------------------------------------------
 
 struct Mode {
-    int what;  // kPhPop, kPhSweep, kPhDone, kPhSwitch, kPhRank
+    int what;  // kPhPop, kPhSweep, kPhDone, kPhSwitch
     int k, b, nb, sweep, lsel, march, ranked;
     int nIn;    // POP: survivors; sweeps: list length
     int nPrev;  // POP: the last bucket's children
@@ -272,13 +272,6 @@ __device__ __forceinline__ Mode decide(const State &S, unsigned long long mcv, b
         m.what = kPhSweep;
         m.sweep = 0;
         m.full = true;
-        m.nIn = S.nC;
-        return m;
-    }
-    // after sweep 1 (which sorted the pop keys per chunk) the bucket's pops get their ranks
-    if (S.phase == kPhSweep && S.sweep == 1 && S.rank_on && S.nP > 0 && !S.ranked) {
-        m.what = kPhRank;
-        m.sweep = 1;
         m.nIn = S.nC;
         return m;
     }
@@ -765,8 +758,9 @@ __device__ __forceinline__ void do_pop(const Args &a, const Mode &m, State &N, i
                     if (nb[d] >= 0 && fn[d] == kInside) old[d] = atomicCAS(&a.fb[nb[d]], kInside, m.b);
 #pragma unroll
                 for (int d = 0; d < 4; ++d) km |= (uint32_t)(nb[d] >= 0 && fn[d] == kInside && old[d] == kInside) << d;
-                // its push key (ranked after sweep 1 by (T, push key))
+                // its push key (ranked in sweep 1 by (T, push key); rank = the base + counts added there)
                 a.pk[p] = pushkey_of(a, p, a.fb[p]);
+                a.rank[p] = (unsigned)m.base;
             } else {
                 keep = 1;
                 const unsigned long long tb = dbits((double)t);
@@ -821,10 +815,11 @@ __device__ __forceinline__ unsigned long long pop_key(const Args &a, int p) {
     return (unsigned long long)__float_as_uint(a.T[p]) << 32 | a.pk[p];
 }
 
-// Sweep 1's side task: this bucket's pop keys (T, push key; unique) sorted per chunk of kRankChunk,
+// Sweep 0's side task: this bucket's pop keys (T, push key; unique) sorted per chunk of kRankChunk,
 // one chunk per block, into sk.  Bitonic network with the chunk in registers (thread t holds elements
-// 16 t .. 16 t + 15): partners 1-8 apart inside a thread, 16-512 apart across the wave by shuffles,
-// 1024 and more apart through LDS (three stages of the 4096 network).
+// E t .. E t + E - 1): partners closer than E inside a thread, up to 64 E apart across the wave by
+// shuffles, farther through LDS.  Chunks of 1024 (E = 4): a 4096-key chunk took one block about 65 us
+// (DSX_INPAINT_STAMPS, C2), a quarter of the chunks' keys now sort in a fraction of that on 4x the blocks.
 __device__ __forceinline__ unsigned long long shfl_xor_u64(unsigned long long v, int m) {
     const unsigned lo = (unsigned)__shfl_xor((int)(unsigned)v, m), hi = (unsigned)__shfl_xor((int)(unsigned)(v >> 32), m);
     return (unsigned long long)hi << 32 | lo;
@@ -861,11 +856,17 @@ __device__ __forceinline__ void do_sort_chunks(const Args &a, const Mode &m, int
                             v[l] = sw ? x : y;
                         }
                     };
-                    static_assert(E == 16, "in-thread stages below are written for 16 elements per thread");
-                    if (j == 8) cx(std::integral_constant<int, 8>{});
-                    else if (j == 4) cx(std::integral_constant<int, 4>{});
-                    else if (j == 2) cx(std::integral_constant<int, 2>{});
-                    else cx(std::integral_constant<int, 1>{});
+                    static_assert(E >= 2 && E <= 16 && (E & (E - 1)) == 0, "E: a power of two, 2 .. 16");
+                    if constexpr (E > 8) {
+                        if (j == 8) cx(std::integral_constant<int, 8>{});
+                    }
+                    if constexpr (E > 4) {
+                        if (j == 4) cx(std::integral_constant<int, 4>{});
+                    }
+                    if constexpr (E > 2) {
+                        if (j == 2) cx(std::integral_constant<int, 2>{});
+                    }
+                    if (j == 1) cx(std::integral_constant<int, 1>{});
                 } else if (j < E * 64) {
                     const int tm = j / E;
                     const bool lower = (t & tm) == 0;
@@ -899,40 +900,56 @@ __device__ __forceinline__ void do_sort_chunks(const Args &a, const Mode &m, int
     }
 }
 
-// RANK: dense ranks of this bucket's pops by (T, push key) - base + the number of pop keys below
-// its own, summed over the sorted chunks by binary searches (kRankILP chunks in flight per thread).
-// The children's push keys read them from the next bucket on.
-__device__ __forceinline__ void do_rank(const Args &a, const Mode &m, int blk, int nblk) {
+// Sweep 1's side task: dense ranks of this bucket's pops by (T, push key) - base + the number of pop
+// keys below each one's own, counted per sorted chunk by binary searches in LDS.  A task is a group of
+// kRankChunk pops (in P order) against a batch of kRankBatch sorted chunks; with more than one batch,
+// each adds its counts to rank[] (the POP set it to the base).  The children's push keys read the
+// ranks from the next bucket on.  (Round 6's first form searched the chunks in global memory, 16
+// chunks in flight per thread: about 50 us per C2 bucket, DSX_INPAINT_STAMPS.)
+__device__ __forceinline__ void do_rank(const Args &a, const Mode &m, int blk, int nblk, unsigned long long *buf) {
+    constexpr int E = kRankChunk / 256;  // pops per thread
     const int np = m.nP;
     const int nch = (np + kRankChunk - 1) / kRankChunk;
-    for (int i = blk * 256 + (int)threadIdx.x; i < np; i += nblk * 256) {
-        const int p = a.P[i];
-        const unsigned long long key = pop_key(a, p);
-        unsigned cnt = 0;
-        for (int c0 = 0; c0 < nch; c0 += kRankILP) {
-            int lo[kRankILP], len[kRankILP];
+    const int nbt = (nch + kRankBatch - 1) / kRankBatch;
+    const int t = threadIdx.x;
+    for (int task = blk; task < nch * nbt; task += nblk) {  // block-uniform
+        const int g = task / nbt, bt = task - g * nbt;
+        int pp[E];
+        unsigned long long key[E];
+        unsigned cnt[E];
 #pragma unroll
-            for (int u = 0; u < kRankILP; ++u) {
-                const int c = c0 + u;
-                lo[u] = 0;
-                len[u] = c < nch ? (np - c * kRankChunk < kRankChunk ? np - c * kRankChunk : kRankChunk) : 0;
-            }
-            // lower_bound in each chunk: first position whose key is not below `key`
-            for (int step = kRankChunk; step > 0; step >>= 1) {
-                unsigned long long v[kRankILP];
-#pragma unroll
-                for (int u = 0; u < kRankILP; ++u) {
-                    const int q = lo[u] + step - 1;
-                    v[u] = q < len[u] ? a.sk[(int64_t)(c0 + u) * kRankChunk + q] : ~0ull;
-                }
-#pragma unroll
-                for (int u = 0; u < kRankILP; ++u)
-                    if (lo[u] + step - 1 < len[u] && v[u] < key) lo[u] += step;
-            }
-#pragma unroll
-            for (int u = 0; u < kRankILP; ++u) cnt += (unsigned)lo[u];
+        for (int i = 0; i < E; ++i) {
+            const int q = g * kRankChunk + t * E + i;
+            pp[i] = q < np ? a.P[q] : -1;
+            cnt[i] = 0;
         }
-        a.rank[p] = (unsigned)m.base + cnt;
+#pragma unroll
+        for (int i = 0; i < E; ++i) key[i] = pp[i] >= 0 ? pop_key(a, pp[i]) : 0ull;
+        const int c1 = (bt + 1) * kRankBatch < nch ? (bt + 1) * kRankBatch : nch;
+        for (int c = bt * kRankBatch; c < c1; ++c) {  // block-uniform
+            const int len = np - c * kRankChunk < kRankChunk ? np - c * kRankChunk : kRankChunk;
+            __syncthreads();  // the last chunk's searches (or the windows that alias buf) are done
+#pragma unroll
+            for (int i = 0; i < E; ++i) buf[t * E + i] = t * E + i < len ? a.sk[(int64_t)c * kRankChunk + t * E + i] : ~0ull;
+            __syncthreads();
+            int lo[E];
+#pragma unroll
+            for (int i = 0; i < E; ++i) lo[i] = 0;
+            // lower_bound: the first position whose key is not below key (padding ~0 never is)
+            for (int step = kRankChunk / 2; step > 0; step >>= 1)
+#pragma unroll
+                for (int i = 0; i < E; ++i) lo[i] += buf[lo[i] + step - 1] < key[i] ? step : 0;
+#pragma unroll
+            for (int i = 0; i < E; ++i) lo[i] += buf[lo[i]] < key[i] ? 1 : 0;
+#pragma unroll
+            for (int i = 0; i < E; ++i) cnt[i] += (unsigned)lo[i];
+        }
+#pragma unroll
+        for (int i = 0; i < E; ++i) {
+            if (pp[i] < 0) continue;
+            if (nbt == 1) a.rank[pp[i]] = (unsigned)m.base + cnt[i];
+            else atomicAdd(a.rank + pp[i], cnt[i]);
+        }
     }
 }
 
@@ -984,10 +1001,14 @@ __device__ __forceinline__ void do_sweep(const Args &a, const Mode &m, unsigned 
             }
         }
     }
-    if (m.sweep == 1 && m.rank_on && m.nP > 0) {
+    // the bucket's pop keys are final after its POP: sweep 0 sorts them per chunk, sweep 1 ranks them
+    // (the next POP reads the ranks; no sweep does).  Round 6 ran the ranks as a step of their own
+    // after sweep 1: C2 2.14 -> 2.08 ms, C4 65.6 -> 64.5 ms without it (profiles/r06_inpaint_lib_ab.txt).
+    if (m.sweep == 0 && m.rank_on && m.nP > 0) {
         __syncthreads();  // the sort buffer aliases the lane groups' windows
         do_sort_chunks(a, m, blk, nblk, sortbuf);
     }
+    if (m.sweep == 1 && m.rank_on && m.nP > 0) do_rank(a, m, blk, nblk, sortbuf);
     if (__syncthreads_or(tagged) && threadIdx.x == 0)
         __hip_atomic_store(tagw + blk % kMinSlots, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     // T of a child only falls over the sweeps (more neighbours filled before it), so the minimum of
@@ -1070,16 +1091,7 @@ __device__ __forceinline__ int step(const Args &a, unsigned s, int blk, int nblk
         N.base = m.base;
         N.rank_on = m.rank_on;
         N.ranked = m.ranked;
-        if (m.what == kPhRank) {  // carried like a sweep; the next step decides as after sweep 1
-            N.phase = kPhSweep;
-            N.ranked = 1;
-            N.lsel = m.lsel;
-            N.nF = S.nF;
-            N.nC = S.nC;
-            N.nP = S.nP;
-            N.minF = S.minF;
-            for (int q = 0; q < kMinSlots; ++q) ctl->tagged[(s + 1) % 3][q] = ctl->tagged[s % 3][q];
-        } else if (m.what == kPhSweep) {  // carried: the POP's outputs
+        if (m.what == kPhSweep) {  // carried: the POP's outputs
             N.lsel = m.lsel;
             N.nF = S.nF;
             N.nC = S.nC;
@@ -1111,7 +1123,6 @@ __device__ __forceinline__ int step(const Args &a, unsigned s, int blk, int nblk
     if (m.what == kPhPop) do_pop(a, m, N, blk, nblk);
     else if (m.what == kPhSweep) do_sweep<RW>(a, m, ctl->tagged[(s + 1) % 3], blk, nblk, lds, sortbuf);
     else if (m.what == kPhSwitch) do_switch(a, N, blk, nblk);
-    else if (m.what == kPhRank) do_rank(a, m, blk, nblk);
     if (a.stamps && threadIdx.x == 0 && s < a.nstamps) {  // diagnostics: when each block finished the step
         unsigned long long *e = a.stamps + 8 * (size_t)s;
         const unsigned long long t = __builtin_amdgcn_s_memrealtime();
