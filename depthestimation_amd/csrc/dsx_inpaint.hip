@@ -63,6 +63,7 @@ constexpr int kG = 16;               // lanes per child (window rows) of the gro
 constexpr int kPer = 256 / kG;       // children per block round of the grouped sweep
 constexpr int kRankChunk = 1024;     // pop keys sorted per block (registers) for the ranks
 constexpr int kRankBatch = 8;        // sorted chunks one rank task counts against (through LDS)
+constexpr int kInitPT = 8;           // pixels per thread of tl_init_b
 
 enum Phase : int { kPhInit = 0, kPhPop = 1, kPhSweep = 2, kPhDone = 3, kPhSwitch = 4 };
 enum : uint8_t { kClsOther = 0, kClsHole = 1, kClsBand = 2, kClsRing = 3 };
@@ -151,9 +152,23 @@ __device__ __forceinline__ unsigned pushkey_of(const Args &a, int q, int fq) {
     return rg * 4u + (pd & 3u);
 }
 
+// Wave-wide exclusive prefix sum of v (and the wave total).
+__device__ __forceinline__ int wave_excl_scan(int v, int &total) {
+    const int lane = threadIdx.x & 63;
+    int incl = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int u = __shfl_up(incl, o);
+        incl += lane >= o ? u : 0;
+    }
+    total = __shfl(incl, 63);
+    return incl - v;
+}
+
 // ---- setup -----------------------------------------------------------------------------------
 
 // out = in; pixel classes hole / band / other; rowd = a hole within `radius` along the row.
+template <int RW>
 __global__ __launch_bounds__(256) void tl_init_a(Args a) {
     const int64_t p = (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (p >= a.n) return;
@@ -168,9 +183,20 @@ __global__ __launch_bounds__(256) void tl_init_a(Args a) {
         nb = (y > 0 && row[x - a.pitch] <= 0.0f) | (y < H - 1 && row[x + a.pitch] <= 0.0f) | (x > 0 && row[x - 1] <= 0.0f) |
              (x < W - 1 && row[x + 1] <= 0.0f);
     a.cls[p] = hole ? kClsHole : (nb ? kClsBand : kClsOther);
+    // a hole within `radius` along the row: with the radius a constant (RW = radius + 1) every load
+    // issues at once (the early-exit loop made them one round trip each: tl_init_a 15.7 us at C2, the
+    // ring test of tl_init_b 70 us)
     bool near = false;
-    const int x0 = x - r > 0 ? x - r : 0, x1 = x + r < W - 1 ? x + r : W - 1;
-    for (int xx = x0; xx <= x1 && !near; ++xx) near = row[xx] <= 0.0f;
+    if constexpr (RW > 0) {
+#pragma unroll
+        for (int d = 1 - RW; d <= RW - 1; ++d) {
+            const int xx = x + d;
+            near |= xx >= 0 && xx < W && row[xx < 0 ? 0 : (xx > W - 1 ? W - 1 : xx)] <= 0.0f;
+        }
+    } else {
+        const int x0 = x - r > 0 ? x - r : 0, x1 = x + r < W - 1 ? x + r : W - 1;
+        for (int xx = x0; xx <= x1 && !near; ++xx) near = row[xx] <= 0.0f;
+    }
     a.rowd[p] = near;
 }
 
@@ -178,8 +204,10 @@ __global__ __launch_bounds__(256) void tl_init_a(Args a) {
 // and T, and its first bucket: every band pixel is a seed of T = 0 that pops at bound 0.7, so the
 // bucket's children are the ring pixels with a band 4-neighbour (fill bucket 1, list C[0]).  The
 // control block was zeroed before.  Block-aggregated list appends.
+template <int RW>
 __global__ __launch_bounds__(256) void tl_init_b(Args a) {
-    const int64_t p = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    // kInitPT pixels per thread (256 apart: coalesced), one list append per block: the appends are
+    // adds on one counter, and one per 256 pixels serialised to about 70 us at C2
     const int H = a.H, W = a.W, r = a.radius;
     State &s0 = a.ctl->st[0];
     if (blockIdx.x == 0 && threadIdx.x < 3) a.ctl->st[threadIdx.x].minF = ~0ull;
@@ -191,27 +219,42 @@ __global__ __launch_bounds__(256) void tl_init_b(Args a) {
         s0.base = (int)a.n;
     }
     if (blockIdx.x == 0 && threadIdx.x < 3 * kMinSlots) a.ctl->minC[threadIdx.x / kMinSlots][threadIdx.x % kMinSlots] = ~0ull;
-    bool kid = false;
-    if (p < a.n) {
+    unsigned kid = 0;
+    const int64_t base = (int64_t)blockIdx.x * 256 * kInitPT + threadIdx.x;
+#pragma unroll
+    for (int k = 0; k < kInitPT; ++k) {
+        const int64_t p = base + 256 * k;
+        if (p >= a.n) break;
         const int y = (int)(p / W), x = (int)(p - (int64_t)y * W);
         const uint8_t c = a.cls[p];
         bool ring = false;
         if (c == kClsOther) {
-            const int y0 = y - r > 0 ? y - r : 0, y1 = y + r < H - 1 ? y + r : H - 1;
-            for (int yy = y0; yy <= y1 && !ring; ++yy) ring = a.rowd[(int64_t)yy * W + x] != 0;
+            if constexpr (RW > 0) {  // every load at once (see tl_init_a)
+#pragma unroll
+                for (int d = 1 - RW; d <= RW - 1; ++d) {
+                    const int yy = y + d;
+                    ring |= yy >= 0 && yy < H && a.rowd[(int64_t)(yy < 0 ? 0 : (yy > H - 1 ? H - 1 : yy)) * W + x] != 0;
+                }
+            } else {
+                const int y0 = y - r > 0 ? y - r : 0, y1 = y + r < H - 1 ? y + r : H - 1;
+                for (int yy = y0; yy <= y1 && !ring; ++yy) ring = a.rowd[(int64_t)yy * W + x] != 0;
+            }
         }
-        if (ring) {
+        bool kd = false;
+        if (ring) {  // (a neighbour that turns Other -> Ring here is never Band: the test is race-free)
             a.cls[p] = kClsRing;
-            kid = (y > 0 && a.cls[p - W] == kClsBand) | (y < H - 1 && a.cls[p + W] == kClsBand) |
-                  (x > 0 && a.cls[p - 1] == kClsBand) | (x < W - 1 && a.cls[p + 1] == kClsBand);
+            kd = (y > 0 && a.cls[p - W] == kClsBand) | (y < H - 1 && a.cls[p + W] == kClsBand) |
+                 (x > 0 && a.cls[p - 1] == kClsBand) | (x < W - 1 && a.cls[p + 1] == kClsBand);
         }
-        a.fb[p] = ring ? (kid ? 1 : kInside) : -1;
+        kid |= (unsigned)kd << k;
+        a.fb[p] = ring ? (kd ? 1 : kInside) : -1;
         a.T[p] = c == kClsBand ? 0.0f : kFar;
     }
     __shared__ int wsum[4], bbase;
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    const unsigned long long m = __ballot(kid);
-    if (lane == 0) wsum[wv] = __popcll(m);
+    int wtot;
+    const int off = wave_excl_scan(__popc(kid), wtot);
+    if (lane == 0) wsum[wv] = wtot;
     __syncthreads();
     int woff = 0, btot = 0;
 #pragma unroll
@@ -221,7 +264,10 @@ __global__ __launch_bounds__(256) void tl_init_b(Args a) {
     }
     if (threadIdx.x == 0) bbase = btot ? atomicAdd(&s0.nC, btot) : 0;
     __syncthreads();
-    if (kid) a.C[0][bbase + woff + __popcll(m & ((1ull << lane) - 1))] = (int)p;
+    int o = bbase + woff + off;
+#pragma unroll
+    for (int k = 0; k < kInitPT; ++k)
+        if ((kid >> k) & 1u) a.C[0][o++] = (int)(base + 256 * k);
 }
 
 // ---- one step ----------------------------------------------------------------------------------
@@ -315,19 +361,6 @@ __device__ __forceinline__ Mode decide(const State &S, unsigned long long mcv, b
     m.rank_on = 1;
     m.ranked = 0;
     return m;
-}
-
-// Wave-wide exclusive prefix sum of v (and the wave total).
-__device__ __forceinline__ int wave_excl_scan(int v, int &total) {
-    const int lane = threadIdx.x & 63;
-    int incl = v;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const int u = __shfl_up(incl, o);
-        incl += lane >= o ? u : 0;
-    }
-    total = __shfl(incl, 63);
-    return incl - v;
 }
 
 // Block-wide minimum of a per-thread 64-bit key, then one atomicMin on *dst by thread 0.
@@ -1020,24 +1053,47 @@ __device__ __forceinline__ void do_sweep(const Args &a, const Mode &m, unsigned 
 // it reached), mark the holes INSIDE, and list the inward march's first bucket - the holes with a
 // known 4-neighbour (every band pixel is a seed that pops at bound 0.7) - in C[0].
 __device__ __forceinline__ void do_switch(const Args &a, State &N, int blk, int nblk) {
+    // kPT pixels per thread and block round (256 apart, so each load instruction stays coalesced), all
+    // loads of a round issued together, one block scan and one counter add per round (one pixel per
+    // thread took 54 us at C2: 7 rounds of dependent loads and three block barriers each)
+    constexpr int kPT = 4;
     const int H = a.H, W = a.W;
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     __shared__ int wsum[4], bbase;
-    for (int64_t base = (int64_t)blk * 256; base < a.n; base += (int64_t)nblk * 256) {  // block-uniform
-        const int64_t p = base + threadIdx.x;
-        bool kid = false;
-        if (p < a.n) {
-            const int y = (int)(p / W), x = (int)(p - (int64_t)y * W);
-            const uint8_t c = a.cls[p];
-            if (c == kClsBand || (c == kClsRing && a.fb[p] != kInside)) a.T[p] = -a.T[p];
-            const bool hole = c == kClsHole;
-            if (hole)
-                kid = (y > 0 && a.cls[p - W] != kClsHole) | (y < H - 1 && a.cls[p + W] != kClsHole) |
-                      (x > 0 && a.cls[p - 1] != kClsHole) | (x < W - 1 && a.cls[p + 1] != kClsHole);
-            a.fb[p] = hole ? (kid ? 1 : kInside) : -1;
+    for (int64_t base = (int64_t)blk * 256 * kPT; base < a.n; base += (int64_t)nblk * 256 * kPT) {  // block-uniform
+        uint8_t c[kPT];
+        int fbv[kPT];
+#pragma unroll
+        for (int k = 0; k < kPT; ++k) {
+            const int64_t p = base + threadIdx.x + 256 * k;
+            c[k] = p < a.n ? a.cls[p] : (uint8_t)kClsOther;
+            fbv[k] = p < a.n ? a.fb[p] : -1;
         }
-        const unsigned long long m = __ballot(kid);
-        if (lane == 0) wsum[wv] = __popcll(m);
+        unsigned kid = 0;
+        bool nbh[kPT][4];
+#pragma unroll
+        for (int k = 0; k < kPT; ++k) {
+            const int64_t p = base + threadIdx.x + 256 * k;
+            const int y = (int)(p / W), x = (int)(p - (int64_t)y * W);
+            const bool hole = p < a.n && c[k] == kClsHole;
+            nbh[k][0] = hole && y > 0 && a.cls[p - W] != kClsHole;
+            nbh[k][1] = hole && y < H - 1 && a.cls[p + W] != kClsHole;
+            nbh[k][2] = hole && x > 0 && a.cls[p - 1] != kClsHole;
+            nbh[k][3] = hole && x < W - 1 && a.cls[p + 1] != kClsHole;
+        }
+#pragma unroll
+        for (int k = 0; k < kPT; ++k) {
+            const int64_t p = base + threadIdx.x + 256 * k;
+            if (p >= a.n) continue;
+            if (c[k] == kClsBand || (c[k] == kClsRing && fbv[k] != kInside)) a.T[p] = -a.T[p];
+            const bool hole = c[k] == kClsHole;
+            const bool kd = nbh[k][0] | nbh[k][1] | nbh[k][2] | nbh[k][3];
+            kid |= (unsigned)kd << k;
+            a.fb[p] = hole ? (kd ? 1 : kInside) : -1;
+        }
+        int wtot;
+        const int off = wave_excl_scan(__popc(kid), wtot);
+        if (lane == 0) wsum[wv] = wtot;
         __syncthreads();
         int woff = 0, btot = 0;
 #pragma unroll
@@ -1047,7 +1103,10 @@ __device__ __forceinline__ void do_switch(const Args &a, State &N, int blk, int 
         }
         if (threadIdx.x == 0) bbase = btot ? atomicAdd(&N.nC, btot) : 0;
         __syncthreads();
-        if (kid) a.C[0][bbase + woff + __popcll(m & ((1ull << lane) - 1))] = (int)p;
+        int o = bbase + woff + off;
+#pragma unroll
+        for (int k = 0; k < kPT; ++k)
+            if ((kid >> k) & 1u) a.C[0][o++] = (int)(base + threadIdx.x + 256 * k);
         __syncthreads();
     }
 }
@@ -1288,9 +1347,9 @@ hipError_t run_march(Args a, int ncu, int *hw, const InpaintOpts &o, hipStream_t
     hipError_t e;
     if ((e = hipMemsetAsync(a.ctl, 0, sizeof(Ctl), st)) != hipSuccess) return e;
     const int ib = (int)((a.n + 255) / 256);
-    hipLaunchKernelGGL(tl_init_a, dim3(ib), dim3(256), 0, st, a);
+    hipLaunchKernelGGL(tl_init_a<RW>, dim3(ib), dim3(256), 0, st, a);
     if ((e = dbg_sync("tl_init_a", st)) != hipSuccess) return e;
-    hipLaunchKernelGGL(tl_init_b, dim3(ib), dim3(256), 0, st, a);
+    hipLaunchKernelGGL(tl_init_b<RW>, dim3((unsigned)((a.n + 256 * kInitPT - 1) / (256 * kInitPT))), dim3(256), 0, st, a);
     if ((e = dbg_sync("tl_init_b", st)) != hipSuccess) return e;
     // step launches: as many as the previous call on this workspace needed (+3); the persistent
     // kernel takes whatever is left
