@@ -59,8 +59,7 @@ constexpr float kFar = 1.0e6f;       // T of the padding and of pixels no march 
 constexpr int kStepBlocks = 1024;    // at most this grid for the step launches (see run_march)
 constexpr unsigned kMaxSteps = 1u << 24;
 constexpr int kMinSlots = 16;
-constexpr int kG = 16;               // lanes per child (window rows) of the grouped sweep
-constexpr int kPer = 256 / kG;       // children per block round of the grouped sweep
+constexpr int kG = 16;               // lessm words per child (one per window row, <= 15 rows)
 constexpr int kRankChunk = 1024;     // pop keys sorted per block (registers) for the ranks
 constexpr int kRankBatch = 8;        // sorted chunks one rank task counts against (through LDS)
 constexpr int kInitPT = 8;           // pixels per thread of tl_init_b
@@ -483,7 +482,7 @@ __device__ __forceinline__ void ring_child(const Args &a, const Mode &m, int i, 
 // double and rounded to float offline (the same bits as the expression)
 __constant__ float kDst[37] = {0.0f, 0x1.0000000000000p+0f, 0x1.6a09e60000000p-2f, 0x1.8a23460000000p-3f, 0x1.0000000000000p-3f, 0x1.6e5b7e0000000p-4f, 0x1.16b2900000000p-4f, 0x1.ba53900000000p-5f, 0x1.6a09e60000000p-5f, 0x1.2f684c0000000p-5f, 0x1.030dc40000000p-5f, 0x1.c116620000000p-6f, 0x1.8a23460000000p-6f, 0x1.5d8be40000000p-6f, 0x1.38c5a20000000p-6f, 0x1.1a05a40000000p-6f, 0x1.0000000000000p-6f, 0x1.d37e9a0000000p-7f, 0x1.ad15360000000p-7f, 0x1.8ba85a0000000p-7f, 0x1.6e5b7e0000000p-7f, 0x1.5480c80000000p-7f, 0x1.3d8d820000000p-7f, 0x1.2911d00000000p-7f, 0x1.16b2900000000p-7f, 0x1.0624de0000000p-7f, 0x1.ee55560000000p-8f, 0x1.d320520000000p-8f, 0x1.ba53900000000p-8f, 0x1.a3a5560000000p-8f, 0x1.8ed6e20000000p-8f, 0x1.7bb27c0000000p-8f, 0x1.6a09e60000000p-8f, 0x1.59b52a0000000p-8f, 0x1.4a918e0000000p-8f, 0x1.3c80c60000000p-8f, 0x1.2f684c0000000p-8f};
 
-// ---- the inward march: Telea's value, kG lanes per child (lane j = window row j - RW) ----
+// ---- the inward march: Telea's value, Win::GL lanes per child (lane j = window row j - RW) ----
 
 template <int RW>
 struct Win {
@@ -496,6 +495,11 @@ struct Win {
         return n;
     }
     static constexpr int ND = nd();
+    // lanes per child: one per window row, 8 up to radius 3 (its last row, read only at the centre
+    // columns, is lane 0's too), 16 above
+    static constexpr int GL = NC <= 9 ? 8 : 16;
+    static constexpr bool XR = NC > GL;
+    static constexpr int PER = 256 / GL;  // children per block round
     struct Lds {
         float v[NC * NC];  // value at this child's fill (current for available cells, the input else)
         float t[NC * NC];  // T (unavailable cells and the padding: 1e6)
@@ -509,8 +513,8 @@ using WinLds = typename Win<RW == 0 ? 2 : RW>::Lds;
 template <int RW>
 __device__ __forceinline__ void fill_child(const Args &a, const Mode &m, int i, int c, float &tc, bool &tagged, WinLds<RW> &L) {
     using WN = Win<RW>;
-    constexpr int NC = WN::NC, R = WN::R, ND = WN::ND;
-    const int j = (int)(threadIdx.x & (kG - 1));
+    constexpr int NC = WN::NC, R = WN::R, ND = WN::ND, GL = WN::GL;
+    const int j = (int)(threadIdx.x & (GL - 1));
     const int H = a.H, W = a.W, b = m.b, sweep = m.sweep;
     const int y = c / W, x = c - y * W;
     const int dy = j - RW, qy = y + dy;
@@ -564,11 +568,60 @@ __device__ __forceinline__ void fill_child(const Args &a, const Mode &m, int i, 
             if (((intra >> cc) & 1u) && kq[cc] < me) less |= 1u << cc;
         if (rowv) a.lessm[(int64_t)i * kG + j] = (uint16_t)less;
     }
+    // the last window row when it has no lane of its own (radius 3): only its centre columns count -
+    // the cell below the disc's bottom cell is read (and its right neighbour at the image's left edge),
+    // and the child one column left reads this one at the left edge.  Every lane of the group loads
+    // the same three cells; lane 0 stages them now (the group's previous child is done with the LDS).
+    uint32_t intra2 = 0, less2 = 0;
+    int64_t rowq2 = 0;
+    if constexpr (WN::XR) {
+        constexpr int jr = NC - 1;
+        const bool rin2 = y + RW < H;
+        const int qyc2 = rin2 ? y + RW : y;
+        rowq2 = (int64_t)qyc2 * W;
+        const float *inrow2 = a.in + (int64_t)qyc2 * a.pitch;
+        less2 = sweep >= 2 ? a.lessm[(int64_t)i * kG + jr] : 0u;
+        int f3[3];
+        float t3[3], v3[3], o3[3];
+        uint32_t inw2 = 0;
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            const int qx = x + k - 1;
+            const bool ok = rin2 && qx >= 0 && qx < W;
+            const int qxc = qx < 0 ? 0 : (qx >= W ? W - 1 : qx);
+            f3[k] = a.fb[rowq2 + qxc];
+            t3[k] = a.T[rowq2 + qxc];
+            v3[k] = a.out[rowq2 + qxc];
+            o3[k] = inrow2[qxc];
+            inw2 |= (uint32_t)ok << (RW - 1 + k);
+        }
+#pragma unroll
+        for (int k = 0; k < 3; ++k) intra2 |= (uint32_t)(((inw2 >> (RW - 1 + k)) & 1u) && f3[k] == b) << (RW - 1 + k);
+        if (sweep == 1) {
+#pragma unroll
+            for (int k = 0; k < 3; ++k)
+                if (((intra2 >> (RW - 1 + k)) & 1u) && a.key[rowq2 + x + k - 1] < me) less2 |= 1u << (RW - 1 + k);
+            if (j == 0) a.lessm[(int64_t)i * kG + jr] = (uint16_t)less2;
+        }
+        if (j == 0) {
+            uint32_t avail2 = 0;  // the other columns are never read
+#pragma unroll
+            for (int k = 0; k < 3; ++k) {
+                const int cc = RW - 1 + k;
+                const bool in = (inw2 >> cc) & 1u;
+                const bool av = !in || f3[k] < b || (f3[k] == b && ((less2 >> cc) & 1u));
+                avail2 |= (uint32_t)av << cc;
+                L.v[jr * NC + cc] = av ? v3[k] : o3[k];
+                L.t[jr * NC + cc] = in && av ? t3[k] : kFar;
+            }
+            L.av[jr] = (uint16_t)avail2;
+        }
+    }
     tc = Told;
     if (sweep == 1) {  // a child with no earlier child in its window keeps its sweep-0 result
-        int any = less != 0;
+        int any = less != 0 || less2 != 0;
 #pragma unroll
-        for (int o = 1; o < kG; o <<= 1) any |= __shfl_xor(any, o, kG);
+        for (int o = 1; o < GL; o <<= 1) any |= __shfl_xor(any, o, GL);
         if (!any) return;
     }
     // stage the window: availability (the padding is known), the value at this fill, T
@@ -672,9 +725,15 @@ __device__ __forceinline__ void fill_child(const Args &a, const Mode &m, int i, 
 #pragma unroll
     for (int cc = 0; cc < NC; ++cc)
         if ((dep >> cc) & 1u) qn[rowq + x + cc - RW] = tag;
-    int dany = dep != 0;
+    const uint32_t dep2 = intra2 & ~less2;
+    if (WN::XR && j == 0) {
 #pragma unroll
-    for (int o = 1; o < kG; o <<= 1) dany |= __shfl_xor(dany, o, kG);
+        for (int cc = RW - 1; cc <= RW + 1; ++cc)
+            if ((dep2 >> cc) & 1u) qn[rowq2 + x + cc - RW] = tag;
+    }
+    int dany = dep != 0 || dep2 != 0;
+#pragma unroll
+    for (int o = 1; o < GL; o <<= 1) dany |= __shfl_xor(dany, o, GL);
     tagged = tagged || dany;
 }
 
@@ -1021,7 +1080,8 @@ __device__ __forceinline__ void do_sweep(const Args &a, const Mode &m, unsigned 
             }
         }
     } else if constexpr (RW > 0) {
-        const int g = (int)threadIdx.x / kG;
+        constexpr int kPer = Win<RW>::PER;
+        const int g = (int)threadIdx.x / Win<RW>::GL;
         // one child per group and block round, so a block's tagged children take one pass
         for (int base = blk * kPer; base < m.nIn; base += nblk * kPer) {  // block-uniform
             const int i = base + g;
@@ -1115,7 +1175,7 @@ __device__ __forceinline__ void do_switch(const Args &a, State &N, int blk, int 
 template <int RW>
 __device__ __forceinline__ int step(const Args &a, unsigned s, int blk, int nblk) {
     // one child window per lane group (inward sweeps), or the pop keys of one chunk (the sort)
-    constexpr size_t kWin = sizeof(WinLds<RW>) * (RW > 0 ? kPer : 1), kSort = sizeof(unsigned long long) * kRankChunk;
+    constexpr size_t kWin = sizeof(WinLds<RW>) * (RW > 0 ? Win<RW>::PER : 1), kSort = sizeof(unsigned long long) * kRankChunk;
     __shared__ __attribute__((aligned(16))) unsigned char smem[kWin > kSort ? kWin : kSort];
     WinLds<RW> *lds = reinterpret_cast<WinLds<RW> *>(smem);
     unsigned long long *sortbuf = reinterpret_cast<unsigned long long *>(smem);
