@@ -500,6 +500,25 @@ struct Win {
     static constexpr int GL = NC <= 9 ? 8 : 16;
     static constexpr bool XR = NC > GL;
     static constexpr int PER = 256 / GL;  // children per block round
+    // the disc cells dealt round-robin to the lanes: term slot q = lane + GL k (row-major disc order,
+    // centre skipped), its offsets packed 4 bits per lane (dx + R, dy + R) so a lane unpacks its own
+    static constexpr int KT = (ND + GL - 1) / GL;  // terms per lane
+    struct Pack {
+        unsigned long long dx[KT > 0 ? KT : 1], dy[KT > 0 ? KT : 1];
+    };
+    static constexpr Pack pack() {
+        Pack p{};
+        int q = 0;
+        for (int dy = -R; dy <= R; ++dy)
+            for (int dx = -R; dx <= R; ++dx)
+                if ((dx * dx + dy * dy <= R * R) && (dx || dy)) {
+                    p.dx[q / GL] |= (unsigned long long)(dx + R) << (4 * (q % GL));
+                    p.dy[q / GL] |= (unsigned long long)(dy + R) << (4 * (q % GL));
+                    ++q;
+                }
+        return p;
+    }
+    static constexpr Pack PK = pack();
     struct Lds {
         float v[NC * NC];  // value at this child's fill (current for available cells, the input else)
         float t[NC * NC];  // T (unavailable cells and the padding: 1e6)
@@ -511,7 +530,8 @@ template <int RW>
 using WinLds = typename Win<RW == 0 ? 2 : RW>::Lds;
 
 template <int RW>
-__device__ __forceinline__ void fill_child(const Args &a, const Mode &m, int i, int c, float &tc, bool &tagged, WinLds<RW> &L) {
+__device__ __forceinline__ void fill_child(const Args &a, const Mode &m, int i, int c, float &tc, bool &tagged, WinLds<RW> &L,
+                                           const float *dstl) {
     using WN = Win<RW>;
     constexpr int NC = WN::NC, R = WN::R, ND = WN::ND, GL = WN::GL;
     const int j = (int)(threadIdx.x & (GL - 1));
@@ -649,50 +669,41 @@ __device__ __forceinline__ void fill_child(const Args &a, const Mode &m, int i, 
     const float gtx = fr ? (fl ? (tr - tl) * 0.5f : tr - tp) : (fl ? tp - tl : 0.0f);
     const float gty = fd ? (fu ? (td - tu) * 0.5f : td - tp) : (fu ? tp - tu : 0.0f);
 
-    // this lane's disc row: the terms of its cells, zero where a cell does not count (adding an exact
-    // zero leaves every sum's bits unchanged: none of them can be -0)
-    if (dy >= -R && dy <= R) {
-        const int cy = qy;
-        const bool yin = cy >= 0 && cy < H;
-        // OpenCV's rows km (the cell's, one inwards in the first image row), kp + 1 (below), km - 1
-        // (above), kp (the cell's, one inwards in the last row), as window rows; likewise columns
-        auto wrow = [&](int r) { return (r < 0 ? 0 : (r > H - 1 ? H - 1 : r)) - y + RW; };
-        auto wcol = [&](int q) { return (q < 0 ? 0 : (q > W - 1 ? W - 1 : q)) - x + RW; };
-        const int rA = wrow(cy + (cy == 0)), rD = wrow(cy + 1 - (cy == H - 1)), rU = wrow(cy - 1 + (cy == 0)),
-                  rB = wrow(cy - (cy == H - 1));
-        // slot of this row's first disc cell: the disc cells of the rows above (centre skipped)
-        int hw = 0;
-        while ((hw + 1) * (hw + 1) + dy * dy <= R * R) ++hw;
-        int rowbase = 0;
-        for (int yy = -R; yy < dy; ++yy) {
-            int h = 0;
-            while ((h + 1) * (h + 1) + yy * yy <= R * R) ++h;
-            rowbase += 2 * h + 1 - (yy == 0);
-        }
-        const int wy = j;
+    // this lane's terms (slots lane + GL k), zero where a cell does not count (adding an exact zero
+    // leaves every sum's bits unchanged: none of them can be -0).  Every window read of a term is
+    // issued before its arithmetic: the rows and columns stay inside the window for any cell.
+    // OpenCV's rows km (the cell's, one inwards in the first image row), kp + 1 (below), km - 1 (above),
+    // kp (the cell's, one inwards in the last row), as window rows; likewise columns.
+    auto wrow = [&](int r) { return (r < 0 ? 0 : (r > H - 1 ? H - 1 : r)) - y + RW; };
+    auto wcol = [&](int q) { return (q < 0 ? 0 : (q > W - 1 ? W - 1 : q)) - x + RW; };
 #pragma unroll 1
-        for (int dx = -R; dx <= R; ++dx) {
-            if (dx * dx + dy * dy > R * R || (dx == 0 && dy == 0)) continue;
-            const int cx = x + dx;
-            const int wx = dx + RW;
+    for (int k = 0; k < WN::KT; ++k) {
+        const int q = j + GL * k;
+        if (q < ND) {
+            const int dx = (int)((WN::PK.dx[k] >> (4 * j)) & 15u) - R, dy = (int)((WN::PK.dy[k] >> (4 * j)) & 15u) - R;
+            const int cy = y + dy, cx = x + dx, wy = dy + RW, wx = dx + RW;
+            const int rA = wrow(cy + (cy == 0)), rD = wrow(cy + 1 - (cy == H - 1)), rU = wrow(cy - 1 + (cy == 0)),
+                      rB = wrow(cy - (cy == H - 1));
+            const int cA = wcol(cx + (cx == 0)), cR = wcol(cx + 1 - (cx == W - 1)), cL = wcol(cx - 1 + (cx == 0)),
+                      cB = wcol(cx - (cx == W - 1));
+            const uint32_t avr = L.av[wy], avu = L.av[wy - 1], avd = L.av[wy + 1];
+            const float tcell = TT(wy, wx), dst = dstl[dx * dx + dy * dy];
+            const float vAR = VV(rA, cR), vAL = VV(rA, cL), vAA = VV(rA, cA), vAB = VV(rA, cB);
+            const float vDA = VV(rD, cA), vUA = VV(rU, cA), vBA = VV(rB, cA);
             float4 term = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-            if (yin && cx >= 0 && cx < W && AV(wy, wx)) {
-                const int cA = wcol(cx + (cx == 0)), cR = wcol(cx + 1 - (cx == W - 1)), cL = wcol(cx - 1 + (cx == 0)),
-                          cB = wcol(cx - (cx == W - 1));
+            if (cy >= 0 && cy < H && cx >= 0 && cx < W && ((avr >> wx) & 1u)) {
                 const float ry = (float)(-dy), rx = (float)(-dx);
-                const float dst = kDst[dx * dx + dy * dy];
-                const float lev = (float)(1.0 / (1.0 + __builtin_fabs((double)(TT(wy, wx) - tp))));
+                const float lev = (float)(1.0 / (1.0 + __builtin_fabs((double)(tcell - tp))));
                 float dir = rx * gtx + ry * gty;
                 if (__builtin_fabs((double)dir) <= 0.01) dir = 0.000001f;
                 const float w = __builtin_fabsf(dst * lev * dir);
-                const bool ar = AV(wy, wx + 1), al = AV(wy, wx - 1), ad = AV(wy + 1, wx), au = AV(wy - 1, wx);
-                const float gix = ar ? (al ? (VV(rA, cR) - VV(rA, cL)) * 2.0f : VV(rA, cR) - VV(rA, cA))
-                                     : (al ? VV(rA, cB) - VV(rA, cL) : 0.0f);
-                const float giy = ad ? (au ? (VV(rD, cA) - VV(rU, cA)) * 2.0f : VV(rD, cA) - VV(rA, cA))
-                                     : (au ? VV(rB, cA) - VV(rU, cA) : 0.0f);
-                term = make_float4(w * VV(rA, cA), w * (gix * rx), w * (giy * ry), w);
+                const bool ar = (avr >> (wx + 1)) & 1u, al = (avr >> (wx - 1)) & 1u, ad = (avd >> wx) & 1u,
+                           au = (avu >> wx) & 1u;
+                const float gix = ar ? (al ? (vAR - vAL) * 2.0f : vAR - vAA) : (al ? vAB - vAL : 0.0f);
+                const float giy = ad ? (au ? (vDA - vUA) * 2.0f : vDA - vAA) : (au ? vBA - vUA : 0.0f);
+                term = make_float4(w * vAA, w * (gix * rx), w * (giy * ry), w);
             }
-            L.term[rowbase + dx + hw - (dy == 0 && dx > 0)] = term;
+            L.term[q] = term;
         }
     }
     wave_lds_sync();
@@ -1082,13 +1093,18 @@ __device__ __forceinline__ void do_sweep(const Args &a, const Mode &m, unsigned 
     } else if constexpr (RW > 0) {
         constexpr int kPer = Win<RW>::PER;
         const int g = (int)threadIdx.x / Win<RW>::GL;
+        // OpenCV's distance weights by |r|^2, in LDS (read with the window: a constant-table read in
+        // the term loop is a memory round trip per term)
+        __shared__ float dstl[40];
+        if (threadIdx.x < 37) dstl[threadIdx.x] = kDst[threadIdx.x];
+        __syncthreads();
         // one child per group and block round, so a block's tagged children take one pass
         for (int base = blk * kPer; base < m.nIn; base += nblk * kPer) {  // block-uniform
             const int i = base + g;
             const int c = i < m.nIn ? Cl[i] : 0;
             if (i < m.nIn && (m.full || qin[c] == want)) {  // group-uniform
                 float t;
-                fill_child<RW>(a, m, i, c, t, tagged, lds[g]);
+                fill_child<RW>(a, m, i, c, t, tagged, lds[g], dstl);
                 const unsigned long long tb = dbits((double)t);
                 mn = tb < mn ? tb : mn;
             }
