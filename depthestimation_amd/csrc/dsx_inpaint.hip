@@ -97,7 +97,8 @@ struct Args {
     unsigned *pk, *rank, *par;   // push key and pop rank of pops; parent * 4 + direction of filled pixels
     unsigned long long *queued;  // [sweep & 1][pixel]: (bucket ordinal << 32 | sweep) it was tagged for
     unsigned long long *sk;   // this bucket's pop keys (T, push key), sorted per chunk of kRankChunk
-    uint16_t *lessm;          // [list position][window row]: cells that are children filled earlier
+    uint32_t *lessm;          // [list position][window row]: available cells | later children << 16 (the
+                              // ring march: the neighbours filled earlier)
     int *F[2], *C[2], *P;     // frontier, children (ping-pong), this bucket's pops
     uint8_t *cls, *rowd;      // pixel class; a hole within `radius` along the row
     int64_t n;
@@ -452,7 +453,7 @@ __device__ __forceinline__ void ring_child(const Args &a, const Mode &m, int i, 
 #pragma unroll
         for (int d = 0; d < 4; ++d)
             if ((intra >> d) & 1u) less |= (uint32_t)(a.key[nbp[d]] < me) << d;
-        a.lessm[(int64_t)i * kG] = (uint16_t)less;
+        a.lessm[(int64_t)i * kG] = less;
     }
     const float Told = a.T[c];
     tc = Told;
@@ -557,42 +558,70 @@ __device__ __forceinline__ void fill_child(const Args &a, const Mode &m, int i, 
         me = a.key[c];
     }
     const float Told = a.T[c], vold = a.out[c];
-    uint32_t less = sweep >= 2 && rowv ? a.lessm[(int64_t)i * kG + j] : 0u;
-
-    // the row's cells: fill bucket, T, current value, input value; all loads in flight
-    int fq[NC];
-    float tq[NC], vq[NC], oq[NC];
+    // a window cell's availability (known, or a child filled earlier) and whether it is a later child
+    // (a dependant) are fixed once sweep 1 has the fill keys: sweep 1 stores them per window row
+    // (avail | dependants << 16), and the later sweeps load only what a row stages - T where a cell is
+    // available, its current value there and its input value elsewhere - without the fill buckets
+    const bool cached = sweep >= 2;
+    uint32_t less = 0, avail = 0, dep = 0;
+    float vst[NC], tst[NC];
     uint32_t inw = 0;
 #pragma unroll
-    for (int cc = 0; cc < NC; ++cc) {
-        const int qx = x + cc - RW;
-        const bool ok = rowin && qx >= 0 && qx < W;
-        const int qxc = qx < 0 ? 0 : (qx >= W ? W - 1 : qx);
-        fq[cc] = a.fb[rowq + qxc];
-        tq[cc] = a.T[rowq + qxc];
-        vq[cc] = a.out[rowq + qxc];
-        oq[cc] = inrow[qxc];
-        inw |= (uint32_t)ok << cc;
-    }
-    const uint32_t self = j == RW ? 1u << RW : 0u;
-    uint32_t intra = 0;
+    for (int cc = 0; cc < NC; ++cc) inw |= (uint32_t)(rowin && x + cc - RW >= 0 && x + cc - RW < W) << cc;
+    if (cached) {
+        const uint32_t wd = rowv ? a.lessm[(int64_t)i * kG + j] : 0u;
+        avail = wd & 0xFFFFu;
+        dep = wd >> 16;
 #pragma unroll
-    for (int cc = 0; cc < NC; ++cc) intra |= (uint32_t)(((inw >> cc) & 1u) && fq[cc] == b) << cc;
-    intra &= ~self;
-    if (sweep == 1) {
-        unsigned long long kq[NC];
+        for (int cc = 0; cc < NC; ++cc) {
+            const int qx = x + cc - RW;
+            const int qxc = qx < 0 ? 0 : (qx >= W ? W - 1 : qx);
+            const bool av = (avail >> cc) & 1u;
+            vst[cc] = *(av ? a.out + rowq + qxc : inrow + qxc);
+            tst[cc] = ((inw >> cc) & 1u) && av ? a.T[rowq + qxc] : kFar;
+        }
+    } else {
+        // the row's cells: fill bucket, T, current value, input value; all loads in flight
+        int fq[NC];
+        float tq[NC], vq[NC], oq[NC];
 #pragma unroll
-        for (int cc = 0; cc < NC; ++cc) kq[cc] = ((intra >> cc) & 1u) ? a.key[rowq + x + cc - RW] : ~0ull;
+        for (int cc = 0; cc < NC; ++cc) {
+            const int qx = x + cc - RW;
+            const int qxc = qx < 0 ? 0 : (qx >= W ? W - 1 : qx);
+            fq[cc] = a.fb[rowq + qxc];
+            tq[cc] = a.T[rowq + qxc];
+            vq[cc] = a.out[rowq + qxc];
+            oq[cc] = inrow[qxc];
+        }
+        const uint32_t self = j == RW ? 1u << RW : 0u;
+        uint32_t intra = 0;
 #pragma unroll
-        for (int cc = 0; cc < NC; ++cc)
-            if (((intra >> cc) & 1u) && kq[cc] < me) less |= 1u << cc;
-        if (rowv) a.lessm[(int64_t)i * kG + j] = (uint16_t)less;
+        for (int cc = 0; cc < NC; ++cc) intra |= (uint32_t)(((inw >> cc) & 1u) && fq[cc] == b) << cc;
+        intra &= ~self;
+        if (sweep == 1) {
+            unsigned long long kq[NC];
+#pragma unroll
+            for (int cc = 0; cc < NC; ++cc) kq[cc] = ((intra >> cc) & 1u) ? a.key[rowq + x + cc - RW] : ~0ull;
+#pragma unroll
+            for (int cc = 0; cc < NC; ++cc)
+                if (((intra >> cc) & 1u) && kq[cc] < me) less |= 1u << cc;
+        }
+#pragma unroll
+        for (int cc = 0; cc < NC; ++cc) {
+            const bool in = (inw >> cc) & 1u;
+            const bool av = !in || fq[cc] < b || (fq[cc] == b && ((less >> cc) & 1u));
+            avail |= (uint32_t)av << cc;
+            vst[cc] = av ? vq[cc] : oq[cc];
+            tst[cc] = in && av ? tq[cc] : kFar;
+        }
+        dep = intra & ~less;
+        if (sweep == 1 && rowv) a.lessm[(int64_t)i * kG + j] = avail | dep << 16;
     }
     // the last window row when it has no lane of its own (radius 3): only its centre columns count -
     // the cell below the disc's bottom cell is read (and its right neighbour at the image's left edge),
     // and the child one column left reads this one at the left edge.  Every lane of the group loads
     // the same three cells; lane 0 stages them now (the group's previous child is done with the LDS).
-    uint32_t intra2 = 0, less2 = 0;
+    uint32_t less2 = 0, dep2 = 0;
     int64_t rowq2 = 0;
     if constexpr (WN::XR) {
         constexpr int jr = NC - 1;
@@ -600,39 +629,59 @@ __device__ __forceinline__ void fill_child(const Args &a, const Mode &m, int i, 
         const int qyc2 = rin2 ? y + RW : y;
         rowq2 = (int64_t)qyc2 * W;
         const float *inrow2 = a.in + (int64_t)qyc2 * a.pitch;
-        less2 = sweep >= 2 ? a.lessm[(int64_t)i * kG + jr] : 0u;
-        int f3[3];
-        float t3[3], v3[3], o3[3];
-        uint32_t inw2 = 0;
+        uint32_t inw2 = 0, avail2 = 0;
 #pragma unroll
-        for (int k = 0; k < 3; ++k) {
-            const int qx = x + k - 1;
-            const bool ok = rin2 && qx >= 0 && qx < W;
-            const int qxc = qx < 0 ? 0 : (qx >= W ? W - 1 : qx);
-            f3[k] = a.fb[rowq2 + qxc];
-            t3[k] = a.T[rowq2 + qxc];
-            v3[k] = a.out[rowq2 + qxc];
-            o3[k] = inrow2[qxc];
-            inw2 |= (uint32_t)ok << (RW - 1 + k);
-        }
-#pragma unroll
-        for (int k = 0; k < 3; ++k) intra2 |= (uint32_t)(((inw2 >> (RW - 1 + k)) & 1u) && f3[k] == b) << (RW - 1 + k);
-        if (sweep == 1) {
-#pragma unroll
-            for (int k = 0; k < 3; ++k)
-                if (((intra2 >> (RW - 1 + k)) & 1u) && a.key[rowq2 + x + k - 1] < me) less2 |= 1u << (RW - 1 + k);
-            if (j == 0) a.lessm[(int64_t)i * kG + jr] = (uint16_t)less2;
-        }
-        if (j == 0) {
-            uint32_t avail2 = 0;  // the other columns are never read
+        for (int k = 0; k < 3; ++k) inw2 |= (uint32_t)(rin2 && x + k - 1 >= 0 && x + k - 1 < W) << (RW - 1 + k);
+        float v3[3], t3[3];
+        if (cached) {
+            const uint32_t wd = a.lessm[(int64_t)i * kG + jr];
+            avail2 = wd & 0xFFFFu;
+            dep2 = wd >> 16;
 #pragma unroll
             for (int k = 0; k < 3; ++k) {
+                const int qx = x + k - 1;
+                const int qxc = qx < 0 ? 0 : (qx >= W ? W - 1 : qx);
+                const bool av = (avail2 >> (RW - 1 + k)) & 1u;
+                v3[k] = *(av ? a.out + rowq2 + qxc : inrow2 + qxc);
+                t3[k] = ((inw2 >> (RW - 1 + k)) & 1u) && av ? a.T[rowq2 + qxc] : kFar;
+            }
+        } else {
+            int f3[3];
+            float tq3[3], vq3[3], oq3[3];
+#pragma unroll
+            for (int k = 0; k < 3; ++k) {
+                const int qx = x + k - 1;
+                const int qxc = qx < 0 ? 0 : (qx >= W ? W - 1 : qx);
+                f3[k] = a.fb[rowq2 + qxc];
+                tq3[k] = a.T[rowq2 + qxc];
+                vq3[k] = a.out[rowq2 + qxc];
+                oq3[k] = inrow2[qxc];
+            }
+            uint32_t intra2 = 0;
+#pragma unroll
+            for (int k = 0; k < 3; ++k) intra2 |= (uint32_t)(((inw2 >> (RW - 1 + k)) & 1u) && f3[k] == b) << (RW - 1 + k);
+            if (sweep == 1) {
+#pragma unroll
+                for (int k = 0; k < 3; ++k)
+                    if (((intra2 >> (RW - 1 + k)) & 1u) && a.key[rowq2 + x + k - 1] < me) less2 |= 1u << (RW - 1 + k);
+            }
+#pragma unroll
+            for (int k = 0; k < 3; ++k) {  // the other columns are never read
                 const int cc = RW - 1 + k;
                 const bool in = (inw2 >> cc) & 1u;
                 const bool av = !in || f3[k] < b || (f3[k] == b && ((less2 >> cc) & 1u));
                 avail2 |= (uint32_t)av << cc;
-                L.v[jr * NC + cc] = av ? v3[k] : o3[k];
-                L.t[jr * NC + cc] = in && av ? t3[k] : kFar;
+                v3[k] = av ? vq3[k] : oq3[k];
+                t3[k] = in && av ? tq3[k] : kFar;
+            }
+            dep2 = intra2 & ~less2;
+            if (sweep == 1 && j == 0) a.lessm[(int64_t)i * kG + jr] = avail2 | dep2 << 16;
+        }
+        if (j == 0) {
+#pragma unroll
+            for (int k = 0; k < 3; ++k) {
+                L.v[jr * NC + RW - 1 + k] = v3[k];
+                L.t[jr * NC + RW - 1 + k] = t3[k];
             }
             L.av[jr] = (uint16_t)avail2;
         }
@@ -645,18 +694,14 @@ __device__ __forceinline__ void fill_child(const Args &a, const Mode &m, int i, 
         if (!any) return;
     }
     // stage the window: availability (the padding is known), the value at this fill, T
-    uint32_t avail = 0;
+    if (rowv) {
 #pragma unroll
-    for (int cc = 0; cc < NC; ++cc) {
-        const bool in = (inw >> cc) & 1u;
-        const bool av = !in || fq[cc] < b || (fq[cc] == b && ((less >> cc) & 1u));
-        avail |= (uint32_t)av << cc;
-        if (rowv) {
-            L.v[j * NC + cc] = av ? vq[cc] : oq[cc];
-            L.t[j * NC + cc] = in && av ? tq[cc] : kFar;
+        for (int cc = 0; cc < NC; ++cc) {
+            L.v[j * NC + cc] = vst[cc];
+            L.t[j * NC + cc] = tst[cc];
         }
+        L.av[j] = (uint16_t)avail;
     }
-    if (rowv) L.av[j] = (uint16_t)avail;
     wave_lds_sync();
 
     // T and grad T from the 4-neighbours (every lane: broadcast reads)
@@ -730,13 +775,11 @@ __device__ __forceinline__ void fill_child(const Args &a, const Mode &m, int i, 
     }
     if (sweep == 0) return;  // sweep 1 visits every child anyway
     // the children that read this one (this bucket's, filled later) are tagged for the next sweep
-    const uint32_t dep = intra & ~less;
     const unsigned long long tag = (unsigned long long)m.nb << 32 | (unsigned)(sweep + 1);
     unsigned long long *qn = a.queued + ((sweep + 1) & 1) * a.n;
 #pragma unroll
     for (int cc = 0; cc < NC; ++cc)
         if ((dep >> cc) & 1u) qn[rowq + x + cc - RW] = tag;
-    const uint32_t dep2 = intra2 & ~less2;
     if (WN::XR && j == 0) {
 #pragma unroll
         for (int cc = RW - 1; cc <= RW + 1; ++cc)
@@ -1362,8 +1405,8 @@ Args views(void *ws, int H, int W) {
     w += align256(2 * n * 8);
     a.sk = reinterpret_cast<unsigned long long *>(w);
     w += align256(n * 8);
-    a.lessm = reinterpret_cast<uint16_t *>(w);
-    w += align256(n * 2 * (size_t)kG);
+    a.lessm = reinterpret_cast<uint32_t *>(w);
+    w += align256(n * 4 * (size_t)kG);
     for (int i = 0; i < 2; ++i) {
         a.F[i] = reinterpret_cast<int *>(w);
         w += align256(n * 4);
@@ -1512,7 +1555,7 @@ hipError_t run_march(Args a, int ncu, int *hw, const InpaintOpts &o, hipStream_t
 size_t inpaint_workspace(int H, int W) {
     const size_t n = (size_t)H * W;
     return align256(sizeof(Ctl)) + 6 * align256(n * 4) + 2 * align256(n * 8) + align256(2 * n * 8) +
-           align256(n * 2 * (size_t)kG) + 4 * align256(n * 4) + 2 * align256(n);
+           align256(n * 4 * (size_t)kG) + 4 * align256(n * 4) + 2 * align256(n);
 }
 
 hipError_t launch_inpaint(const float *in, int64_t pitch, int H, int W, int radius, float *out, void *ws, hipStream_t st,
