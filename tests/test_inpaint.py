@@ -195,6 +195,38 @@ def test_fill_holes_device_edge_cases():
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("radius", [2, 3, 4])
+@pytest.mark.parametrize("where", ["left", "left1", "right", "top", "bottom", "corners"])
+def test_fill_holes_device_border_strips(where, radius):
+    """Holes against each image edge: the window's clamped rows / columns (OpenCV's one-inwards
+    gradient rows at the first and last image row and column), and at radius 3 the last window row,
+    which a child's lane group stages only at its centre columns."""
+    import torch
+    from depthestimation_amd.matcher import fill_holes_device
+    yy, xx = np.mgrid[0:36, 0:44]
+    d = (3 + 0.25 * xx + 0.15 * yy + 0.5 * np.sin(0.7 * xx * yy)).astype(np.float32)
+    if where == "left":
+        d[4:30, 0:3] = 0
+    elif where == "left1":
+        d[5:31, 1:4] = 0
+        d[12, 0] = 0
+    elif where == "right":
+        d[3:33, -3:] = 0
+    elif where == "top":
+        d[0:3, 5:40] = 0
+    elif where == "bottom":
+        d[-4:, 2:42] = 0
+        d[-1, 0] = 0
+    else:
+        d[:5, :5] = 0
+        d[-5:, -5:] = 0
+        d[:4, -6:] = 0
+        d[-6:, :4] = 0
+    got = fill_holes_device(torch.from_numpy(d).cuda(), radius=radius).cpu().numpy()
+    np.testing.assert_array_equal(_bits(got), _bits(telea_heap(d, d <= 0, radius)))
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("case", ["island", "center", "square", "disc", "diagonal", "grid", "corner"])
 def test_fill_holes_device_symmetric_and_island(case):
     """Equal arrival times everywhere (the push order decides who sees whom), and ADVICE r5's island."""
