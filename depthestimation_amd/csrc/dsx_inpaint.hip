@@ -63,6 +63,11 @@ constexpr int kG = 16;               // lessm words per child (one per window ro
 constexpr int kRankChunk = 1024;     // pop keys sorted per block (registers) for the ranks
 constexpr int kRankBatch = 8;        // sorted chunks one rank task counts against (through LDS)
 constexpr int kInitPT = 8;           // pixels per thread of tl_init_b
+// CHASE (an inward sweep after a sweep in which at most kChaseTags children tagged later ones): block 0
+// alone runs the following sweeps back to back, its frontier in LDS (at most kChaseCap children, deduped
+// by a kChaseHash-slot table), up to kChaseSweeps of them, with a block barrier between sweeps instead
+// of a launch
+constexpr int kChaseTags = 2, kChaseCap = 192, kChaseHash = 256, kChaseSweeps = 64;
 
 enum Phase : int { kPhInit = 0, kPhPop = 1, kPhSweep = 2, kPhDone = 3, kPhSwitch = 4 };
 enum : uint8_t { kClsOther = 0, kClsHole = 1, kClsBand = 2, kClsRing = 3 };
@@ -279,6 +284,7 @@ struct Mode {
     int nPrev;  // POP: the last bucket's children
     int nP, base, rank_on;
     bool full;  // sweep over the bucket's whole list, else over the tagged children
+    bool chase;  // block 0 runs the sweeps from this one on by itself (CHASE)
     double bound;
 };
 
@@ -293,7 +299,8 @@ __device__ __forceinline__ unsigned long long wave_min_u64(unsigned long long v)
 // The step's mode from the slot the previous step wrote (every block computes the same).  mcv: this
 // lane's word of the bucket minima, minC[lane / 16][lane % 16] (lanes < 48), loaded with the slot.
 template <int RW>
-__device__ __forceinline__ Mode decide(const State &S, unsigned long long mcv, bool tagged) {
+__device__ __forceinline__ Mode decide(const State &S, unsigned long long mcv, unsigned ntag) {
+    const bool tagged = ntag != 0;
     Mode m{};
     m.k = S.k;
     m.b = S.b;
@@ -326,6 +333,7 @@ __device__ __forceinline__ Mode decide(const State &S, unsigned long long mcv, b
         m.what = kPhSweep;
         m.sweep = S.sweep + 1;
         m.full = RW == 0 || m.sweep == 1;
+        m.chase = RW > 0 && S.march == 1 && m.sweep >= 2 && ntag <= (unsigned)kChaseTags;
         m.nIn = S.nC;
         return m;
     }
@@ -446,14 +454,14 @@ __device__ __forceinline__ void ring_child(const Args &a, const Mode &m, int i, 
         fq[d] = a.fb[q];
         tq[d] = a.T[q];
     }
-    uint32_t less = sweep >= 2 ? a.lessm[(int64_t)i * kG] : 0u, intra = 0;
+    uint32_t less = sweep >= 2 ? a.lessm[(int64_t)c * kG] : 0u, intra = 0;
 #pragma unroll
     for (int d = 0; d < 4; ++d) intra |= (uint32_t)(nbp[d] >= 0 && fq[d] == b) << d;
     if (sweep == 1) {
 #pragma unroll
         for (int d = 0; d < 4; ++d)
             if ((intra >> d) & 1u) less |= (uint32_t)(a.key[nbp[d]] < me) << d;
-        a.lessm[(int64_t)i * kG] = less;
+        a.lessm[(int64_t)c * kG] = less;
     }
     const float Told = a.T[c];
     tc = Told;
@@ -484,6 +492,28 @@ __device__ __forceinline__ void ring_child(const Args &a, const Mode &m, int i, 
 __constant__ float kDst[37] = {0.0f, 0x1.0000000000000p+0f, 0x1.6a09e60000000p-2f, 0x1.8a23460000000p-3f, 0x1.0000000000000p-3f, 0x1.6e5b7e0000000p-4f, 0x1.16b2900000000p-4f, 0x1.ba53900000000p-5f, 0x1.6a09e60000000p-5f, 0x1.2f684c0000000p-5f, 0x1.030dc40000000p-5f, 0x1.c116620000000p-6f, 0x1.8a23460000000p-6f, 0x1.5d8be40000000p-6f, 0x1.38c5a20000000p-6f, 0x1.1a05a40000000p-6f, 0x1.0000000000000p-6f, 0x1.d37e9a0000000p-7f, 0x1.ad15360000000p-7f, 0x1.8ba85a0000000p-7f, 0x1.6e5b7e0000000p-7f, 0x1.5480c80000000p-7f, 0x1.3d8d820000000p-7f, 0x1.2911d00000000p-7f, 0x1.16b2900000000p-7f, 0x1.0624de0000000p-7f, 0x1.ee55560000000p-8f, 0x1.d320520000000p-8f, 0x1.ba53900000000p-8f, 0x1.a3a5560000000p-8f, 0x1.8ed6e20000000p-8f, 0x1.7bb27c0000000p-8f, 0x1.6a09e60000000p-8f, 0x1.59b52a0000000p-8f, 0x1.4a918e0000000p-8f, 0x1.3c80c60000000p-8f, 0x1.2f684c0000000p-8f};
 
 // ---- the inward march: Telea's value, Win::GL lanes per child (lane j = window row j - RW) ----
+
+// CHASE's frontier: this sweep's children and the next one's (deduped as they are tagged)
+struct ChaseBuf {
+    int list[2][kChaseCap];
+    int hkey[kChaseHash];
+    int n[2];
+};
+__device__ __forceinline__ void chase_push(ChaseBuf &cb, int nxt, int p) {
+    unsigned h = ((unsigned)p * 2654435761u) >> 24;  // kChaseHash = 256 slots
+#pragma unroll 1
+    for (int probe = 0; probe < kChaseHash; ++probe) {
+        const int old = atomicCAS(&cb.hkey[h], -1, p);
+        if (old == -1) {
+            const int q = atomicAdd(&cb.n[nxt], 1);
+            if (q < kChaseCap) cb.list[nxt][q] = p;
+            return;
+        }
+        if (old == p) return;
+        h = (h + 1) & (kChaseHash - 1);
+    }
+    atomicAdd(&cb.n[nxt], kChaseCap + 1);  // the table is full: the frontier overflows
+}
 
 template <int RW>
 struct Win {
@@ -531,8 +561,8 @@ template <int RW>
 using WinLds = typename Win<RW == 0 ? 2 : RW>::Lds;
 
 template <int RW>
-__device__ __forceinline__ void fill_child(const Args &a, const Mode &m, int i, int c, float &tc, bool &tagged, WinLds<RW> &L,
-                                           const float *dstl) {
+__device__ __forceinline__ void fill_child(const Args &a, const Mode &m, int c, float &tc, bool &tagged, WinLds<RW> &L,
+                                           const float *dstl, ChaseBuf *cb, int nxt) {
     using WN = Win<RW>;
     constexpr int NC = WN::NC, R = WN::R, ND = WN::ND, GL = WN::GL;
     const int j = (int)(threadIdx.x & (GL - 1));
@@ -569,7 +599,7 @@ __device__ __forceinline__ void fill_child(const Args &a, const Mode &m, int i, 
 #pragma unroll
     for (int cc = 0; cc < NC; ++cc) inw |= (uint32_t)(rowin && x + cc - RW >= 0 && x + cc - RW < W) << cc;
     if (cached) {
-        const uint32_t wd = rowv ? a.lessm[(int64_t)i * kG + j] : 0u;
+        const uint32_t wd = rowv ? a.lessm[(int64_t)c * kG + j] : 0u;
         avail = wd & 0xFFFFu;
         dep = wd >> 16;
 #pragma unroll
@@ -615,7 +645,7 @@ __device__ __forceinline__ void fill_child(const Args &a, const Mode &m, int i, 
             tst[cc] = in && av ? tq[cc] : kFar;
         }
         dep = intra & ~less;
-        if (sweep == 1 && rowv) a.lessm[(int64_t)i * kG + j] = avail | dep << 16;
+        if (sweep == 1 && rowv) a.lessm[(int64_t)c * kG + j] = avail | dep << 16;
     }
     // the last window row when it has no lane of its own (radius 3): only its centre columns count -
     // the cell below the disc's bottom cell is read (and its right neighbour at the image's left edge),
@@ -634,7 +664,7 @@ __device__ __forceinline__ void fill_child(const Args &a, const Mode &m, int i, 
         for (int k = 0; k < 3; ++k) inw2 |= (uint32_t)(rin2 && x + k - 1 >= 0 && x + k - 1 < W) << (RW - 1 + k);
         float v3[3], t3[3];
         if (cached) {
-            const uint32_t wd = a.lessm[(int64_t)i * kG + jr];
+            const uint32_t wd = a.lessm[(int64_t)c * kG + jr];
             avail2 = wd & 0xFFFFu;
             dep2 = wd >> 16;
 #pragma unroll
@@ -675,7 +705,7 @@ __device__ __forceinline__ void fill_child(const Args &a, const Mode &m, int i, 
                 t3[k] = in && av ? tq3[k] : kFar;
             }
             dep2 = intra2 & ~less2;
-            if (sweep == 1 && j == 0) a.lessm[(int64_t)i * kG + jr] = avail2 | dep2 << 16;
+            if (sweep == 1 && j == 0) a.lessm[(int64_t)c * kG + jr] = avail2 | dep2 << 16;
         }
         if (j == 0) {
 #pragma unroll
@@ -779,11 +809,17 @@ __device__ __forceinline__ void fill_child(const Args &a, const Mode &m, int i, 
     unsigned long long *qn = a.queued + ((sweep + 1) & 1) * a.n;
 #pragma unroll
     for (int cc = 0; cc < NC; ++cc)
-        if ((dep >> cc) & 1u) qn[rowq + x + cc - RW] = tag;
+        if ((dep >> cc) & 1u) {
+            qn[rowq + x + cc - RW] = tag;
+            if (cb) chase_push(*cb, nxt, (int)(rowq + x + cc - RW));
+        }
     if (WN::XR && j == 0) {
 #pragma unroll
         for (int cc = RW - 1; cc <= RW + 1; ++cc)
-            if ((dep2 >> cc) & 1u) qn[rowq2 + x + cc - RW] = tag;
+            if ((dep2 >> cc) & 1u) {
+                qn[rowq2 + x + cc - RW] = tag;
+                if (cb) chase_push(*cb, nxt, (int)(rowq2 + x + cc - RW));
+            }
     }
     int dany = dep != 0 || dep2 != 0;
 #pragma unroll
@@ -1103,7 +1139,7 @@ __device__ __forceinline__ void do_rank(const Args &a, const Mode &m, int blk, i
 // this sweep (a child's group checks its tag).  Sweep 1 also sorts the bucket's pop keys per chunk.
 template <int RW>
 __device__ __forceinline__ void do_sweep(const Args &a, const Mode &m, unsigned *tagw, int blk, int nblk, WinLds<RW> *lds,
-                         unsigned long long *sortbuf) {
+                         unsigned long long *sortbuf, State *N) {
     const int *Cl = a.C[m.lsel];
     unsigned long long mn = ~0ull;
     bool tagged = false;
@@ -1141,15 +1177,63 @@ __device__ __forceinline__ void do_sweep(const Args &a, const Mode &m, unsigned 
         __shared__ float dstl[40];
         if (threadIdx.x < 37) dstl[threadIdx.x] = kDst[threadIdx.x];
         __syncthreads();
-        // one child per group and block round, so a block's tagged children take one pass
-        for (int base = blk * kPer; base < m.nIn; base += nblk * kPer) {  // block-uniform
-            const int i = base + g;
-            const int c = i < m.nIn ? Cl[i] : 0;
-            if (i < m.nIn && (m.full || qin[c] == want)) {  // group-uniform
-                float t;
-                fill_child<RW>(a, m, i, c, t, tagged, lds[g], dstl);
-                const unsigned long long tb = dbits((double)t);
-                mn = tb < mn ? tb : mn;
+        if (m.chase) {
+            // CHASE: block 0 finds this sweep's children once, then runs sweep after sweep over its LDS
+            // frontier (each child it changes queues the later children it tags, as the global tags do)
+            __shared__ ChaseBuf cb;
+            if (blk == 0) {
+                const int tid = (int)threadIdx.x;
+                if (tid < kChaseHash) cb.hkey[tid] = -1;
+                if (tid == 0) cb.n[0] = cb.n[1] = 0;
+                __syncthreads();
+                for (int i = tid; i < m.nIn; i += 256)
+                    if (qin[Cl[i]] == want) chase_push(cb, 0, Cl[i]);
+                __syncthreads();
+                Mode mm = m;
+                int cur = 0, sw = m.sweep;
+                bool dummy = false;
+#pragma unroll 1
+                for (int r = 0; r < kChaseSweeps; ++r) {  // block-uniform
+                    const int n = cb.n[cur];
+                    if (n == 0 || n > kChaseCap) break;
+                    __syncthreads();  // everyone has read n before it is reset
+                    if (tid < kChaseHash) cb.hkey[tid] = -1;
+                    if (tid == 0) cb.n[cur ^ 1] = 0;
+                    __syncthreads();
+                    mm.sweep = sw;
+                    for (int q0 = 0; q0 < n; q0 += kPer) {
+                        const int q = q0 + g;
+                        if (q < n) {  // group-uniform
+                            float t;
+                            fill_child<RW>(a, mm, cb.list[cur][q], t, dummy, lds[g], dstl, &cb, cur ^ 1);
+                            const unsigned long long tb = dbits((double)t);
+                            mn = tb < mn ? tb : mn;
+                        }
+                    }
+                    __syncthreads();
+                    cur ^= 1;
+                    ++sw;
+                }
+                // sw: the sweep the remaining frontier is tagged for (its tags are set), or the one after
+                // the last when it is empty
+                if (tid == 0) {
+                    N->sweep = sw - 1;
+                    const int left = cb.n[cur];
+                    if (left) __hip_atomic_store(tagw, left > kChaseCap ? (unsigned)kChaseCap : (unsigned)left,
+                                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                }
+            }
+        } else {
+            // one child per group and block round, so a block's tagged children take one pass
+            for (int base = blk * kPer; base < m.nIn; base += nblk * kPer) {  // block-uniform
+                const int i = base + g;
+                const int c = i < m.nIn ? Cl[i] : 0;
+                if (i < m.nIn && (m.full || qin[c] == want)) {  // group-uniform
+                    float t;
+                    fill_child<RW>(a, m, c, t, tagged, lds[g], dstl, nullptr, 0);
+                    const unsigned long long tb = dbits((double)t);
+                    mn = tb < mn ? tb : mn;
+                }
             }
         }
     }
@@ -1161,8 +1245,12 @@ __device__ __forceinline__ void do_sweep(const Args &a, const Mode &m, unsigned 
         do_sort_chunks(a, m, blk, nblk, sortbuf);
     }
     if (m.sweep == 1 && m.rank_on && m.nP > 0) do_rank(a, m, blk, nblk, sortbuf);
-    if (__syncthreads_or(tagged) && threadIdx.x == 0)
-        __hip_atomic_store(tagw + blk % kMinSlots, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // the children that tagged later ones (a group counts once), summed per slot: CHASE follows a
+    // sweep with few of them
+    constexpr int kGL = RW > 0 ? Win<RW>::GL : 1;
+    const bool one = m.march == 0 || RW == 0 || (threadIdx.x & (kGL - 1)) == 0;
+    const int nt = __syncthreads_count(tagged && one);
+    if (nt && threadIdx.x == 0) atomicAdd(tagw + blk % kMinSlots, (unsigned)nt);
     // T of a child only falls over the sweeps (more neighbours filled before it), so the minimum of
     // every T computed in the bucket is the minimum of the final ones
     block_min_to(mn, &a.ctl->minC[m.nb % 3][blk % kMinSlots]);
@@ -1242,9 +1330,11 @@ __device__ __forceinline__ int step(const Args &a, unsigned s, int blk, int nblk
     const State S = ctl->st[s % 3];
     const int lane = threadIdx.x & 63;
     const unsigned long long mcv = lane < 3 * kMinSlots ? (&ctl->minC[0][0])[lane] : ~0ull;
-    const unsigned tg = lane < kMinSlots ? ctl->tagged[s % 3][lane] : 0u;
+    unsigned tg = lane < kMinSlots ? ctl->tagged[s % 3][lane] : 0u;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) tg += __shfl_xor(tg, o);
     State &N = ctl->st[(s + 1) % 3];
-    const Mode m = decide<RW>(S, mcv, __ballot(tg != 0u) != 0ull);
+    const Mode m = decide<RW>(S, mcv, tg);
     if (a.stamps && blk == 0 && threadIdx.x == 0 && s < a.nstamps) {
         unsigned long long *e = a.stamps + 8 * (size_t)s;
         e[0] = __builtin_amdgcn_s_memrealtime();
@@ -1299,7 +1389,7 @@ __device__ __forceinline__ int step(const Args &a, unsigned s, int blk, int nblk
         }
     }
     if (m.what == kPhPop) do_pop(a, m, N, blk, nblk);
-    else if (m.what == kPhSweep) do_sweep<RW>(a, m, ctl->tagged[(s + 1) % 3], blk, nblk, lds, sortbuf);
+    else if (m.what == kPhSweep) do_sweep<RW>(a, m, ctl->tagged[(s + 1) % 3], blk, nblk, lds, sortbuf, &N);
     else if (m.what == kPhSwitch) do_switch(a, N, blk, nblk);
     // diagnostics: when block 0 finished the step (only block 0 writes: per-block atomics on one word
     // cost about 20 us per 1,024-block step and hid the steps' own times)
