@@ -66,8 +66,9 @@ constexpr int kInitPT = 8;           // pixels per thread of tl_init_b
 // CHASE (an inward sweep after a sweep in which at most kChaseTags children tagged later ones): block 0
 // alone runs the following sweeps back to back, its frontier in LDS (at most kChaseCap children, deduped
 // by a kChaseHash-slot table), up to kChaseSweeps of them, with a block barrier between sweeps instead
-// of a launch
-constexpr int kChaseTags = 2, kChaseCap = 192, kChaseHash = 256, kChaseSweeps = 64;
+// of a launch; a frontier above kChaseRun children (two rounds of the block's lane groups) goes back to
+// the launched sweeps
+constexpr int kChaseTags = 32, kChaseCap = 192, kChaseHash = 256, kChaseSweeps = 64, kChaseRun = 64;
 
 enum Phase : int { kPhInit = 0, kPhPop = 1, kPhSweep = 2, kPhDone = 3, kPhSwitch = 4 };
 enum : uint8_t { kClsOther = 0, kClsHole = 1, kClsBand = 2, kClsRing = 3 };
@@ -1195,7 +1196,7 @@ __device__ __forceinline__ void do_sweep(const Args &a, const Mode &m, unsigned 
 #pragma unroll 1
                 for (int r = 0; r < kChaseSweeps; ++r) {  // block-uniform
                     const int n = cb.n[cur];
-                    if (n == 0 || n > kChaseCap) break;
+                    if (n == 0 || n > kChaseRun) break;
                     __syncthreads();  // everyone has read n before it is reset
                     if (tid < kChaseHash) cb.hkey[tid] = -1;
                     if (tid == 0) cb.n[cur ^ 1] = 0;
