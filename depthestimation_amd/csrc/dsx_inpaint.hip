@@ -103,7 +103,7 @@ struct Args {
     unsigned *pk, *rank, *par;   // push key and pop rank of pops; parent * 4 + direction of filled pixels
     unsigned long long *queued;  // [sweep & 1][pixel]: (bucket ordinal << 32 | sweep) it was tagged for
     unsigned long long *sk;   // this bucket's pop keys (T, push key), sorted per chunk of kRankChunk
-    uint32_t *lessm;          // [list position][window row]: available cells | later children << 16 (the
+    uint32_t *lessm;          // [pixel][window row]: available cells | later children << 16 (the
                               // ring march: the neighbours filled earlier)
     int *F[2], *C[2], *P;     // frontier, children (ping-pong), this bucket's pops
     uint8_t *cls, *rowd;      // pixel class; a hole within `radius` along the row
@@ -433,7 +433,7 @@ __device__ __forceinline__ unsigned parent_word(int c, int W, unsigned long long
 
 // ---- the outward march: T only, one thread per child ----
 
-__device__ __forceinline__ void ring_child(const Args &a, const Mode &m, int i, int c, float &tc, bool &tagged) {
+__device__ __forceinline__ void ring_child(const Args &a, const Mode &m, int c, float &tc, bool &tagged) {
     const int H = a.H, W = a.W, b = m.b, sweep = m.sweep;
     const int y = c / W, x = c - y * W;
     const int nbp[4] = {y > 0 ? c - W : -1, x > 0 ? c - 1 : -1, y < H - 1 ? c + W : -1, x < W - 1 ? c + 1 : -1};
@@ -1155,7 +1155,7 @@ __device__ __forceinline__ void do_sweep(const Args &a, const Mode &m, unsigned 
                 bool run = false;
                 if (m.march == 0) {
                     if (m.full || qin[c] == want) {
-                        ring_child(a, m, i, c, t, tagged);
+                        ring_child(a, m, c, t, tagged);
                         run = true;
                     }
                 } else {
