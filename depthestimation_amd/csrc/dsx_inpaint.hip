@@ -1146,8 +1146,17 @@ __device__ __forceinline__ void do_sweep(const Args &a, const Mode &m, unsigned 
     bool tagged = false;
     const unsigned long long want = (unsigned long long)m.nb << 32 | (unsigned)m.sweep;
     const unsigned long long *qin = a.queued + (m.sweep & 1) * a.n;
-    if (m.march == 0 || RW == 0) {
-        for (int base = blk * 256; base < m.nIn; base += nblk * 256) {  // block-uniform
+    // the pop keys' sort (sweep 0) or ranks (sweep 1) take blocks of their own when they need at most
+    // half the grid, so they run beside the sweep instead of after it in the same blocks
+    const int nch = (m.nP + kRankChunk - 1) / kRankChunk;
+    const int nwork = !m.rank_on || m.nP <= 0 ? 0
+                      : (m.sweep == 0 ? nch : (m.sweep == 1 ? nch * ((nch + kRankBatch - 1) / kRankBatch) : 0));
+    const bool split = nwork > 0 && 2 * nwork <= nblk;
+    const bool sorter = split && blk < nwork;  // block-uniform
+    const int sb = split ? blk - nwork : blk, snb = split ? nblk - nwork : nblk;
+    if (sorter) {
+    } else if (m.march == 0 || RW == 0) {
+        for (int base = sb * 256; base < m.nIn; base += snb * 256) {  // block-uniform
             const int i = base + (int)threadIdx.x;
             if (i < m.nIn) {
                 const int c = Cl[i];
@@ -1226,7 +1235,7 @@ __device__ __forceinline__ void do_sweep(const Args &a, const Mode &m, unsigned 
             }
         } else {
             // one child per group and block round, so a block's tagged children take one pass
-            for (int base = blk * kPer; base < m.nIn; base += nblk * kPer) {  // block-uniform
+            for (int base = sb * kPer; base < m.nIn; base += snb * kPer) {  // block-uniform
                 const int i = base + g;
                 const int c = i < m.nIn ? Cl[i] : 0;
                 if (i < m.nIn && (m.full || qin[c] == want)) {  // group-uniform
@@ -1241,11 +1250,11 @@ __device__ __forceinline__ void do_sweep(const Args &a, const Mode &m, unsigned 
     // the bucket's pop keys are final after its POP: sweep 0 sorts them per chunk, sweep 1 ranks them
     // (the next POP reads the ranks; no sweep does).  Round 6 ran the ranks as a step of their own
     // after sweep 1: C2 2.14 -> 2.08 ms, C4 65.6 -> 64.5 ms without it (profiles/r06_inpaint_lib_ab.txt).
-    if (m.sweep == 0 && m.rank_on && m.nP > 0) {
+    if (m.sweep == 0 && nwork > 0 && (sorter || !split)) {
         __syncthreads();  // the sort buffer aliases the lane groups' windows
-        do_sort_chunks(a, m, blk, nblk, sortbuf);
+        do_sort_chunks(a, m, blk, split ? nwork : nblk, sortbuf);
     }
-    if (m.sweep == 1 && m.rank_on && m.nP > 0) do_rank(a, m, blk, nblk, sortbuf);
+    if (m.sweep == 1 && nwork > 0 && (sorter || !split)) do_rank(a, m, blk, split ? nwork : nblk, sortbuf);
     // the children that tagged later ones (a group counts once), summed per slot: CHASE follows a
     // sweep with few of them
     constexpr int kGL = RW > 0 ? Win<RW>::GL : 1;
